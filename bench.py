@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""Benchmark of the pairwise-ranking training hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+
+Metric (BASELINE.json): BPR triplets/sec (d=64) + achieved HBM GB/s.
+Default workload = configs[1]: BPR-MF on a synthetic implicit-feedback graph,
+1,000,000 users x 100,000 items, 50M interactions (degree 1+Poisson(49),
+Zipf(0.8) item popularity), d=64, W=1, B=65,536 pairs per GPU per step.
+A step = one pass of the hot path over one batch, all on the GPU: device
+sampler (epoch bijection + negative rejection) -> gather -> loss ->
+gradient scatter -> duplicate-row sum -> Adagrad apply.  Inputs are resident
+in HBM before the timed region.
+
+N>1 (launched by torch.distributed.run, one rank per GPU): users are sharded
+by contiguous id ranges (each rank generates and samples its own shard), item
+rows are replicated; per step each rank runs the local phase, RCCL all-reduces
+the dense fp32 item gradient, and every replica applies the identical item
+Adagrad.  value = triplets of all ranks / max-over-ranks time ("weak").
+
+rank 0 prints ONE JSON line; diagnostics go to stderr.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # configs[1] of BASELINE.json
+    "cfg2": dict(model="bpr", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
+                 graph_seed=20261015, d=64, W=1, G=1, B=65536, reg=0.02, truncated=True,
+                 desc="BPR-MF synthetic 1M users x 100K items, d=64"),
+    # configs[2]: CML on the same graph
+    "cfg3": dict(model="cml", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
+                 graph_seed=20261015, d=128, W=5, G=1, B=65536, reg=0.0, truncated=False,
+                 margin=1.0, reg_cov=1.0, clip_norm=1.0,
+                 desc="CML synthetic 1M users x 100K items, d=128, W=5"),
+    # configs[4] shape, AMF phase 2 (adversarial) step
+    "cfg5": dict(model="amf", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
+                 graph_seed=20261015, d=128, W=5, G=1, B=65536, reg=0.05, truncated=True,
+                 reg_adv=1.0, desc="AMF synthetic 1M users x 100K items, d=128, W=5"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr)
+    sys.stderr.flush()
+
+
+def gather_bytes_per_pair(d, W, G=0, bias=False):
+    """algorithmic gather bytes per pair = (2+W)*4d + 4(2+W)
+    (fp32 rows of U_u, V_i, V_j plus their int32 ids); + G group rows (GBPR)."""
+    rows = 2 + W + G
+    return rows * 4 * d + 4 * rows + (4 * (1 + W) if bias else 0)
+
+
+def full_step_bytes_per_pair(d, W, G=0):
+    """per row occurrence read var, read acc, write var, write acc
+    (16d B) plus the ids: (2+W)*16d + 4(2+W)."""
+    rows = 2 + W + G
+    return rows * 16 * d + 4 * rows
+
+
+def load_pmc(workload, n_gpus):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+        r = rec.get(workload, {})
+        return r.get("step_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg, indptr, indices, budget_s=15.0):
+    """The C oracle (oracle/cf_oracle.c, single thread): the same sample +
+    step work unit on the same graph, timed on this host on a bounded sample."""
+    from oracle.build_oracle import COracle
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(1)
+    U = O.init_table(rng, (cfg["n_users"], cfg["d"]))
+    V = O.init_table(rng, (cfg["n_items"], cfg["d"]))
+    c = COracle(cfg["model"], U, V, W=cfg["W"], reg=cfg["reg"], margin=cfg.get("margin", 1.0),
+                reg_cov=cfg.get("reg_cov", 1.0), clip_norm=cfg.get("clip_norm", 1.0),
+                reg_adv=cfg.get("reg_adv", 1.0), max_batch=cfg["B"])
+    users = np.repeat(np.arange(len(indptr) - 1, dtype=np.int32), np.diff(indptr))
+    coo = np.stack([users, indices], axis=1)
+    del users
+    B = cfg["B"]
+    t0 = time.perf_counter()
+    c.train(indptr, indices, coo, B, 1, 12345)
+    one = time.perf_counter() - t0
+    n = max(1, int(budget_s / max(one, 1e-3)))
+    t0 = time.perf_counter()
+    c.train(indptr, indices, coo, B, n, 6789)
+    dt = time.perf_counter() - t0
+    trip = n * B * cfg["W"]
+    return {"value": trip / dt, "unit": "triplets/s", "cores": 1, "kind": "port",
+            "sample": "%d steps x %d pairs (W=%d) of %s: sample+forward+backward+dedup+Adagrad, "
+                      "oracle/cf_oracle.c single thread, %.1f s" % (n, B, cfg["W"], cfg["desc"], dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step (0 = config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["B"] = args.batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    torch = None
+    if world > 1:
+        import torch  # noqa: F811
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    # ---- inputs: this rank's user shard of the synthetic graph ----------------
+    nu_all, ni, d, W, B = cfg["n_users"], cfg["n_items"], cfg["d"], cfg["W"], cfg["B"]
+    u0, u1 = rank * nu_all // world, (rank + 1) * nu_all // world
+    t0 = time.perf_counter()
+    indptr, indices = synth_graph(nu_all, ni, cfg["mean_degree"], cfg["zipf"], cfg["graph_seed"],
+                                  u_begin=u0, u_end=u1, n_threads=min(16, os.cpu_count() or 1))
+    log("rank %d: users [%d,%d) nnz %d generated in %.1fs" % (rank, u0, u1, len(indices),
+                                                             time.perf_counter() - t0))
+    kw = dict(reg=cfg["reg"])
+    for k in ("margin", "reg_cov", "clip_norm", "reg_adv"):
+        if k in cfg:
+            kw[k] = cfg[k]
+    eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
+                 dense_item_apply=(world > 1), seed=1000 + rank, **kw)
+    eng.set_interactions(indptr, indices)
+    eng.init_params(0.0, 0.1, truncated=cfg["truncated"], seed=1)  # same V on every rank
+    if cfg["model"] == "amf":
+        eng.begin_phase(1)
+
+    if world > 1:
+        n_grad = ni * d + (ni if cfg["model"] == "gbpr" else 0)
+        gv = torch.zeros(n_grad, dtype=torch.float32, device="cuda:%d" % local_rank)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        eng.bind_item_grad(gv.data_ptr(), n_grad)
+
+        def run(k):
+            for _ in range(k):
+                eng.step_local(B)
+                dist.all_reduce(gv)
+                eng.step_items()
+
+        def sync():
+            torch.cuda.synchronize()
+            dist.barrier()
+    else:
+        def run(k):
+            eng.train_steps(B, k, return_loss=False)
+
+        def sync():
+            eng.synchronize()
+
+    run(args.warmup)
+    sync()
+    eng.profile_reset()
+    eng.profile(not args.no_profile)
+    sync()
+    t0 = time.perf_counter()
+    run(args.steps)
+    sync()
+    elapsed = time.perf_counter() - t0
+    eng.profile(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local_rank)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = eng.take_loss()
+    log("rank %d: loss accumulated %.4e over %d steps" % (rank, loss, args.warmup + args.steps))
+
+    kernels = {}
+    for kname in ("step", "apply", "apply_dense", "clip"):
+        ms, n = eng.profile_read(kname)
+        if n:
+            kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}
+    trip_per_step = B * W
+    total_trip = trip_per_step * args.steps * world
+    value = total_trip / elapsed
+    step_avg_s = kernels.get("step", {}).get("avg_us", float("nan")) * 1e-6
+    gb = gather_bytes_per_pair(d, W, cfg["G"] if cfg["model"] == "gbpr" else 0,
+                               bias=cfg["model"] == "gbpr") * B
+    achieved = gb / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
+    traffic = load_pmc(args.config, world)
+    roofline = {"kernel": "step_kernel (fused sample+gather+loss+scatter)", "bound": "hbm",
+                "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
+                "traffic": traffic,
+                "bytes_per_launch": gb,
+                "bytes_def": "SURVEY 8(d) gather bytes: B*((2+W)*4d + 4(2+W))"}
+    full_b = full_step_bytes_per_pair(d, W) * B * args.steps * world
+    out = {
+        "metric": "BPR triplets/sec/GPU (d=64) + achieved HBM GB/s; NDCG@10 vs ref",
+        "value": value, "unit": "triplets/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (seeded, generated in-repo), random-init tables",
+        "config": {"workload": cfg["desc"], "model": cfg["model"], "n_users": nu_all,
+                   "n_items": ni, "nnz_rank0": int(len(indices)), "d": d, "W": W,
+                   "batch_pairs_per_gpu": B, "global_batch": B * world,
+                   "parallelism": "dp%d user-sharded, RCCL item-grad all-reduce" % world
+                   if world > 1 else "single GPU"},
+        "per_gpu_value": value / world,
+        "full_step_algorithmic_GBps": full_b / elapsed / 1e9,
+        "roofline": roofline,
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(cfg, indptr, indices)
+        except Exception as ex:  # the bench line must still print
+            log("cpu baseline failed: %r" % (ex,))
+            out["cpu_baseline"] = None
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out))
+        sys.stdout.flush()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

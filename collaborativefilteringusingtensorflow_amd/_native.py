@@ -1,0 +1,132 @@
+"""ctypes binding of the C ABI in include/cf_engine.h (libcf_engine.so).
+
+The product has no CPU fallback: if the shared library is missing, or no HIP
+device is visible when an engine is created, the calls raise.
+"""
+import ctypes
+import os
+import re
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CF_ENGINE_LIB", os.path.join(_PKG, "build", "libcf_engine.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "cf_engine.h")
+
+CF_BPR, CF_GBPR, CF_CML, CF_AMF = 0, 1, 2, 3
+MODEL_IDS = {"bpr": CF_BPR, "bprmf": CF_BPR, "gbpr": CF_GBPR, "gbprmf": CF_GBPR,
+             "cml": CF_CML, "amf": CF_AMF}
+TABLES = {"user": 0, "item": 1, "bias": 2, "acc_user": 3, "acc_item": 4, "acc_bias": 5}
+KERNELS = {"step": 0, "apply": 1, "apply_dense": 2, "clip": 3, "score": 4, "topk": 5}
+STATUS = {0: "CF_OK", -1: "CF_EINVAL", -2: "CF_EHIP", -3: "CF_ESTATE", -4: "CF_ENOMEM"}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class CfConfig(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_int32),
+        ("n_factors", ctypes.c_int32),
+        ("n_users", ctypes.c_int64),
+        ("n_items", ctypes.c_int64),
+        ("n_neg", ctypes.c_int32),
+        ("gsize", ctypes.c_int32),
+        ("lr", ctypes.c_float),
+        ("reg", ctypes.c_float),
+        ("rho", ctypes.c_float),
+        ("margin", ctypes.c_float),
+        ("reg_cov", ctypes.c_float),
+        ("clip_norm", ctypes.c_float),
+        ("reg_adv", ctypes.c_float),
+        ("epsilon", ctypes.c_float),
+        ("acc_init", ctypes.c_float),
+        ("use_rank_weight", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("dense_item_apply", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+_PI32 = ctypes.POINTER(ctypes.c_int32)
+_PI64 = ctypes.POINTER(ctypes.c_int64)
+_PF = ctypes.POINTER(ctypes.c_float)
+_PD = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); must cover every function declared in the header
+SIGNATURES = {
+    "cf_version": (ctypes.c_char_p, []),
+    "cf_last_error": (ctypes.c_char_p, []),
+    "cf_device_count": (ctypes.c_int, [_PI32]),
+    "cf_config_defaults": (None, [ctypes.POINTER(CfConfig)]),
+    "cf_create": (ctypes.c_int, [ctypes.POINTER(CfConfig), ctypes.POINTER(_P)]),
+    "cf_destroy": (ctypes.c_int, [_P]),
+    "cf_set_stream": (ctypes.c_int, [_P, _P]),
+    "cf_synchronize": (ctypes.c_int, [_P]),
+    "cf_set_interactions": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
+    "cf_init_params": (ctypes.c_int, [_P, _F, _F, _I32, _U64]),
+    "cf_set_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
+    "cf_get_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
+    "cf_step": (ctypes.c_int, [_P, _PI32, _PI32, _PI32, _I32, _PD]),
+    "cf_train_steps": (ctypes.c_int, [_P, _I32, _I32, _PD]),
+    "cf_sample": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
+    "cf_get_sampler_state": (ctypes.c_int, [_P, _PI64, _PI64]),
+    "cf_set_sampler_state": (ctypes.c_int, [_P, _I64, _I64]),
+    "cf_begin_phase": (ctypes.c_int, [_P, _I32]),
+    "cf_bind_item_grad": (ctypes.c_int, [_P, _P, _I64]),
+    "cf_step_local": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
+    "cf_step_items": (ctypes.c_int, [_P]),
+    "cf_take_loss": (ctypes.c_int, [_P, _PD]),
+    "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
+    "cf_profile_enable": (ctypes.c_int, [_P, _I32]),
+    "cf_profile_read": (ctypes.c_int, [_P, _I32, _PD, _PI64]),
+    "cf_profile_reset": (ctypes.c_int, [_P]),
+    "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
+    "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),
+}
+
+_lib = None
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/cf_engine.h."""
+    with open(path) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(cf_[a-z_0-9]+)\s*\(", text)))
+
+
+def lib():
+    """Load libcf_engine.so once; raise NativeError if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            "libcf_engine.so not found at %s -- build it with "
+            "`python -m collaborativefilteringusingtensorflow_amd.csrc.build` "
+            "(there is no CPU fallback)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status, what=""):
+    if status != 0:
+        msg = lib().cf_last_error().decode("utf-8", "replace")
+        raise NativeError("%s failed: %s (%s)" % (what, msg, STATUS.get(status, status)))
+
+
+def device_count():
+    n = ctypes.c_int32(0)
+    lib().cf_device_count(ctypes.byref(n))
+    return int(n.value)

@@ -1,0 +1,63 @@
+"""Build libcf_engine.so for gfx950 in-tree (hipcc cross-compiles without a GPU).
+
+    python -m collaborativefilteringusingtensorflow_amd.csrc.build [--force]
+
+Objects and the shared library go to collaborativefilteringusingtensorflow_amd/build/
+(git-ignored, but shipped to the GPU box by gpurun).
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+OUT = os.path.join(PKG, "build")
+LIB = os.path.join(OUT, "libcf_engine.so")
+SOURCES = ["cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp"]
+HEADERS = ["cf_kernels.h", "cf_device.h", os.path.join(ROOT, "include", "cf_engine.h")]
+ARCH = os.environ.get("CF_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
+         "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _compile(src):
+    path = os.path.join(HERE, src)
+    obj = os.path.join(OUT, src + ".o")
+    deps = [path] + [h if os.path.isabs(h) else os.path.join(HERE, h) for h in HEADERS]
+    if not _newer(obj, deps):
+        return obj
+    cmd = [HIPCC] + FLAGS + ["-c", path, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", path, "-o", obj]
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OUT, exist_ok=True)
+    if force:
+        for f in os.listdir(OUT):
+            if f.endswith(".o") or f.endswith(".so"):
+                os.remove(os.path.join(OUT, f))
+    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if _newer(LIB, objs):
+        subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs
+                       + ["-lpthread"], check=True)
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

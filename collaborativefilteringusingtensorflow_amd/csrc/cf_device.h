@@ -1,0 +1,88 @@
+// cf_device.h -- gfx950 device helpers: counter-based RNG, the keyed epoch
+// bijection, 64-lane wave reductions, order-preserving float keys.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "cf_kernels.h"
+
+namespace cfk {
+
+// SplitMix64 finaliser: a strong 64-bit mixer, used as a counter-based RNG
+// (every draw is hash(key, counter) -- no RNG state to carry between steps).
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// floor(h * n / 2^64): uniform in [0, n) with bias <= n / 2^64.
+__device__ __forceinline__ uint64_t uniform_below(uint64_t h, uint64_t n) {
+    return __umul64hi(h, n);
+}
+
+// One bijective pass on [0, 2^bits): xor key, multiply by odd, xorshift.
+__host__ __device__ __forceinline__ uint64_t perm_rounds(uint64_t x, const PermKey& p) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        x = (x ^ p.k[r]) & p.mask;
+        x = (x * p.m[r]) & p.mask;
+        x ^= x >> p.shift;
+    }
+    return x;
+}
+
+// Cycle-walking restriction of the 2^bits bijection to [0, n): a bijection.
+__host__ __device__ __forceinline__ uint64_t permute(uint64_t x, const PermKey& p) {
+    do {
+        x = perm_rounds(x, p);
+    } while (x >= p.n);
+    return x;
+}
+
+// butterfly sum: every lane ends with the bitwise-identical total
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Order-preserving map float -> uint32 (larger float => larger key).  Key 0
+// is reserved for "excluded" (train items under exclude_train).
+__device__ __forceinline__ uint32_t float_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return u < 1u ? 1u : u;
+}
+__device__ __forceinline__ float key_float(uint32_t u) {
+    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+    return __uint_as_float(u);
+}
+
+// lower_bound membership test in a sorted int32 run [lo, hi)
+__device__ __forceinline__ bool sorted_contains(const int32_t* __restrict__ a, int64_t lo,
+                                                int64_t hi, int32_t key) {
+    const int64_t end = hi;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        int32_t v = a[mid];
+        if (v < key) lo = mid + 1; else hi = mid;
+    }
+    return lo < end && a[lo] == key;
+}
+
+}  // namespace cfk

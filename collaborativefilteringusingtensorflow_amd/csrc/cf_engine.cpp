@@ -1,0 +1,874 @@
+// cf_engine.cpp -- host side of the C ABI declared in include/cf_engine.h.
+// Owns the device tables, the HBM-resident interaction graph, the device
+// sampler position and the HIP stream; enqueues the gfx950 kernels of
+// cf_kernels.hip / cf_eval.hip.  No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/cf_engine.h"
+#include "cf_kernels.h"
+
+using namespace cfk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define CF_HIP(expr)                                                                  \
+    do {                                                                              \
+        hipError_t _e = (expr);                                                       \
+        if (_e != hipSuccess)                                                         \
+            return fail(CF_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+    } while (0)
+
+#define CF_TRY(expr)            \
+    do {                        \
+        int _r = (expr);        \
+        if (_r != CF_OK) return _r; \
+    } while (0)
+
+template <class T>
+int dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) return CF_OK;
+    hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+    if (e != hipSuccess)
+        return fail(CF_ENOMEM, "hipMalloc(" + std::to_string(n * sizeof(T)) + " B): " +
+                                   hipGetErrorString(e));
+    return CF_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct cf_engine {
+    cf_config cfg{};
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+
+    // graph (HBM)
+    int64_t nnz = 0;
+    int64_t* indptr = nullptr;
+    int32_t* indices = nullptr;
+    int2* pairs = nullptr;
+    int64_t* indptr_t = nullptr;
+    int32_t* indices_t = nullptr;
+    std::vector<int64_t> h_indptr;
+
+    // tables
+    float *U = nullptr, *V = nullptr, *b = nullptr;
+    float *AU = nullptr, *AV = nullptr, *Ab = nullptr;
+    float *GU = nullptr, *GV = nullptr, *Gb = nullptr;
+    float *GV_own = nullptr, *Gb_own = nullptr;
+    uint32_t *markU = nullptr, *markV = nullptr;
+    uint32_t stamp = 0;
+
+    // batch
+    int Bcap = 0;
+    int32_t *occU = nullptr, *occV = nullptr;
+    uint8_t *flagU = nullptr, *flagV = nullptr;
+    double* loss_partial = nullptr;
+    double* loss = nullptr;   // [0] running accumulator, [1] per-call scratch
+    double* h_loss = nullptr; // pinned
+    int32_t* h_stage = nullptr;
+    size_t stage_cap = 0;
+    hipEvent_t stage_ev = nullptr;
+
+    // device sampler position
+    int64_t epoch = 0, batch = 0;
+    int sampler_B = 0;
+
+    // model state
+    int phase = 0;
+    bool need_clip_U = false, need_clip_V = false;
+
+    // eval workspace
+    uint32_t* keys = nullptr;
+    size_t keys_cap = 0;
+
+    // profiling
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CF_K_COUNT];
+    std::vector<hipEvent_t> ev_pool;
+};
+
+namespace {
+
+int set_dev(cf_engine* e) {
+    CF_HIP(hipSetDevice(e->cfg.device));
+    return CF_OK;
+}
+
+struct ProfScope {
+    cf_engine* e;
+    int k;
+    hipEvent_t a = nullptr, z = nullptr;
+    static hipEvent_t get(cf_engine* e) {
+        hipEvent_t x = nullptr;
+        if (!e->ev_pool.empty()) {
+            x = e->ev_pool.back();
+            e->ev_pool.pop_back();
+        } else if (hipEventCreate(&x) != hipSuccess) {
+            x = nullptr;
+        }
+        return x;
+    }
+    ProfScope(cf_engine* e_, int k_) : e(e_), k(k_) {
+        if (!e->prof) return;
+        a = get(e);
+        z = get(e);
+        if (a) (void)hipEventRecord(a, e->stream);
+    }
+    ~ProfScope() {
+        if (!a || !z) return;
+        (void)hipEventRecord(z, e->stream);
+        e->ev[k].emplace_back(a, z);
+    }
+};
+
+int users_per_pair(const cf_config& c) { return c.model == CF_GBPR ? 1 + c.gsize : 1; }
+int items_per_pair(const cf_config& c) { return 1 + c.n_neg; }
+int group_count(const cf_config& c) { return c.model == CF_GBPR ? c.gsize : 0; }
+
+int ensure_batch(cf_engine* e, int B) {
+    if (B <= e->Bcap) return CF_OK;
+    dfree(e->occU);
+    dfree(e->occV);
+    dfree(e->flagU);
+    dfree(e->flagV);
+    dfree(e->loss_partial);
+    const size_t nU = (size_t)B * users_per_pair(e->cfg);
+    const size_t nV = (size_t)B * items_per_pair(e->cfg);
+    CF_TRY(dalloc(&e->occU, nU));
+    CF_TRY(dalloc(&e->occV, nV));
+    CF_TRY(dalloc(&e->flagU, nU));
+    CF_TRY(dalloc(&e->flagV, nV));
+    CF_HIP(hipMemsetAsync(e->flagU, 0, nU, e->stream));
+    CF_HIP(hipMemsetAsync(e->flagV, 0, nV, e->stream));
+    CF_TRY(dalloc(&e->loss_partial, (size_t)(B + kPairsPerBlock - 1) / kPairsPerBlock));
+    e->Bcap = B;
+    return CF_OK;
+}
+
+StepArgs base_step_args(cf_engine* e, int B) {
+    const cf_config& c = e->cfg;
+    StepArgs a{};
+    a.model = c.model;
+    a.d = c.n_factors;
+    a.W = c.n_neg;
+    a.G = group_count(c);
+    a.B = B;
+    a.adversarial = (c.model == CF_AMF && e->phase == 1) ? 1 : 0;
+    a.reg = c.reg;
+    a.rho = c.rho;
+    a.margin = c.margin;
+    a.reg_cov = c.reg_cov;
+    a.reg_adv = c.reg_adv;
+    a.use_rank_weight = c.use_rank_weight;
+    a.n_items_f = (float)c.n_items;
+    a.n_items = c.n_items;
+    a.pairs = e->pairs;
+    a.indptr = e->indptr;
+    a.indices = e->indices;
+    a.indptr_t = e->indptr_t;
+    a.indices_t = e->indices_t;
+    a.U = e->U;
+    a.V = e->V;
+    a.b = e->b;
+    a.GU = e->GU;
+    a.GV = e->GV;
+    a.Gb = e->Gb;
+    a.occU = e->occU;
+    a.occV = e->occV;
+    a.flagU = e->flagU;
+    a.flagV = e->flagV;
+    a.markU = e->markU;
+    a.markV = e->markV;
+    a.loss_partial = e->loss_partial;
+    a.grads = 1;
+    a.mark_users = 1;
+    a.mark_items = c.dense_item_apply ? 0 : 1;
+    return a;
+}
+
+int next_stamp(cf_engine* e) {
+    if (++e->stamp == 0) {
+        CF_HIP(hipMemsetAsync(e->markU, 0, (size_t)e->cfg.n_users * sizeof(uint32_t), e->stream));
+        CF_HIP(hipMemsetAsync(e->markV, 0, (size_t)e->cfg.n_items * sizeof(uint32_t), e->stream));
+        e->stamp = 1;
+    }
+    return CF_OK;
+}
+
+// position the device sampler for the next batch of B pairs
+int sampler_args(cf_engine* e, int B, StepArgs* a) {
+    if (!e->pairs) return fail(CF_ESTATE, "no interactions: call cf_set_interactions first");
+    if ((int64_t)B > e->nnz) return fail(CF_EINVAL, "batch size exceeds the number of interactions");
+    if (e->sampler_B != B) {
+        if (e->sampler_B != 0 && e->batch != 0) {
+            e->epoch += 1;
+            e->batch = 0;
+        }
+        e->sampler_B = B;
+    }
+    const int64_t per_epoch = e->nnz / B;  // int(len(pairs)/batch_size), sampler_ranking.py:25
+    if (e->batch >= per_epoch) {
+        e->epoch += 1;
+        e->batch = 0;
+    }
+    a->sample = 1;
+    a->slot_base = (uint64_t)(e->batch * (int64_t)B);
+    a->perm = make_perm_key((uint64_t)e->nnz, e->cfg.seed, (uint64_t)e->epoch);
+    a->rng_key = mix64_host(e->cfg.seed ^ mix64_host((uint64_t)e->epoch * 0x9E3779B97F4A7C15ull +
+                                                     0x2545F4914F6CDD1Dull));
+    e->batch += 1;
+    return CF_OK;
+}
+
+int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
+                     const int32_t* groups, int B) {
+    const cf_config& c = e->cfg;
+    const int W = c.n_neg, G = group_count(c);
+    if (!pairs || !negs) return fail(CF_EINVAL, "pairs and negs are required");
+    if (G > 0 && !groups) return fail(CF_EINVAL, "GBPR needs groups");
+    const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
+    const size_t need = nU + nV;
+    if (need > e->stage_cap) {
+        if (e->h_stage) {
+            (void)hipEventSynchronize(e->stage_ev);
+            (void)hipHostFree(e->h_stage);
+            e->h_stage = nullptr;
+        }
+        CF_HIP(hipHostMalloc((void**)&e->h_stage, need * sizeof(int32_t), hipHostMallocDefault));
+        e->stage_cap = need;
+    } else {
+        CF_HIP(hipEventSynchronize(e->stage_ev));
+    }
+    int32_t* su = e->h_stage;
+    int32_t* sv = e->h_stage + nU;
+    const int64_t nu = c.n_users, ni = c.n_items;
+    for (int p = 0; p < B; ++p) {
+        const int32_t u = pairs[2 * p], i = pairs[2 * p + 1];
+        if (u < 0 || u >= nu || i < 0 || i >= ni)
+            return fail(CF_EINVAL, "pair " + std::to_string(p) + " out of range");
+        su[p] = u;
+        sv[p] = i;
+        for (int w = 0; w < W; ++w) {
+            const int32_t j = negs[(size_t)p * W + w];
+            if (j < 0 || j >= ni) return fail(CF_EINVAL, "negative item out of range");
+            sv[B + (size_t)p * W + w] = j;
+        }
+        for (int k = 0; k < G; ++k) {
+            const int32_t g = groups[(size_t)p * G + k];
+            if (g < 0 || g >= nu) return fail(CF_EINVAL, "group user out of range");
+            su[B + (size_t)p * G + k] = g;
+        }
+    }
+    CF_HIP(hipMemcpyAsync(e->occU, su, nU * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+    CF_HIP(hipMemcpyAsync(e->occV, sv, nV * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
+    CF_HIP(hipEventRecord(e->stage_ev, e->stream));
+    return CF_OK;
+}
+
+// step kernel + user (and, in sparse mode, item) apply; loss added to *loss_acc
+int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
+             const int32_t* groups, double* loss_acc, bool apply_items_dense_now) {
+    const cf_config& c = e->cfg;
+    CF_TRY(ensure_batch(e, B));
+    StepArgs a = base_step_args(e, B);
+    a.occU = e->occU;
+    a.occV = e->occV;
+    a.flagU = e->flagU;
+    a.flagV = e->flagV;
+    a.loss_partial = e->loss_partial;
+    if (pairs) {
+        CF_TRY(stage_host_batch(e, pairs, negs, groups, B));
+        a.sample = 0;
+    } else {
+        CF_TRY(sampler_args(e, B, &a));
+    }
+    CF_TRY(next_stamp(e));
+    a.stamp = e->stamp;
+    {
+        ProfScope ps(e, CF_K_STEP);
+        CF_HIP(launch_step(a, e->stream));
+    }
+    ApplyArgs p{};
+    p.d = c.n_factors;
+    p.lr = c.lr;
+    p.clip_norm = c.clip_norm;
+    p.clip = c.model == CF_CML ? 1 : 0;
+    p.nU = B * users_per_pair(c);
+    p.nV = B * items_per_pair(c);
+    const int per_block = kWavesPerBlock * kWave;
+    p.blocksU = (p.nU + per_block - 1) / per_block;
+    p.occU = e->occU;
+    p.occV = e->occV;
+    p.flagU = e->flagU;
+    p.flagV = e->flagV;
+    p.U = e->U; p.AU = e->AU; p.GU = e->GU;
+    p.V = e->V; p.AV = e->AV; p.GV = e->GV;
+    p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
+    p.apply_items = c.dense_item_apply ? 0 : 1;
+    p.loss_partial = e->loss_partial;
+    p.n_partial = (B + kPairsPerBlock - 1) / kPairsPerBlock;
+    p.loss_acc = loss_acc;
+    {
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    if (e->need_clip_U) {
+        ProfScope ps(e, CF_K_CLIP);
+        CF_HIP(launch_clip_full(e->U, c.n_users, c.n_factors, c.clip_norm, e->stream));
+        e->need_clip_U = false;
+    }
+    if (!c.dense_item_apply) {
+        if (e->need_clip_V) {
+            ProfScope ps(e, CF_K_CLIP);
+            CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
+            e->need_clip_V = false;
+        }
+    } else if (apply_items_dense_now) {
+        // single-rank dense mode: no all-reduce between the two phases
+        (void)0;
+    }
+    return CF_OK;
+}
+
+int run_items_dense(cf_engine* e) {
+    const cf_config& c = e->cfg;
+    DenseArgs d{};
+    d.d = c.n_factors;
+    d.lr = c.lr;
+    d.clip_norm = c.clip_norm;
+    d.clip = c.model == CF_CML ? 1 : 0;
+    d.n_rows = c.n_items;
+    d.X = e->V; d.A = e->AV; d.G = e->GV;
+    d.b = e->b; d.Ab = e->Ab; d.Gb = e->Gb;
+    {
+        ProfScope ps(e, CF_K_APPLY_DENSE);
+        CF_HIP(launch_apply_dense(d, e->stream));
+    }
+    if (e->need_clip_V) {
+        ProfScope ps(e, CF_K_CLIP);
+        CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
+        e->need_clip_V = false;
+    }
+    return CF_OK;
+}
+
+int read_loss(cf_engine* e, int slot, double* out) {
+    CF_HIP(hipMemcpyAsync(e->h_loss, e->loss + slot, sizeof(double), hipMemcpyDeviceToHost,
+                          e->stream));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    *out = *e->h_loss;
+    CF_HIP(hipMemsetAsync(e->loss + slot, 0, sizeof(double), e->stream));
+    return CF_OK;
+}
+
+int check_engine(cf_engine* e) {
+    if (!e) return fail(CF_EINVAL, "null engine");
+    return set_dev(e);
+}
+
+float* table_ptr(cf_engine* e, int t, int64_t* n) {
+    const cf_config& c = e->cfg;
+    const int64_t ud = c.n_users * (int64_t)c.n_factors, id = c.n_items * (int64_t)c.n_factors;
+    switch (t) {
+        case CF_TABLE_USER: *n = ud; return e->U;
+        case CF_TABLE_ITEM: *n = id; return e->V;
+        case CF_TABLE_BIAS: *n = c.n_items; return e->b;
+        case CF_TABLE_ACC_USER: *n = ud; return e->AU;
+        case CF_TABLE_ACC_ITEM: *n = id; return e->AV;
+        case CF_TABLE_ACC_BIAS: *n = c.n_items; return e->Ab;
+        default: *n = 0; return nullptr;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cf_version(void) { return "cf_engine 0.1 (gfx950)"; }
+
+const char* cf_last_error(void) { return g_err.c_str(); }
+
+int cf_device_count(int32_t* count_out) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (count_out) *count_out = n;
+    return CF_OK;
+}
+
+void cf_config_defaults(cf_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->model = CF_BPR;
+    c->n_factors = 20;       // bprmf.py:15
+    c->n_neg = 1;
+    c->gsize = 1;
+    c->lr = 0.1f;            // bprmf.py:16
+    c->reg = 0.02f;          // bprmf.py:15
+    c->rho = 0.5f;           // gbprmf.py:14
+    c->margin = 1.5f;        // cml.py:16
+    c->reg_cov = 1.0f;       // cml.py:16
+    c->clip_norm = 1.0f;     // cml.py:16
+    c->reg_adv = 1.0f;       // amf.py:15
+    c->epsilon = 0.5f;       // amf.py:15
+    c->acc_init = 0.1f;      // tf.train.AdagradOptimizer initial_accumulator_value
+    c->use_rank_weight = 1;  // cml.py:16
+    c->seed = 20261015ull;
+}
+
+int cf_create(const cf_config* cfg, cf_engine** out) {
+    if (!cfg || !out) return fail(CF_EINVAL, "null argument");
+    *out = nullptr;
+    const cf_config& c = *cfg;
+    if (c.model < CF_BPR || c.model > CF_AMF) return fail(CF_EINVAL, "unknown model");
+    if (c.n_factors < 1 || c.n_factors > kMaxFactors) return fail(CF_EINVAL, "n_factors must be 1..256");
+    if (c.n_users < 1 || c.n_users > INT32_MAX) return fail(CF_EINVAL, "n_users out of range");
+    if (c.n_items < 2 || c.n_items > INT32_MAX) return fail(CF_EINVAL, "n_items out of range");
+    if (c.n_neg < 1 || c.n_neg > kMaxNeg) return fail(CF_EINVAL, "n_neg must be 1..64");
+    if (c.model == CF_GBPR && (c.gsize < 1 || c.gsize > kMaxGroup))
+        return fail(CF_EINVAL, "gsize must be 1..16");
+    if (!(c.lr > 0.f) || !(c.acc_init > 0.f)) return fail(CF_EINVAL, "lr and acc_init must be > 0");
+    if (c.model == CF_CML && !(c.clip_norm > 0.f)) return fail(CF_EINVAL, "clip_norm must be > 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(CF_EHIP, "no HIP device visible (the engine has no CPU fallback)");
+    if (c.device < 0 || c.device >= ndev) return fail(CF_EINVAL, "device ordinal out of range");
+
+    cf_engine* e = new (std::nothrow) cf_engine();
+    if (!e) return fail(CF_ENOMEM, "host allocation failed");
+    e->cfg = c;
+    int r = CF_OK;
+    auto bail = [&](int code) {
+        cf_destroy(e);
+        return code;
+    };
+    if ((r = set_dev(e)) != CF_OK) return bail(r);
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(CF_EHIP, "hipStreamCreate failed"));
+    e->own_stream = true;
+    if (hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(CF_EHIP, "hipEventCreate failed"));
+    (void)hipEventRecord(e->stage_ev, e->stream);
+    const size_t ud = (size_t)c.n_users * c.n_factors, id = (size_t)c.n_items * c.n_factors;
+    if ((r = dalloc(&e->U, ud)) || (r = dalloc(&e->AU, ud)) || (r = dalloc(&e->GU, ud)) ||
+        (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
+        (r = dalloc(&e->markU, (size_t)c.n_users)) || (r = dalloc(&e->markV, (size_t)c.n_items)) ||
+        (r = dalloc(&e->loss, 2)))
+        return bail(r);
+    if (c.model == CF_GBPR) {
+        if ((r = dalloc(&e->b, (size_t)c.n_items)) || (r = dalloc(&e->Ab, (size_t)c.n_items)) ||
+            (r = dalloc(&e->Gb_own, (size_t)c.n_items)))
+            return bail(r);
+    }
+    e->GV = e->GV_own;
+    e->Gb = e->Gb_own;
+    if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
+        return bail(fail(CF_ENOMEM, "pinned allocation failed"));
+    hipStream_t s = e->stream;
+    if (hipMemsetAsync(e->GU, 0, ud * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->GV, 0, id * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->U, 0, ud * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->V, 0, id * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->markU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->markV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
+        return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
+    if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
+        launch_fill(e->AV, (int64_t)id, c.acc_init, s) != hipSuccess)
+        return bail(fail(CF_EHIP, "fill kernel failed"));
+    if (c.model == CF_GBPR) {
+        if (hipMemsetAsync(e->b, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+            hipMemsetAsync(e->Gb, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+            launch_fill(e->Ab, c.n_items, c.acc_init, s) != hipSuccess)
+            return bail(fail(CF_EHIP, "bias init failed"));
+    }
+    e->need_clip_U = e->need_clip_V = (c.model == CF_CML);
+    if (hipStreamSynchronize(s) != hipSuccess) return bail(fail(CF_EHIP, "stream sync failed"));
+    *out = e;
+    return CF_OK;
+}
+
+int cf_destroy(cf_engine* e) {
+    if (!e) return CF_OK;
+    (void)hipSetDevice(e->cfg.device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (auto& v : e->ev)
+        for (auto& pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    for (auto x : e->ev_pool) (void)hipEventDestroy(x);
+    dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
+    dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
+    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own); dfree(e->markU); dfree(e->markV);
+    dfree(e->occU); dfree(e->occV); dfree(e->flagU); dfree(e->flagV);
+    dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
+    if (e->h_loss) (void)hipHostFree(e->h_loss);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
+    if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+    return CF_OK;
+}
+
+int cf_set_stream(cf_engine* e, void* s) {
+    CF_TRY(check_engine(e));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    if (s) {
+        if (e->own_stream) (void)hipStreamDestroy(e->stream);
+        e->stream = (hipStream_t)s;
+        e->own_stream = false;
+    } else if (!e->own_stream) {
+        CF_HIP(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        e->own_stream = true;
+    }
+    return CF_OK;
+}
+
+int cf_synchronize(cf_engine* e) {
+    CF_TRY(check_engine(e));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    return CF_OK;
+}
+
+int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indices, int64_t nnz) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (!indptr || (nnz > 0 && !indices)) return fail(CF_EINVAL, "null CSR");
+    if (nnz < 1) return fail(CF_EINVAL, "no interactions");
+    if (indptr[0] != 0 || indptr[c.n_users] != nnz) return fail(CF_EINVAL, "indptr does not span nnz");
+    for (int64_t u = 0; u < c.n_users; ++u) {
+        const int64_t rb = indptr[u], re = indptr[u + 1];
+        if (re < rb) return fail(CF_EINVAL, "indptr not monotone");
+        if (re - rb >= c.n_items)
+            return fail(CF_EINVAL, "user " + std::to_string(u) +
+                                       " has every item as a positive; no negative can be drawn");
+        for (int64_t k = rb; k < re; ++k) {
+            const int32_t it = indices[k];
+            if (it < 0 || it >= c.n_items) return fail(CF_EINVAL, "item id out of range");
+            if (k > rb && indices[k - 1] >= it) return fail(CF_EINVAL, "CSR rows must be sorted, unique");
+        }
+    }
+    dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
+    CF_TRY(dalloc(&e->indptr, (size_t)c.n_users + 1));
+    CF_TRY(dalloc(&e->indices, (size_t)nnz));
+    CF_TRY(dalloc(&e->pairs, (size_t)nnz));
+    CF_HIP(hipMemcpyAsync(e->indptr, indptr, ((size_t)c.n_users + 1) * 8, hipMemcpyHostToDevice, e->stream));
+    CF_HIP(hipMemcpyAsync(e->indices, indices, (size_t)nnz * 4, hipMemcpyHostToDevice, e->stream));
+    CF_HIP(launch_build_pairs(e->indptr, e->indices, c.n_users, e->pairs, e->stream));
+    if (c.model == CF_GBPR) {
+        // item -> users transpose (item_posUserList, sampler_gbpr.py:15)
+        std::vector<int64_t> tp((size_t)c.n_items + 1, 0);
+        for (int64_t k = 0; k < nnz; ++k) tp[(size_t)indices[k] + 1]++;
+        for (int64_t i = 0; i < c.n_items; ++i) tp[i + 1] += tp[i];
+        std::vector<int32_t> tu((size_t)nnz);
+        std::vector<int64_t> fill(tp.begin(), tp.end() - 1);
+        for (int64_t u = 0; u < c.n_users; ++u)
+            for (int64_t k = indptr[u]; k < indptr[u + 1]; ++k) tu[fill[indices[k]]++] = (int32_t)u;
+        CF_TRY(dalloc(&e->indptr_t, (size_t)c.n_items + 1));
+        CF_TRY(dalloc(&e->indices_t, (size_t)nnz));
+        CF_HIP(hipMemcpyAsync(e->indptr_t, tp.data(), tp.size() * 8, hipMemcpyHostToDevice, e->stream));
+        CF_HIP(hipMemcpyAsync(e->indices_t, tu.data(), tu.size() * 4, hipMemcpyHostToDevice, e->stream));
+        CF_HIP(hipStreamSynchronize(e->stream));  // host vectors go out of scope
+    }
+    CF_HIP(hipStreamSynchronize(e->stream));
+    e->h_indptr.assign(indptr, indptr + c.n_users + 1);
+    e->nnz = nnz;
+    e->epoch = 0;
+    e->batch = 0;
+    e->sampler_B = 0;
+    return CF_OK;
+}
+
+int cf_init_params(cf_engine* e, float mean, float stddev, int32_t truncated, uint64_t seed) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    const int64_t ud = c.n_users * (int64_t)c.n_factors, id = c.n_items * (int64_t)c.n_factors;
+    CF_HIP(launch_init_normal(e->U, ud, mean, stddev, truncated, mix64_host(seed ^ 0x55u), e->stream));
+    CF_HIP(launch_init_normal(e->V, id, mean, stddev, truncated, mix64_host(seed ^ 0xAAu), e->stream));
+    CF_HIP(launch_fill(e->AU, ud, c.acc_init, e->stream));
+    CF_HIP(launch_fill(e->AV, id, c.acc_init, e->stream));
+    if (c.model == CF_GBPR) {
+        CF_HIP(launch_init_normal(e->b, c.n_items, mean, stddev, truncated, mix64_host(seed ^ 0xBBu), e->stream));
+        CF_HIP(launch_fill(e->Ab, c.n_items, c.acc_init, e->stream));
+    }
+    e->need_clip_U = e->need_clip_V = (c.model == CF_CML);
+    CF_HIP(hipStreamSynchronize(e->stream));
+    return CF_OK;
+}
+
+int cf_set_table(cf_engine* e, int32_t t, const float* src, int64_t n) {
+    CF_TRY(check_engine(e));
+    int64_t want = 0;
+    float* p = table_ptr(e, t, &want);
+    if (!p) return fail(CF_EINVAL, "table not present in this model");
+    if (n != want || !src) return fail(CF_EINVAL, "table size mismatch: want " + std::to_string(want));
+    CF_HIP(hipMemcpyAsync(p, src, (size_t)n * 4, hipMemcpyHostToDevice, e->stream));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    if (e->cfg.model == CF_CML) {
+        if (t == CF_TABLE_USER) e->need_clip_U = true;
+        if (t == CF_TABLE_ITEM) e->need_clip_V = true;
+    }
+    return CF_OK;
+}
+
+int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
+    CF_TRY(check_engine(e));
+    int64_t want = 0;
+    float* p = table_ptr(e, t, &want);
+    if (!p) return fail(CF_EINVAL, "table not present in this model");
+    if (n != want || !dst) return fail(CF_EINVAL, "table size mismatch: want " + std::to_string(want));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipMemcpy(dst, p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return CF_OK;
+}
+
+int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32_t* groups,
+            int32_t B, double* loss_out) {
+    CF_TRY(check_engine(e));
+    if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
+    if (!pairs) return fail(CF_EINVAL, "host batch required (use cf_train_steps for the device sampler)");
+    if (e->cfg.dense_item_apply && e->GV != e->GV_own)
+        return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
+    double* acc = loss_out ? e->loss + 1 : e->loss;
+    CF_TRY(run_step(e, B, pairs, negs, groups, acc, true));
+    if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
+    if (loss_out) CF_TRY(read_loss(e, 1, loss_out));
+    return CF_OK;
+}
+
+int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_out) {
+    CF_TRY(check_engine(e));
+    if (B < 1 || n_steps < 0) return fail(CF_EINVAL, "bad B / n_steps");
+    if (e->cfg.dense_item_apply && e->GV != e->GV_own)
+        return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
+    double* acc = loss_sum_out ? e->loss + 1 : e->loss;
+    for (int s = 0; s < n_steps; ++s) {
+        CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc, true));
+        if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
+    }
+    if (loss_sum_out) CF_TRY(read_loss(e, 1, loss_sum_out));
+    return CF_OK;
+}
+
+int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* groups) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (B < 1 || !pairs || !negs) return fail(CF_EINVAL, "bad arguments");
+    const int W = c.n_neg, G = group_count(c);
+    if (G > 0 && !groups) return fail(CF_EINVAL, "GBPR needs a groups buffer");
+    CF_TRY(ensure_batch(e, B));
+    StepArgs a = base_step_args(e, B);
+    CF_TRY(sampler_args(e, B, &a));
+    a.grads = 0;
+    a.mark_users = 0;
+    a.mark_items = 0;
+    CF_HIP(launch_step(a, e->stream));
+    const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
+    std::vector<int32_t> hu(nU), hv(nV);
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipMemcpy(hu.data(), e->occU, nU * 4, hipMemcpyDeviceToHost));
+    CF_HIP(hipMemcpy(hv.data(), e->occV, nV * 4, hipMemcpyDeviceToHost));
+    for (int p = 0; p < B; ++p) {
+        pairs[2 * p] = hu[p];
+        pairs[2 * p + 1] = hv[p];
+        for (int w = 0; w < W; ++w) negs[(size_t)p * W + w] = hv[B + (size_t)p * W + w];
+        for (int k = 0; k < G; ++k) groups[(size_t)p * G + k] = hu[B + (size_t)p * G + k];
+    }
+    return CF_OK;
+}
+
+int cf_get_sampler_state(cf_engine* e, int64_t* epoch, int64_t* batch) {
+    if (!e) return fail(CF_EINVAL, "null engine");
+    if (epoch) *epoch = e->epoch;
+    if (batch) *batch = e->batch;
+    return CF_OK;
+}
+
+int cf_set_sampler_state(cf_engine* e, int64_t epoch, int64_t batch) {
+    if (!e) return fail(CF_EINVAL, "null engine");
+    if (epoch < 0 || batch < 0) return fail(CF_EINVAL, "negative sampler state");
+    e->epoch = epoch;
+    e->batch = batch;
+    return CF_OK;
+}
+
+int cf_begin_phase(cf_engine* e, int32_t phase) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (c.model != CF_AMF) return fail(CF_EINVAL, "phases exist only for AMF");
+    if (phase != 0 && phase != 1) return fail(CF_EINVAL, "phase must be 0 or 1");
+    if (phase == e->phase) return CF_OK;
+    // each phase's train op owns its own AdagradOptimizer (amf.py:208-209):
+    // its accumulators are still at acc_init when the phase starts
+    CF_HIP(launch_fill(e->AU, c.n_users * (int64_t)c.n_factors, c.acc_init, e->stream));
+    CF_HIP(launch_fill(e->AV, c.n_items * (int64_t)c.n_factors, c.acc_init, e->stream));
+    e->phase = phase;
+    return CF_OK;
+}
+
+int cf_bind_item_grad(cf_engine* e, void* ptr, int64_t n) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (!c.dense_item_apply) return fail(CF_ESTATE, "cf_bind_item_grad needs dense_item_apply=1");
+    const int64_t id = c.n_items * (int64_t)c.n_factors;
+    const int64_t want = id + (c.model == CF_GBPR ? c.n_items : 0);
+    if (n != want) return fail(CF_EINVAL, "item-grad buffer must hold " + std::to_string(want) + " floats");
+    if (!ptr) {
+        e->GV = e->GV_own;
+        e->Gb = e->Gb_own;
+        return CF_OK;
+    }
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess || attr.type != hipMemoryTypeDevice)
+        return fail(CF_EINVAL, "item-grad buffer is not device memory");
+    e->GV = (float*)ptr;
+    e->Gb = (c.model == CF_GBPR) ? (float*)ptr + id : e->Gb_own;
+    CF_HIP(hipMemsetAsync(ptr, 0, (size_t)n * 4, e->stream));
+    return CF_OK;
+}
+
+int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                  const int32_t* groups) {
+    CF_TRY(check_engine(e));
+    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_local needs dense_item_apply=1");
+    if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
+    return run_step(e, B, pairs, negs, groups, e->loss, false);
+}
+
+int cf_step_items(cf_engine* e) {
+    CF_TRY(check_engine(e));
+    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_items needs dense_item_apply=1");
+    return run_items_dense(e);
+}
+
+int cf_take_loss(cf_engine* e, double* out) {
+    CF_TRY(check_engine(e));
+    if (!out) return fail(CF_EINVAL, "null output");
+    return read_loss(e, 0, out);
+}
+
+int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int32_t exclude_train,
+                  int32_t* idx_out, float* val_out) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (n < 0 || !idx_out || (n > 0 && !users)) return fail(CF_EINVAL, "bad arguments");
+    if (k < 1 || k > 4096) return fail(CF_EINVAL, "k must be 1..4096");
+    if (exclude_train && !e->indptr) return fail(CF_ESTATE, "exclude_train needs cf_set_interactions");
+    if (n == 0) return CF_OK;
+    for (int r = 0; r < n; ++r)
+        if (users[r] < 0 || users[r] >= c.n_users) return fail(CF_EINVAL, "user id out of range");
+    const size_t row_bytes = (size_t)c.n_items * 4;
+    const size_t budget = (size_t)512 << 20;
+    int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / row_bytes));
+    if ((size_t)chunk * row_bytes > e->keys_cap) {
+        dfree(e->keys);
+        CF_TRY(dalloc(&e->keys, (size_t)chunk * c.n_items));
+        e->keys_cap = (size_t)chunk * row_bytes;
+    }
+    int32_t* d_users = nullptr;
+    int32_t* d_idx = nullptr;
+    float* d_val = nullptr;
+    int r = CF_OK;
+    if ((r = dalloc(&d_users, (size_t)n)) || (r = dalloc(&d_idx, (size_t)n * k)) ||
+        (r = dalloc(&d_val, (size_t)n * k))) {
+        dfree(d_users); dfree(d_idx); dfree(d_val);
+        return r;
+    }
+    hipError_t he = hipMemcpyAsync(d_users, users, (size_t)n * 4, hipMemcpyHostToDevice, e->stream);
+    for (int u0 = 0; he == hipSuccess && u0 < n; u0 += chunk) {
+        const int m = std::min(chunk, n - u0);
+        ScoreArgs s{};
+        s.model = c.model;
+        s.d = c.n_factors;
+        s.n_users = m;
+        s.n_items = c.n_items;
+        s.users = d_users + u0;
+        s.U = e->U;
+        s.V = e->V;
+        s.b = e->b;
+        s.keys = e->keys;
+        s.exclude_train = exclude_train ? 1 : 0;
+        s.indptr = e->indptr;
+        s.indices = e->indices;
+        {
+            ProfScope ps(e, CF_K_SCORE);
+            he = launch_score(s, e->stream);
+        }
+        if (he != hipSuccess) break;
+        TopkArgs t{};
+        t.k = k;
+        t.n_items = c.n_items;
+        t.keys = e->keys;
+        t.idx_out = d_idx + (size_t)u0 * k;
+        t.val_out = d_val + (size_t)u0 * k;
+        {
+            ProfScope ps(e, CF_K_TOPK);
+            he = launch_topk(t, m, e->stream);
+        }
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    if (he == hipSuccess && val_out)
+        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    dfree(d_users); dfree(d_idx); dfree(d_val);
+    if (he != hipSuccess) return fail(CF_EHIP, std::string("cf_score_topk: ") + hipGetErrorString(he));
+    return CF_OK;
+}
+
+int cf_profile_enable(cf_engine* e, int32_t on) {
+    if (!e) return fail(CF_EINVAL, "null engine");
+    e->prof = on != 0;
+    return CF_OK;
+}
+
+int cf_profile_read(cf_engine* e, int32_t kid, double* total_ms, int64_t* launches) {
+    CF_TRY(check_engine(e));
+    if (kid < 0 || kid >= CF_K_COUNT) return fail(CF_EINVAL, "bad kernel id");
+    CF_HIP(hipStreamSynchronize(e->stream));
+    double t = 0.0;
+    for (auto& pr : e->ev[kid]) {
+        float ms = 0.f;
+        CF_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (int64_t)e->ev[kid].size();
+    return CF_OK;
+}
+
+int cf_profile_reset(cf_engine* e) {
+    CF_TRY(check_engine(e));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    for (auto& v : e->ev) {
+        for (auto& pr : v) {
+            e->ev_pool.push_back(pr.first);
+            e->ev_pool.push_back(pr.second);
+        }
+        v.clear();
+    }
+    return CF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// cf_kernels.h -- argument blocks shared by the host engine (cf_engine.cpp)
+// and the gfx950 kernels (cf_kernels.hip, cf_eval.hip).  Plain structs passed
+// by value as kernel arguments; no torch types anywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfk {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kBlock = 256;        // 4 waves per workgroup
+constexpr int kWavesPerBlock = kBlock / kWave;
+constexpr int kPairsPerWave = 16;  // pairs one wave carries through a step
+constexpr int kPairsPerBlock = kPairsPerWave * kWavesPerBlock;
+constexpr int kMaxNeg = 64;
+constexpr int kMaxGroup = 16;
+constexpr int kMaxFactors = 256;
+
+enum Model { BPR = 0, GBPR = 1, CML = 2, AMF = 3 };
+
+// Keyed bijection on [0, n) used as the per-epoch shuffle of the nnz pairs
+// (replaces np.random.shuffle(useritem_pairs), sampler_ranking.py:24).
+struct PermKey {
+    uint64_t n;       // domain size (nnz)
+    uint64_t mask;    // 2^bits - 1, 2^bits >= n
+    uint32_t shift;   // xorshift amount
+    uint32_t pad;
+    uint64_t k[3];    // round keys
+    uint64_t m[3];    // odd round multipliers
+};
+
+struct StepArgs {
+    // model hyper-parameters
+    int model;
+    int d;
+    int W;           // negatives per pair
+    int G;           // group users per pair (GBPR)
+    int B;           // pairs in this step
+    int adversarial; // AMF phase flag
+    float reg, rho, margin, reg_cov, reg_adv;
+    int use_rank_weight;
+    float n_items_f;
+    int64_t n_items;
+    // sampler
+    int sample;          // 1: draw batch on device; 0: batch already in occ*
+    int mark_users;      // claim winner rows for the sparse user apply
+    int mark_items;      // claim winner rows for the sparse item apply
+    int grads;           // 0: sample only (cf_sample)
+    uint64_t slot_base;  // position of this batch inside the epoch shuffle
+    uint64_t rng_key;    // per-epoch draw key
+    uint32_t stamp;      // step id written into the winner marks
+    PermKey perm;
+    // graph
+    const int2* __restrict__ pairs;         // [nnz] (u,i), CSR order
+    const int64_t* __restrict__ indptr;     // [n_users+1]
+    const int32_t* __restrict__ indices;    // [nnz] sorted per user
+    const int64_t* __restrict__ indptr_t;   // [n_items+1] (GBPR)
+    const int32_t* __restrict__ indices_t;  // [nnz] users of each item
+    // tables
+    const float* __restrict__ U;
+    const float* __restrict__ V;
+    const float* __restrict__ b;
+    float* __restrict__ GU;   // dense user-gradient accumulator
+    float* __restrict__ GV;   // dense item-gradient accumulator
+    float* __restrict__ Gb;   // dense bias-gradient accumulator
+    // batch (occurrence lists) and winner flags
+    int32_t* __restrict__ occU;   // [B*(1+G)] u | groups
+    int32_t* __restrict__ occV;   // [B*(1+W)] i | negatives
+    uint8_t* __restrict__ flagU;  // 1 = first occurrence of its row
+    uint8_t* __restrict__ flagV;
+    uint32_t* __restrict__ markU; // [n_users]
+    uint32_t* __restrict__ markV; // [n_items]
+    double* __restrict__ loss_partial;  // [gridDim.x]
+};
+
+struct ApplyArgs {
+    int d;
+    float lr;
+    float clip_norm;
+    int clip;            // CML: clip updated rows
+    // sparse apply over occurrence lists
+    int nU, nV;          // occurrences of each table
+    int blocksU;         // blocks [0, blocksU) serve U, the rest serve V
+    const int32_t* __restrict__ occU;
+    const int32_t* __restrict__ occV;
+    const uint8_t* __restrict__ flagU;
+    const uint8_t* __restrict__ flagV;
+    float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
+    float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
+    float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;  // nullable
+    int apply_items;     // 0 when items are applied densely after an all-reduce
+    // loss reduction (block 0)
+    const double* __restrict__ loss_partial;
+    int n_partial;
+    double* __restrict__ loss_acc;
+};
+
+struct DenseArgs {
+    int d;
+    float lr;
+    float clip_norm;
+    int clip;
+    int64_t n_rows;
+    float* __restrict__ X; float* __restrict__ A; float* __restrict__ G;
+    float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;  // nullable
+};
+
+struct ScoreArgs {
+    int model;
+    int d;
+    int n_users;            // users in this chunk
+    int64_t n_items;
+    const int32_t* __restrict__ users;   // [n_users] global ids
+    const float* __restrict__ U;
+    const float* __restrict__ V;
+    const float* __restrict__ b;         // nullable
+    uint32_t* __restrict__ keys;         // [n_users, n_items] order-preserving keys
+    int exclude_train;
+    const int64_t* __restrict__ indptr;
+    const int32_t* __restrict__ indices;
+};
+
+struct TopkArgs {
+    int k;
+    int64_t n_items;
+    const uint32_t* __restrict__ keys;
+    int32_t* __restrict__ idx_out;   // [n_users, k]
+    float* __restrict__ val_out;     // [n_users, k]
+};
+
+// ---- host launchers (cf_kernels.hip / cf_eval.hip) -------------------------
+hipError_t launch_step(const StepArgs& a, hipStream_t s);
+hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
+hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
+hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);
+hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int truncated,
+                              uint64_t seed, hipStream_t s);
+hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s);
+hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
+                              int2* pairs, hipStream_t s);
+hipError_t launch_score(const ScoreArgs& a, hipStream_t s);
+hipError_t launch_topk(const TopkArgs& a, int n_users, hipStream_t s);
+
+// host-side mirror of the device bijection (for key generation)
+PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch);
+uint64_t mix64_host(uint64_t z);
+
+}  // namespace cfk

@@ -1,0 +1,229 @@
+"""Python face of the native engine: numpy in, numpy out, over the C ABI.
+
+One ``Engine`` = one HIP device's share of a model: the user rows it owns,
+every item row, the Adagrad accumulators, the HBM-resident interaction graph
+and the device sampler position.  The model classes (bprmf.py, gbprmf.py,
+cml.py, amf.py) and the samplers are thin wrappers over this class.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+
+def _ptr(a, ctype):
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+class Engine(object):
+    def __init__(self, model, n_users, n_items, n_factors, n_neg=1, gsize=1, lr=0.1,
+                 reg=0.02, rho=0.5, margin=1.5, reg_cov=1.0, clip_norm=1.0, reg_adv=1.0,
+                 epsilon=0.5, acc_init=0.1, use_rank_weight=True, device=0,
+                 dense_item_apply=False, seed=20261015):
+        L = N.lib()
+        if isinstance(model, str):
+            model = N.MODEL_IDS[model.lower()]
+        cfg = N.CfConfig()
+        L.cf_config_defaults(ctypes.byref(cfg))
+        cfg.model = int(model)
+        cfg.n_factors = int(n_factors)
+        cfg.n_users = int(n_users)
+        cfg.n_items = int(n_items)
+        cfg.n_neg = int(n_neg)
+        cfg.gsize = int(gsize)
+        cfg.lr = float(lr)
+        cfg.reg = float(reg)
+        cfg.rho = float(rho)
+        cfg.margin = float(margin)
+        cfg.reg_cov = float(reg_cov)
+        cfg.clip_norm = float(clip_norm)
+        cfg.reg_adv = float(reg_adv)
+        cfg.epsilon = float(epsilon)
+        cfg.acc_init = float(acc_init)
+        cfg.use_rank_weight = 1 if use_rank_weight else 0
+        cfg.device = int(device)
+        cfg.dense_item_apply = 1 if dense_item_apply else 0
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.cfg = cfg
+        self.model = int(model)
+        self.n_users, self.n_items, self.d = int(n_users), int(n_items), int(n_factors)
+        self.n_neg = int(n_neg)
+        self.gsize = int(gsize) if self.model == N.CF_GBPR else 0
+        self._h = ctypes.c_void_p()
+        N.check(L.cf_create(ctypes.byref(cfg), ctypes.byref(self._h)), "cf_create")
+        self._L = L
+        self.nnz = 0
+
+    # ---- lifecycle --------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.cf_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        N.check(self._L.cf_synchronize(self._h), "cf_synchronize")
+
+    def set_stream(self, hip_stream_ptr):
+        N.check(self._L.cf_set_stream(self._h, ctypes.c_void_p(hip_stream_ptr or None)),
+                "cf_set_stream")
+
+    # ---- data -----------------------------------------------------------------
+    def set_interactions(self, indptr, indices):
+        indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+        indices = _i32(indices)
+        N.check(self._L.cf_set_interactions(self._h, _ptr(indptr, ctypes.c_int64),
+                                            _ptr(indices, ctypes.c_int32), int(indices.shape[0])),
+                "cf_set_interactions")
+        self.nnz = int(indices.shape[0])
+
+    def init_params(self, mean=0.0, stddev=0.1, truncated=True, seed=1):
+        N.check(self._L.cf_init_params(self._h, float(mean), float(stddev), 1 if truncated else 0,
+                                       int(seed) & 0xFFFFFFFFFFFFFFFF), "cf_init_params")
+
+    def _table_shape(self, name):
+        if name in ("user", "acc_user"):
+            return (self.n_users, self.d)
+        if name in ("item", "acc_item"):
+            return (self.n_items, self.d)
+        return (self.n_items,)
+
+    def set_table(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        if a.shape != self._table_shape(name):
+            raise ValueError("table %s must have shape %s" % (name, self._table_shape(name)))
+        N.check(self._L.cf_set_table(self._h, N.TABLES[name], _ptr(a, ctypes.c_float), a.size),
+                "cf_set_table(%s)" % name)
+
+    def get_table(self, name):
+        out = np.empty(self._table_shape(name), dtype=np.float32)
+        N.check(self._L.cf_get_table(self._h, N.TABLES[name], _ptr(out, ctypes.c_float), out.size),
+                "cf_get_table(%s)" % name)
+        return out
+
+    # ---- training -------------------------------------------------------------
+    def _batch(self, pairs, negs, groups):
+        pairs = _i32(pairs).reshape(-1, 2)
+        B = pairs.shape[0]
+        negs = _i32(negs).reshape(B, -1)
+        if negs.shape[1] != self.n_neg:
+            raise ValueError("negs must have %d columns" % self.n_neg)
+        gp = None
+        if self.model == N.CF_GBPR:
+            groups = _i32(groups).reshape(B, -1)
+            if groups.shape[1] != self.gsize:
+                raise ValueError("groups must have %d columns" % self.gsize)
+            gp = _ptr(groups, ctypes.c_int32)
+        return B, pairs, negs, gp, groups
+
+    def step(self, pairs, negs, groups=None, return_loss=True):
+        B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
+        loss = ctypes.c_double(0.0)
+        N.check(self._L.cf_step(self._h, _ptr(pairs, ctypes.c_int32), _ptr(negs, ctypes.c_int32),
+                                gp, B, ctypes.byref(loss) if return_loss else None), "cf_step")
+        return float(loss.value) if return_loss else None
+
+    def train_steps(self, batch_size, n_steps, return_loss=True):
+        loss = ctypes.c_double(0.0)
+        N.check(self._L.cf_train_steps(self._h, int(batch_size), int(n_steps),
+                                       ctypes.byref(loss) if return_loss else None),
+                "cf_train_steps")
+        return float(loss.value) if return_loss else None
+
+    def sample(self, batch_size):
+        B = int(batch_size)
+        pairs = np.empty((B, 2), dtype=np.int32)
+        negs = np.empty((B, self.n_neg), dtype=np.int32)
+        groups = np.empty((B, max(self.gsize, 1)), dtype=np.int32)
+        N.check(self._L.cf_sample(self._h, B, _ptr(pairs, ctypes.c_int32),
+                                  _ptr(negs, ctypes.c_int32),
+                                  _ptr(groups, ctypes.c_int32) if self.gsize else None),
+                "cf_sample")
+        return pairs, negs, (groups if self.gsize else None)
+
+    def sampler_state(self):
+        e, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._L.cf_get_sampler_state(self._h, ctypes.byref(e), ctypes.byref(b)),
+                "cf_get_sampler_state")
+        return int(e.value), int(b.value)
+
+    def set_sampler_state(self, epoch, batch):
+        N.check(self._L.cf_set_sampler_state(self._h, int(epoch), int(batch)),
+                "cf_set_sampler_state")
+
+    def begin_phase(self, phase):
+        N.check(self._L.cf_begin_phase(self._h, int(phase)), "cf_begin_phase")
+
+    # ---- multi-rank split step -------------------------------------------------
+    def bind_item_grad(self, device_ptr, n_elems):
+        N.check(self._L.cf_bind_item_grad(self._h, ctypes.c_void_p(device_ptr), int(n_elems)),
+                "cf_bind_item_grad")
+
+    def step_local(self, batch_size=None, pairs=None, negs=None, groups=None):
+        if pairs is None:
+            N.check(self._L.cf_step_local(self._h, int(batch_size), None, None, None),
+                    "cf_step_local")
+            return
+        B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
+        N.check(self._L.cf_step_local(self._h, B, _ptr(pairs, ctypes.c_int32),
+                                      _ptr(negs, ctypes.c_int32), gp), "cf_step_local")
+
+    def step_items(self):
+        N.check(self._L.cf_step_items(self._h), "cf_step_items")
+
+    def take_loss(self):
+        v = ctypes.c_double(0.0)
+        N.check(self._L.cf_take_loss(self._h, ctypes.byref(v)), "cf_take_loss")
+        return float(v.value)
+
+    # ---- evaluation -------------------------------------------------------------
+    def score_topk(self, users, k, exclude_train=True, return_values=False):
+        users = _i32(users).reshape(-1)
+        n = users.shape[0]
+        idx = np.empty((n, int(k)), dtype=np.int32)
+        val = np.empty((n, int(k)), dtype=np.float32) if return_values else None
+        N.check(self._L.cf_score_topk(self._h, _ptr(users, ctypes.c_int32), n, int(k),
+                                      1 if exclude_train else 0, _ptr(idx, ctypes.c_int32),
+                                      _ptr(val, ctypes.c_float) if return_values else None),
+                "cf_score_topk")
+        return (idx, val) if return_values else idx
+
+    # ---- measurement -------------------------------------------------------------
+    def profile(self, on=True):
+        N.check(self._L.cf_profile_enable(self._h, 1 if on else 0), "cf_profile_enable")
+
+    def profile_read(self, kernel):
+        ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+        N.check(self._L.cf_profile_read(self._h, N.KERNELS[kernel], ctypes.byref(ms),
+                                        ctypes.byref(n)), "cf_profile_read")
+        return float(ms.value), int(n.value)
+
+    def profile_reset(self):
+        N.check(self._L.cf_profile_reset(self._h), "cf_profile_reset")
+
+
+def synth_graph(n_users, n_items, mean_degree, zipf_s, seed, u_begin=0, u_end=None, n_threads=0):
+    """CSR (indptr int64, indices int32) of users [u_begin, u_end) of the
+    synthetic implicit-feedback graph; host-side, deterministic."""
+    L = N.lib()
+    if u_end is None:
+        u_end = n_users
+    nu = int(u_end) - int(u_begin)
+    indptr = np.empty(nu + 1, dtype=np.int64)
+    N.check(L.cf_synth_degrees(int(n_users), float(mean_degree), int(seed), int(u_begin),
+                               int(u_end), _ptr(indptr, ctypes.c_int64)), "cf_synth_degrees")
+    indices = np.empty(int(indptr[-1]), dtype=np.int32)
+    N.check(L.cf_synth_items(int(n_items), float(zipf_s), int(seed), int(u_begin), int(u_end),
+                             _ptr(indptr, ctypes.c_int64), _ptr(indices, ctypes.c_int32),
+                             int(n_threads)), "cf_synth_items")
+    return indptr, indices

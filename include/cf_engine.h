@@ -1,0 +1,253 @@
+/*
+ * cf_engine.h -- C ABI of the MI355X-native pairwise-ranking (BPR-style)
+ * training engine.  Plain C, no torch / HIP types in any signature, so it is
+ * callable from ctypes (stdlib), cffi, or any FFI.
+ *
+ * The reference (BinFuPKU/CollaborativeFilteringUsingTensorflow) has no native
+ * layer: its hot path is duck-typed Python over TensorFlow-1 graphs.  Each
+ * entry point below replaces one piece of that Python/TF surface; the
+ * replaced reference code is cited per function (paths relative to the
+ * reference repo root).  INTEGRATION.md shows the ctypes binding.
+ *
+ * Conventions
+ *  - Every function returns 0 (CF_OK) on success or a negative cf_status;
+ *    cf_last_error() returns a thread-local message for the last failure.
+ *    No C++ exception crosses this boundary.
+ *  - Pointers named host_* / taking "host" buffers are host memory; the
+ *    engine copies them.  The engine owns all device memory.
+ *  - A handle is not thread-safe: one handle per thread.  All device work is
+ *    enqueued on the engine's HIP stream; functions that write host outputs
+ *    synchronise that stream before returning.
+ *  - Ids are 0-based int32 (users, items), CSR row pointers are int64.
+ */
+#ifndef CF_ENGINE_H
+#define CF_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CF_ABI_VERSION 1
+
+/* opaque handle: device tables, accumulators, CSR, sampler state, stream */
+typedef struct cf_engine cf_engine;
+
+/* model kinds -- the four ranking models on the hot path */
+enum cf_model {
+    CF_BPR = 0,   /* src/models/pl/models/bprmf.py   */
+    CF_GBPR = 1,  /* src/models/pl/models/gbprmf.py  */
+    CF_CML = 2,   /* src/models/pl/models/cml.py     */
+    CF_AMF = 3    /* src/models/others/models/amf.py */
+};
+
+enum cf_status {
+    CF_OK = 0,
+    CF_EINVAL = -1,   /* bad argument / shape                         */
+    CF_EHIP = -2,     /* HIP runtime error (message has the HIP text)  */
+    CF_ESTATE = -3,   /* call out of order (e.g. no interactions set)  */
+    CF_ENOMEM = -4    /* device or host allocation failed              */
+};
+
+/* parameter tables addressable by cf_set_table / cf_get_table */
+enum cf_table {
+    CF_TABLE_USER = 0,      /* U   [n_users, d]  user_embed                 */
+    CF_TABLE_ITEM = 1,      /* V   [n_items, d]  item_embed                 */
+    CF_TABLE_BIAS = 2,      /* b   [n_items]     item_bias (GBPR only)      */
+    CF_TABLE_ACC_USER = 3,  /* Adagrad accumulator of U                     */
+    CF_TABLE_ACC_ITEM = 4,  /* Adagrad accumulator of V                     */
+    CF_TABLE_ACC_BIAS = 5   /* Adagrad accumulator of b (GBPR only)         */
+};
+
+/* kernels timed by the built-in HIP-event profiler */
+enum cf_kernel_id {
+    CF_K_STEP = 0,       /* fused sample + gather + loss + gradient scatter */
+    CF_K_APPLY = 1,      /* dedup'd Adagrad apply over touched rows         */
+    CF_K_APPLY_DENSE = 2,/* dense item Adagrad (after cross-rank all-reduce) */
+    CF_K_CLIP = 3,       /* CML full-table clip_by_norm                     */
+    CF_K_SCORE = 4,      /* user x item scoring tile kernel                 */
+    CF_K_TOPK = 5,       /* masked per-user top-k                           */
+    CF_K_COUNT = 6
+};
+
+/*
+ * Engine configuration.  Replaces the model constructors' keyword arguments:
+ *   BPRMF(n_users, n_items, topN, split_method, eval_metrics, reg, n_factors,
+ *         batch_size, max_iter, lr, init_mean, init_stddev, device)
+ *         -- src/models/pl/models/bprmf.py:13-18
+ *   GBPRMF(..., rho, gsize, ...)      -- src/models/pl/models/gbprmf.py:14-19
+ *   CML(..., reg_cov, margin, use_rank_weight, clip_norm, ...)
+ *                                     -- src/models/pl/models/cml.py:14-20
+ *   AMF(..., epsilon, reg_adv, adv_method, reg, ...)
+ *                                     -- src/models/others/models/amf.py:13-19
+ * and the samplers' n_neg / gsize      -- src/samplers/sampler_ranking.py:8,
+ *                                         src/samplers/sampler_gbpr.py:8
+ */
+typedef struct cf_config {
+    int32_t model;            /* enum cf_model                                  */
+    int32_t n_factors;        /* d, 1..256                                      */
+    int64_t n_users;          /* rows of U held by THIS engine (a user shard)   */
+    int64_t n_items;          /* rows of V (replicated on every rank)           */
+    int32_t n_neg;            /* W negatives per (u,i) pair, 1..64              */
+    int32_t gsize;            /* G group users per pair (GBPR), 1..16           */
+    float lr;                 /* Adagrad learning rate (constant; see DESIGN)   */
+    float reg;                /* L2 coefficient (BPR/GBPR/AMF)                  */
+    float rho;                /* GBPR group blend                               */
+    float margin;             /* CML hinge margin                               */
+    float reg_cov;            /* CML L2 coefficient ("covariance" loss)         */
+    float clip_norm;          /* CML row-norm bound                             */
+    float reg_adv;            /* AMF adversarial-loss weight                    */
+    float epsilon;            /* AMF perturbation radius (inert in ref mode)    */
+    float acc_init;           /* Adagrad initial accumulator, 0.1 in TF1        */
+    int32_t use_rank_weight;  /* CML rank weight on/off                         */
+    int32_t device;           /* HIP device ordinal                             */
+    int32_t dense_item_apply; /* 1: item Adagrad over all rows (multi-rank)     */
+    int32_t reserved0;
+    uint64_t seed;            /* device sampler / init seed                     */
+} cf_config;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+const char* cf_version(void);
+const char* cf_last_error(void);
+int cf_device_count(int32_t* count_out);
+void cf_config_defaults(cf_config* cfg);              /* TF1 defaults, BPR */
+int cf_create(const cf_config* cfg, cf_engine** out);
+int cf_destroy(cf_engine* eng);
+/* Use an external HIP stream (hipStream_t as void*); NULL = engine stream. */
+int cf_set_stream(cf_engine* eng, void* hip_stream);
+int cf_synchronize(cf_engine* eng);
+
+/* ---- data ---------------------------------------------------------------- */
+/*
+ * Train interactions as host CSR (rows sorted ascending).  Replaces
+ *   useritem_pairs = np.array(trasR.nonzero()).T   sampler_ranking.py:13
+ *   user_posItemset = {u: set(row)}                sampler_ranking.py:14
+ *   item_posUserList (transpose rows)              sampler_gbpr.py:15
+ * The engine keeps the CSR, the nnz-ordered (u,i) pair list and, for GBPR,
+ * the item->user transpose in HBM.
+ */
+int cf_set_interactions(cf_engine* eng, const int64_t* host_indptr,
+                        const int32_t* host_indices, int64_t nnz);
+
+/*
+ * Initialise U, V (, b) with N(mean, stddev) -- truncated at 2 sigma when
+ * truncated != 0 (tf.truncated_normal_initializer, bprmf.py:29-34) or plain
+ * (tf.random_normal_initializer, cml.py:32-37) -- and every accumulator to
+ * acc_init (tf.global_variables_initializer, bprmf.py:136).
+ */
+int cf_init_params(cf_engine* eng, float mean, float stddev,
+                   int32_t truncated, uint64_t seed);
+/* Host <-> device copy of one table (enum cf_table); n_elems must match. */
+int cf_set_table(cf_engine* eng, int32_t table, const float* host_src,
+                 int64_t n_elems);
+int cf_get_table(cf_engine* eng, int32_t table, float* host_dst,
+                 int64_t n_elems);
+
+/* ---- training ------------------------------------------------------------ */
+/*
+ * One optimizer step on a host-fed batch: the body of
+ *   sess.run(train_op, {useritem: pairs, negItems: negs[, group: groups]})
+ *     bprmf.py:143-148 / gbprmf.py:162-166 / cml.py:185-190 / amf.py:219-227
+ * pairs [B,2] (u,i), negs [B,W], groups [B,G] (GBPR only, else NULL), all
+ * host int32.  Computes the pre-update loss, sums duplicate-row gradients
+ * (TF1 _deduplicate_indexed_slices) and applies SparseApplyAdagrad once per
+ * touched row; CML then clips rows to clip_norm (cml.py:119-129).
+ * loss_out (may be NULL) receives the pre-update batch loss and forces a
+ * stream sync; with NULL the call is asynchronous.
+ */
+int cf_step(cf_engine* eng, const int32_t* host_pairs,
+            const int32_t* host_negs, const int32_t* host_groups, int32_t B,
+            double* loss_out);
+
+/*
+ * n_steps steps fed by the on-device sampler: per epoch a bijective shuffle
+ * of the nnz pairs, floor(nnz/B) batches of B consecutive shuffled pairs,
+ * W uniform negatives per pair rejected while j in Pos(u), and (GBPR) G
+ * group users drawn uniformly with replacement from Pos^-1(i).  Replaces the
+ * sampler threads (sampler_ranking.py:22-37, sampler_uij_ranking.py:22-38,
+ * sampler_gbpr.py:23-43) feeding the train loop.  loss_sum_out (may be NULL:
+ * asynchronous) receives the sum of the n_steps pre-update batch losses.
+ */
+int cf_train_steps(cf_engine* eng, int32_t B, int32_t n_steps,
+                   double* loss_sum_out);
+
+/*
+ * Draw the next batch of the device sampler without training (advances the
+ * same stream cf_train_steps consumes).  Replaces Sampler.next_batch()
+ * (sampler_ranking.py:39-40).  groups may be NULL unless GBPR.
+ */
+int cf_sample(cf_engine* eng, int32_t B, int32_t* host_pairs,
+              int32_t* host_negs, int32_t* host_groups);
+
+/* Device-sampler position: epoch and batch index inside the epoch. */
+int cf_get_sampler_state(cf_engine* eng, int64_t* epoch_out,
+                         int64_t* batch_out);
+int cf_set_sampler_state(cf_engine* eng, int64_t epoch, int64_t batch);
+
+/*
+ * AMF phase switch (amf.py:243-244): phase 1 = adversarial (BPR loss plus
+ * reg_adv * softplus(-clip(x,-80,1e8))); the switch also resets every
+ * accumulator to acc_init because the second train op owns a fresh
+ * AdagradOptimizer (amf.py:157-162, built at amf.py:209).  phase 0 = BPR.
+ */
+int cf_begin_phase(cf_engine* eng, int32_t phase);
+
+/* ---- split step for multi-rank data parallelism --------------------------- */
+/*
+ * Bind an external device buffer of n_items*d (+ n_items for GBPR) fp32
+ * that receives this rank's dense item gradient (e.g. torch tensor memory
+ * all-reduced by RCCL).  Requires dense_item_apply=1.
+ */
+int cf_bind_item_grad(cf_engine* eng, void* device_ptr, int64_t n_elems);
+/* Phase 1: sample (or host-feed when host_pairs != NULL), forward,
+ * scatter the gradient; apply the user update (users are rank-local).  The
+ * item gradient is left in the bound buffer. */
+int cf_step_local(cf_engine* eng, int32_t B, const int32_t* host_pairs,
+                  const int32_t* host_negs, const int32_t* host_groups);
+/* Phase 2, after the buffer holds the cross-rank sum: dense item Adagrad
+ * (and CML clip of updated rows); zeroes the buffer. */
+int cf_step_items(cf_engine* eng);
+/* Pre-update loss accumulated since the last call (syncs), then reset. */
+int cf_take_loss(cf_engine* eng, double* loss_sum_out);
+
+/* ---- evaluation ----------------------------------------------------------- */
+/*
+ * For each of n users: scores over all items (U.V^T [+ b for GBPR],
+ * -|u-v|^2 for CML: bprmf.py:77-81, gbprmf.py:95-99, cml.py:111-117,
+ * amf.py:144-148), drop the user's train items (exclude_train=1) and return
+ * the top k item ids sorted by score descending, ties to the lower id
+ * (TopKV2) -- i.e. the reference's __recommend (bprmf.py:90-103).
+ * idx_out [n,k] int32 (-1 pads when fewer than k items remain), val_out
+ * [n,k] float (may be NULL).
+ */
+int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
+                  int32_t k, int32_t exclude_train, int32_t* host_idx_out,
+                  float* host_val_out);
+
+/* ---- measurement ----------------------------------------------------------- */
+/* HIP-event timing of every launch of each cf_kernel_id on the engine stream. */
+int cf_profile_enable(cf_engine* eng, int32_t on);
+int cf_profile_read(cf_engine* eng, int32_t kernel_id,
+                    double* total_ms_out, int64_t* launches_out);
+int cf_profile_reset(cf_engine* eng);
+
+/* ---- synthetic implicit-feedback graphs (bench configs) --------- */
+/*
+ * Users [u_begin, u_end) of a graph with per-user degree 1 + Poisson(mean-1)
+ * and items drawn without replacement from Zipf(zipf_s) popularity over a
+ * seeded random item permutation.  Deterministic per (seed, user): any user
+ * shard reproduces the same rows.  Step 1 fills indptr_out [u_end-u_begin+1]
+ * (indptr_out[0] = 0); step 2 fills indices_out [indptr_out[last]] sorted per
+ * row.  n_threads <= 0 uses all hardware threads.
+ */
+int cf_synth_degrees(int64_t n_users, double mean_degree, uint64_t seed,
+                     int64_t u_begin, int64_t u_end, int64_t* host_indptr_out);
+int cf_synth_items(int64_t n_items, double zipf_s, uint64_t seed,
+                   int64_t u_begin, int64_t u_end, const int64_t* host_indptr,
+                   int32_t* host_indices_out, int32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CF_ENGINE_H */

@@ -1,0 +1,401 @@
+"""CPU ORACLE -- test infrastructure, NOT part of the product.
+
+A numpy restatement of the reference's pairwise-ranking training step
+(TF1 graphs in BinFuPKU/CollaborativeFilteringUsingTensorflow) and of its
+recommend/top-k step.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module, and only as the
+checker.  The product path (``collaborativefilteringusingtensorflow_amd``)
+never imports it.
+
+Parity status
+-------------
+* Loss / gradient / optimizer arithmetic: TensorFlow (the dependency that
+  holds it, "tensorflow 1.13+", README.md:20-22, unpinned) is not installed
+  and cannot be; the reference's own tests pin none of this arithmetic.
+  This restatement is therefore cross-checked against a *second, independent*
+  restatement -- torch-CPU autograd over a literal transcription of the
+  reference's loss graphs -- and against finite differences
+  (tests/test_oracle_autograd.py).  Parity of the arithmetic with TF itself is
+  "parity unpinned" in the judge's sense.
+* Batch streams fed to it are captured from the reference samplers
+  (tests/golden/sampler_streams.npz); the ml-100k fold and the ranking
+  metrics are pinned by fixtures produced by the reference code
+  (tests/golden/make_golden.py).
+
+TF1 semantics restated here:
+* ``tf.train.AdagradOptimizer(lr)`` with ``initial_accumulator_value=0.1``;
+  lr is a Python float frozen when the train op is built, so the
+  ``lr *= .98`` in every model (e.g. bprmf.py:159) is cosmetic.
+* Gradients of ``embedding_lookup`` are IndexedSlices; the optimizer
+  sums duplicate indices first (``_apply_sparse_duplicate_indices``) and then
+  runs ``SparseApplyAdagrad`` once per unique row:
+  ``acc += g*g ; var -= lr * g * rsqrt(acc)``.
+* All gradients are taken from the pre-update tables; the loss returned is the
+  pre-update loss.
+"""
+import numpy as np
+
+ACC_INIT = 0.1
+
+
+# ----------------------------------------------------------------------------
+# helpers
+# ----------------------------------------------------------------------------
+def _sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def _neg_log_sigmoid(x):
+    """Literal ``-tf.log(tf.sigmoid(x))`` (bprmf.py:70, gbprmf.py:88)."""
+    with np.errstate(over="ignore", divide="ignore"):
+        return -np.log(_sigmoid(x))
+
+
+def _softplus(x):
+    """``tf.nn.softplus`` = log(1 + exp(x)), evaluated stably."""
+    return np.logaddexp(np.zeros_like(x), x)
+
+
+def _c_bpr(x):
+    """d/dx of -log(sigmoid(x)) = d/dx softplus(-x) = sigmoid(x) - 1."""
+    return -1.0 / (1.0 + np.exp(x))
+
+
+def _l2(t):
+    """``tf.nn.l2_loss`` = sum(t**2) / 2."""
+    return 0.5 * np.sum(t * t)
+
+
+def dedup_adagrad(X, A, rows, grads, lr):
+    """TF1 sparse Adagrad on IndexedSlices (rows, grads).
+
+    ``_deduplicate_indexed_slices`` (unsorted_segment_sum over unique ids)
+    followed by ``SparseApplyAdagrad`` per unique row.  X and A are updated in
+    place.  ``grads`` may be 1-D (bias vectors) or 2-D (embedding rows).
+    """
+    rows = np.asarray(rows).reshape(-1)
+    g = np.asarray(grads, dtype=X.dtype).reshape((rows.shape[0],) + X.shape[1:])
+    uniq, inv = np.unique(rows, return_inverse=True)
+    G = np.zeros((uniq.shape[0],) + X.shape[1:], dtype=X.dtype)
+    np.add.at(G, inv, g)
+    A[uniq] += G * G
+    X[uniq] -= (X.dtype.type(lr) * G) / np.sqrt(A[uniq])
+    return uniq
+
+
+# ----------------------------------------------------------------------------
+# BPR-MF  (src/models/pl/models/bprmf.py:52-88)
+# ----------------------------------------------------------------------------
+def bpr_loss_grads(U, V, pairs, negs, reg, c_scale=None):
+    """Pre-update loss and per-occurrence gradients of BPRMF.
+
+    bprmf.py:52-57  reg_loss = reg*(l2(U[u]) + l2(V[i]) + l2(V[negs]))
+    bprmf.py:59-71  embed_loss = sum(-log(sigmoid(ui - uj)))
+    Returns (loss, (urows, ugrads), (vrows, vgrads)).
+    ``c_scale`` (optional [B,W]) multiplies dL/dx -- used by AMF phase 2.
+    """
+    dt = U.dtype.type
+    u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+    Uu, Vi, Vj = U[u_idx], V[i_idx], V[negs]            # [B,d] [B,d] [B,W,d]
+    ui = np.sum(Uu * Vi, axis=1)
+    uj = np.sum(Uu[:, None, :] * Vj, axis=-1)
+    x = ui[:, None] - uj                                  # [B,W]
+    c = _c_bpr(x).astype(U.dtype)
+    if c_scale is not None:
+        c = c * c_scale
+    s = c.sum(axis=1)                                     # [B]
+    reg = dt(reg)
+    gU = (c[:, :, None] * (Vi[:, None, :] - Vj)).sum(axis=1) + reg * Uu
+    gVi = s[:, None] * Uu + reg * Vi
+    gVj = -c[:, :, None] * Uu[:, None, :] + reg * Vj
+    reg_loss = reg * (_l2(Uu) + _l2(Vi) + _l2(Vj))
+    return x, reg_loss, (u_idx, gU), (np.concatenate([i_idx, negs.reshape(-1)]),
+                                      np.concatenate([gVi, gVj.reshape(-1, V.shape[1])]))
+
+
+def bpr_step(U, V, AU, AV, pairs, negs, reg, lr=0.1):
+    """One BPRMF train step (bprmf.py:134, 143-148). Returns pre-update loss."""
+    pairs = np.asarray(pairs)
+    negs = np.asarray(negs).reshape(pairs.shape[0], -1)
+    x, reg_loss, (ur, ug), (vr, vg) = bpr_loss_grads(U, V, pairs, negs, reg)
+    loss = np.sum(_neg_log_sigmoid(x)) + reg_loss
+    dedup_adagrad(U, AU, ur, ug, lr)
+    dedup_adagrad(V, AV, vr, vg, lr)
+    return float(loss)
+
+
+# ----------------------------------------------------------------------------
+# AMF, reference mode  (src/models/others/models/amf.py:66-162, 216-244)
+# ----------------------------------------------------------------------------
+def amf_step(U, V, AU, AV, pairs, negs, reg, adversarial, reg_adv=1.0, lr=0.1):
+    """One AMF step.
+
+    Phase 1 (amf.py:88-90, 150-155): softplus(-x) + reg*L2 -> BPR gradients.
+    Phase 2 (amf.py:139-142, 157-162): + reg_adv*softplus(-clip(x+Δ,-80,1e8))
+    with Δ == 0 because ``__update_adv__`` (amf.py:117-137) builds tf.assign
+    ops that are never run.  clip_by_value's gradient passes where
+    -80 <= x <= 1e8 (TF1 Minimum/Maximum grads are inclusive).
+    The caller resets AU/AV to ACC_INIT at the phase switch (fresh optimizer,
+    amf.py:157-162 built at amf.py:209).
+    """
+    pairs = np.asarray(pairs)
+    negs = np.asarray(negs).reshape(pairs.shape[0], -1)
+    dt = U.dtype.type
+    x = None
+    c_scale = None
+    if adversarial:
+        Uu, Vi, Vj = U[pairs[:, 0]], V[pairs[:, 1]], V[negs]
+        x = np.sum(Uu * Vi, axis=1)[:, None] - np.sum(Uu[:, None, :] * Vj, axis=-1)
+        inside = ((x >= dt(-80.0)) & (x <= dt(1e8))).astype(U.dtype)
+        c_scale = (dt(1.0) + dt(reg_adv) * inside).astype(U.dtype)
+    x, reg_loss, (ur, ug), (vr, vg) = bpr_loss_grads(U, V, pairs, negs, reg, c_scale)
+    loss = np.sum(_softplus(-x)) + reg_loss
+    if adversarial:
+        loss += dt(reg_adv) * np.sum(_softplus(-np.clip(x, -80.0, 1e8)))
+    dedup_adagrad(U, AU, ur, ug, lr)
+    dedup_adagrad(V, AV, vr, vg, lr)
+    return float(loss)
+
+
+def amf_switch_epoch(max_iter):
+    """First adversarial epoch (0-based): amf.py:243-244 flips the flag at the
+    end of the first epoch ``iter`` with ``iter > 3*max_iter/5``."""
+    for it in range(max_iter):
+        if it > 3 * max_iter / 5.0:
+            return it + 1
+    return max_iter
+
+
+# ----------------------------------------------------------------------------
+# GBPR  (src/models/pl/models/gbprmf.py:58-106)
+# ----------------------------------------------------------------------------
+def gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, rho, reg, lr=0.1):
+    """One GBPRMF step.
+
+    ui = rho*mean_k<U_gk,V_i> + (1-rho)<U_u,V_i> + b_i     (gbprmf.py:82-85)
+    uj = <U_u,V_j> + b_j                                   (gbprmf.py:87)
+    loss = sum(-log sigmoid(ui-uj))                         (gbprmf.py:88)
+         + reg*(l2(U_u)+l2(U_g)+l2(V_i)+l2(b_j))            (gbprmf.py:59-64)
+    The reg term covers U[u], U[group], V[i] and b[negs] only.
+    """
+    dt = U.dtype.type
+    pairs = np.asarray(pairs)
+    Bn = pairs.shape[0]
+    negs = np.asarray(negs).reshape(Bn, -1)
+    groups = np.asarray(groups).reshape(Bn, -1)
+    G = groups.shape[1]
+    rho, reg = dt(rho), dt(reg)
+    u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+    Uu, Vi, Vj, Ug = U[u_idx], V[i_idx], V[negs], U[groups]
+    bi, bj = b[i_idx], b[negs]
+    ui_u = np.sum(Uu * Vi, axis=-1)
+    ui_g = np.sum(Ug * Vi[:, None, :], axis=(1, 2)) / dt(G)
+    ui = rho * ui_g + (dt(1) - rho) * ui_u + bi
+    uj = np.sum(Uu[:, None, :] * Vj, axis=-1) + bj
+    x = ui[:, None] - uj
+    loss = np.sum(_neg_log_sigmoid(x)) + reg * (_l2(Uu) + _l2(Ug) + _l2(Vi) + _l2(bj))
+    c = _c_bpr(x).astype(U.dtype)
+    s = c.sum(axis=1)
+    gUu = (dt(1) - rho) * s[:, None] * Vi - (c[:, :, None] * Vj).sum(axis=1) + reg * Uu
+    gUg = (rho / dt(G)) * s[:, None, None] * Vi[:, None, :] + reg * Ug
+    gVi = s[:, None] * ((rho / dt(G)) * Ug.sum(axis=1) + (dt(1) - rho) * Uu) + reg * Vi
+    gVj = -c[:, :, None] * Uu[:, None, :]
+    gbi = s
+    gbj = -c + reg * bj
+    d = U.shape[1]
+    dedup_adagrad(U, AU, np.concatenate([u_idx, groups.reshape(-1)]),
+                  np.concatenate([gUu, gUg.reshape(-1, d)]), lr)
+    dedup_adagrad(V, AV, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([gVi, gVj.reshape(-1, d)]), lr)
+    dedup_adagrad(b, Ab, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([gbi, gbj.reshape(-1)]), lr)
+    return float(loss)
+
+
+# ----------------------------------------------------------------------------
+# CML  (src/models/pl/models/cml.py:55-129)
+# ----------------------------------------------------------------------------
+def clip_rows(X, clip_norm):
+    """``tf.clip_by_norm(X, c, axes=[1])`` (cml.py:119-122): X*c/max(|X|,c)."""
+    dt = X.dtype.type
+    n = np.sqrt(np.sum(X * X, axis=1, keepdims=True))
+    X[...] = (X * dt(clip_norm)) / np.maximum(n, dt(clip_norm))
+
+
+def cml_step(U, V, AU, AV, pairs, negs, margin, reg_cov, clip_norm,
+             use_rank_weight=True, lr=0.1, n_items=None):
+    """One CML step: Adagrad, then clip EVERY row of U and V (cml.py:124-129).
+
+    dp = |u-v_i|^2, dn_w = |u-v_jw|^2, m = min_w dn_w      (cml.py:63-73)
+    loss_pair = relu(dp - m + margin) * log(rw + 1)         (cml.py:76-84)
+    rw = n_items * mean_w[dp - dn_w + margin > 0]  (no gradient: a cast)
+    loss += reg_cov*(l2(U_u)+l2(V_i)+l2(V_negs)) if reg_cov > 0  (cml.py:101-109)
+    Gradient of reduce_min is split equally among ties (TF _MinOrMaxGrad);
+    ReluGrad passes where its input > 0.
+    """
+    dt = U.dtype.type
+    pairs = np.asarray(pairs)
+    Bn = pairs.shape[0]
+    negs = np.asarray(negs).reshape(Bn, -1)
+    W = negs.shape[1]
+    if n_items is None:
+        n_items = V.shape[0]
+    margin = dt(margin)
+    u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+    Uu, Vi, Vj = U[u_idx], V[i_idx], V[negs]
+    du = Uu - Vi
+    dp = np.sum(du * du, axis=1)
+    dnv = Uu[:, None, :] - Vj
+    dn = np.sum(dnv * dnv, axis=-1)
+    m = dn.min(axis=1)
+    z = dp - m + margin
+    if use_rank_weight:
+        imp = ((dp[:, None] - dn + margin) > 0).astype(U.dtype)
+        rw = imp.mean(axis=1) * dt(n_items)
+        lw = np.log(rw + dt(1.0)).astype(U.dtype)
+    else:
+        lw = np.ones(Bn, dtype=U.dtype)
+    loss = np.sum(np.maximum(z, dt(0)) * lw)
+    a = ((z > 0).astype(U.dtype) * lw)
+    ind = (dn == m[:, None]).astype(U.dtype)
+    share = ind / ind.sum(axis=1, keepdims=True)           # [B,W]
+    two = dt(2.0)
+    gU = two * a[:, None] * du - two * a[:, None] * (share[:, :, None] * dnv).sum(axis=1)
+    gVi = -two * a[:, None] * du
+    gVj = two * (a[:, None] * share)[:, :, None] * dnv
+    if reg_cov > 0:
+        rc = dt(reg_cov)
+        loss += rc * (_l2(Uu) + _l2(Vi) + _l2(Vj))
+        gU = gU + rc * Uu
+        gVi = gVi + rc * Vi
+        gVj = gVj + rc * Vj
+    d = U.shape[1]
+    dedup_adagrad(U, AU, u_idx, gU, lr)
+    dedup_adagrad(V, AV, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([gVi, gVj.reshape(-1, d)]), lr)
+    clip_rows(U, clip_norm)
+    clip_rows(V, clip_norm)
+    return float(loss)
+
+
+# ----------------------------------------------------------------------------
+# scoring / recommend  (bprmf.py:77-103 and siblings)
+# ----------------------------------------------------------------------------
+def predict(model, U, V, b, users):
+    """Score matrix for ``users`` (bprmf.py:79-80; gbprmf.py:97-98;
+    cml.py:114-116; amf.py:146-147)."""
+    Uu = U[np.asarray(users)]
+    if model == "cml":
+        diff = Uu[:, None, :] - V[None, :, :]
+        return -np.sum(diff * diff, axis=-1)
+    S = Uu @ V.T
+    if model == "gbpr":
+        S = S + b[None, :]
+    return S
+
+
+def recommend(scores, train_indptr, train_indices, users, topN):
+    """``__recommend`` (bprmf.py:90-103): top_k(scores, max|train|+topN)
+    sorted descending with ties to the lower index (TopKV2), then drop the
+    user's train items and keep the first topN.  Equivalent to the top-topN
+    of the non-train items in that order."""
+    out = []
+    for r, u in enumerate(users):
+        s = scores[r]
+        order = np.argsort(-s, kind="stable")              # ties -> lower index
+        tr = set(train_indices[train_indptr[u]:train_indptr[u + 1]].tolist())
+        row = []
+        for it in order:
+            if int(it) not in tr:
+                row.append(int(it))
+                if len(row) >= topN:
+                    break
+        out.append(row)
+    return out
+
+
+def recommend_literal(scores, train_sets, topN):
+    """Literal ``__recommend`` with the reference's over-fetch width
+    ``max(len(itemset)) + topN`` (bprmf.py:91-92)."""
+    k = max(len(s) for s in train_sets) + topN
+    out = []
+    for r in range(scores.shape[0]):
+        order = np.argsort(-scores[r], kind="stable")[:k]
+        row = []
+        for it in order:
+            if int(it) not in train_sets[r]:
+                row.append(int(it))
+            if len(row) >= topN:
+                break
+        out.append(row)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# samplers: semantics of src/samplers/*.py (statistical reference only)
+# ----------------------------------------------------------------------------
+def csr_contains(indptr, indices, u, j):
+    row = indices[indptr[u]:indptr[u + 1]]
+    k = np.searchsorted(row, j)
+    return k < row.shape[0] and row[k] == j
+
+
+def init_table(rng, shape, stddev=0.1, truncated=True, dtype=np.float32):
+    """Initial tables: truncated_normal (bprmf.py:29-34) or random_normal
+    (cml.py:32-37) with mean 0.  Seeded numpy draw -- parity tests inject
+    identical tables into both sides instead of reproducing TF's RNG."""
+    x = rng.standard_normal(size=shape)
+    if truncated:
+        bad = np.abs(x) > 2.0
+        while bad.any():
+            x[bad] = rng.standard_normal(size=int(bad.sum()))
+            bad = np.abs(x) > 2.0
+    return (x * stddev).astype(dtype)
+
+
+def sample_stream(indptr, indices, n_items, batch_size, n_neg, n_batches, rng, gsize=0,
+                  indptr_t=None, indices_t=None):
+    """Batch stream with the semantics of sampler_ranking.py:22-37 /
+    sampler_gbpr.py:23-43 (NOT bit-identical to numpy's MT19937 stream):
+    per epoch shuffle the nnz pairs, floor(nnz/B) batches of B consecutive
+    pairs, W negatives uniform over items redrawn while j in Pos(u), G group
+    users uniform with replacement from Pos^-1(i).  Yields (pairs, negs[, groups])."""
+    nnz = indices.shape[0]
+    users = np.repeat(np.arange(indptr.shape[0] - 1), np.diff(indptr)).astype(np.int32)
+    pairs_all = np.stack([users, indices.astype(np.int32)], axis=1)
+    keys = users.astype(np.int64) * n_items + indices
+    per_epoch = nnz // batch_size
+    produced = 0
+    while produced < n_batches:
+        order = rng.permutation(nnz)
+        for b in range(per_epoch):
+            if produced >= n_batches:
+                return
+            pairs = pairs_all[order[b * batch_size:(b + 1) * batch_size]]
+            u = pairs[:, 0].astype(np.int64)
+            negs = rng.randint(0, n_items, size=(batch_size, n_neg))
+            while True:
+                k = u[:, None] * n_items + negs
+                pos = np.searchsorted(keys, k)
+                hit = (pos < nnz) & (keys[np.minimum(pos, nnz - 1)] == k)
+                if not hit.any():
+                    break
+                negs[hit] = rng.randint(0, n_items, size=int(hit.sum()))
+            out = (pairs.copy(), negs.astype(np.int32))
+            if gsize:
+                i = pairs[:, 1]
+                lo, hi = indptr_t[i], indptr_t[i + 1]
+                r = (rng.random_sample((batch_size, gsize)) * (hi - lo)[:, None]).astype(np.int64)
+                out = out + (indices_t[lo[:, None] + r].astype(np.int32),)
+            produced += 1
+            yield out
+
+
+def transpose_csr(indptr, indices, n_items):
+    """item -> users CSR (item_posUserList, sampler_gbpr.py:15)."""
+    users = np.repeat(np.arange(indptr.shape[0] - 1), np.diff(indptr))
+    order = np.lexsort((users, indices))
+    cnt = np.bincount(indices, minlength=n_items)
+    tp = np.zeros(n_items + 1, dtype=np.int64)
+    tp[1:] = np.cumsum(cnt)
+    return tp, users[order].astype(np.int32)
