@@ -194,7 +194,7 @@ def main():
     log("rank %d: loss accumulated %.4e over %d steps" % (rank, loss, args.warmup + args.steps))
 
     kernels = {}
-    for kname in ("step", "apply", "apply_dense", "clip"):
+    for kname in ("sample", "step", "apply", "apply_dense", "clip"):
         ms, n = eng.profile_read(kname)
         if n:
             kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}
@@ -206,7 +206,8 @@ def main():
                                bias=cfg["model"] == "gbpr") * B
     achieved = gb / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
     traffic = load_pmc(args.config, world)
-    roofline = {"kernel": "step_kernel (fused sample+gather+loss+scatter)", "bound": "hbm",
+    roofline = {"kernel": "grad_kernel (gather + loss + grads + singleton-row Adagrad)",
+                "bound": "hbm",
                 "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                 "traffic": traffic,

@@ -76,13 +76,12 @@ struct cf_engine {
     float *AU = nullptr, *AV = nullptr, *Ab = nullptr;
     float *GU = nullptr, *GV = nullptr, *Gb = nullptr;
     float *GV_own = nullptr, *Gb_own = nullptr;
-    uint32_t *markU = nullptr, *markV = nullptr;
-    uint32_t stamp = 0;
+    int32_t *cntU = nullptr, *cntV = nullptr;  // per-row occurrence counts (0 between steps)
 
     // batch
     int Bcap = 0;
     int32_t *occU = nullptr, *occV = nullptr;
-    uint8_t *flagU = nullptr, *flagV = nullptr;
+    int32_t *rankU = nullptr, *rankV = nullptr;
     double* loss_partial = nullptr;
     double* loss = nullptr;   // [0] running accumulator, [1] per-call scratch
     double* h_loss = nullptr; // pinned
@@ -150,18 +149,16 @@ int ensure_batch(cf_engine* e, int B) {
     if (B <= e->Bcap) return CF_OK;
     dfree(e->occU);
     dfree(e->occV);
-    dfree(e->flagU);
-    dfree(e->flagV);
+    dfree(e->rankU);
+    dfree(e->rankV);
     dfree(e->loss_partial);
     const size_t nU = (size_t)B * users_per_pair(e->cfg);
     const size_t nV = (size_t)B * items_per_pair(e->cfg);
     CF_TRY(dalloc(&e->occU, nU));
     CF_TRY(dalloc(&e->occV, nV));
-    CF_TRY(dalloc(&e->flagU, nU));
-    CF_TRY(dalloc(&e->flagV, nV));
-    CF_HIP(hipMemsetAsync(e->flagU, 0, nU, e->stream));
-    CF_HIP(hipMemsetAsync(e->flagV, 0, nV, e->stream));
-    CF_TRY(dalloc(&e->loss_partial, (size_t)(B + kPairsPerBlock - 1) / kPairsPerBlock));
+    CF_TRY(dalloc(&e->rankU, nU));
+    CF_TRY(dalloc(&e->rankV, nV));
+    CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks(B)));
     e->Bcap = B;
     return CF_OK;
 }
@@ -188,32 +185,22 @@ StepArgs base_step_args(cf_engine* e, int B) {
     a.indices = e->indices;
     a.indptr_t = e->indptr_t;
     a.indices_t = e->indices_t;
-    a.U = e->U;
-    a.V = e->V;
-    a.b = e->b;
-    a.GU = e->GU;
-    a.GV = e->GV;
-    a.Gb = e->Gb;
+    a.U = e->U; a.AU = e->AU; a.GU = e->GU;
+    a.V = e->V; a.AV = e->AV; a.GV = e->GV;
+    a.b = e->b; a.Ab = e->Ab; a.Gb = e->Gb;
+    a.lr = c.lr;
+    a.clip_norm = c.clip_norm;
+    a.clip = c.model == CF_CML ? 1 : 0;
     a.occU = e->occU;
     a.occV = e->occV;
-    a.flagU = e->flagU;
-    a.flagV = e->flagV;
-    a.markU = e->markU;
-    a.markV = e->markV;
+    a.rankU = e->rankU;
+    a.rankV = e->rankV;
+    a.cntU = e->cntU;
+    a.cntV = e->cntV;
     a.loss_partial = e->loss_partial;
-    a.grads = 1;
-    a.mark_users = 1;
-    a.mark_items = c.dense_item_apply ? 0 : 1;
+    a.count_users = 1;
+    a.count_items = c.dense_item_apply ? 0 : 1;
     return a;
-}
-
-int next_stamp(cf_engine* e) {
-    if (++e->stamp == 0) {
-        CF_HIP(hipMemsetAsync(e->markU, 0, (size_t)e->cfg.n_users * sizeof(uint32_t), e->stream));
-        CF_HIP(hipMemsetAsync(e->markV, 0, (size_t)e->cfg.n_items * sizeof(uint32_t), e->stream));
-        e->stamp = 1;
-    }
-    return CF_OK;
 }
 
 // position the device sampler for the next batch of B pairs
@@ -288,26 +275,23 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
 
 // step kernel + user (and, in sparse mode, item) apply; loss added to *loss_acc
 int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
-             const int32_t* groups, double* loss_acc, bool apply_items_dense_now) {
+             const int32_t* groups, double* loss_acc) {
     const cf_config& c = e->cfg;
     CF_TRY(ensure_batch(e, B));
     StepArgs a = base_step_args(e, B);
-    a.occU = e->occU;
-    a.occV = e->occV;
-    a.flagU = e->flagU;
-    a.flagV = e->flagV;
-    a.loss_partial = e->loss_partial;
     if (pairs) {
         CF_TRY(stage_host_batch(e, pairs, negs, groups, B));
         a.sample = 0;
     } else {
         CF_TRY(sampler_args(e, B, &a));
     }
-    CF_TRY(next_stamp(e));
-    a.stamp = e->stamp;
+    {
+        ProfScope ps(e, CF_K_SAMPLE);
+        CF_HIP(launch_prep(a, e->stream));
+    }
     {
         ProfScope ps(e, CF_K_STEP);
-        CF_HIP(launch_step(a, e->stream));
+        CF_HIP(launch_grad(a, e->stream));
     }
     ApplyArgs p{};
     p.d = c.n_factors;
@@ -320,14 +304,16 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
     p.blocksU = (p.nU + per_block - 1) / per_block;
     p.occU = e->occU;
     p.occV = e->occV;
-    p.flagU = e->flagU;
-    p.flagV = e->flagV;
+    p.rankU = e->rankU;
+    p.rankV = e->rankV;
+    p.cntU = e->cntU;
+    p.cntV = e->cntV;
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
     p.V = e->V; p.AV = e->AV; p.GV = e->GV;
     p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
     p.apply_items = c.dense_item_apply ? 0 : 1;
     p.loss_partial = e->loss_partial;
-    p.n_partial = (B + kPairsPerBlock - 1) / kPairsPerBlock;
+    p.n_partial = grad_blocks(B);
     p.loss_acc = loss_acc;
     {
         ProfScope ps(e, CF_K_APPLY);
@@ -344,9 +330,6 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
             CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
             e->need_clip_V = false;
         }
-    } else if (apply_items_dense_now) {
-        // single-rank dense mode: no all-reduce between the two phases
-        (void)0;
     }
     return CF_OK;
 }
@@ -450,6 +433,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         return fail(CF_EINVAL, "gsize must be 1..16");
     if (!(c.lr > 0.f) || !(c.acc_init > 0.f)) return fail(CF_EINVAL, "lr and acc_init must be > 0");
     if (c.model == CF_CML && !(c.clip_norm > 0.f)) return fail(CF_EINVAL, "clip_norm must be > 0");
+    if (c.model == CF_CML && c.n_neg > 16) return fail(CF_EINVAL, "CML supports n_neg <= 16");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(CF_EHIP, "no HIP device visible (the engine has no CPU fallback)");
@@ -473,7 +457,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     const size_t ud = (size_t)c.n_users * c.n_factors, id = (size_t)c.n_items * c.n_factors;
     if ((r = dalloc(&e->U, ud)) || (r = dalloc(&e->AU, ud)) || (r = dalloc(&e->GU, ud)) ||
         (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
-        (r = dalloc(&e->markU, (size_t)c.n_users)) || (r = dalloc(&e->markV, (size_t)c.n_items)) ||
+        (r = dalloc(&e->cntU, (size_t)c.n_users)) || (r = dalloc(&e->cntV, (size_t)c.n_items)) ||
         (r = dalloc(&e->loss, 2)))
         return bail(r);
     if (c.model == CF_GBPR) {
@@ -490,8 +474,8 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         hipMemsetAsync(e->GV, 0, id * 4, s) != hipSuccess ||
         hipMemsetAsync(e->U, 0, ud * 4, s) != hipSuccess ||
         hipMemsetAsync(e->V, 0, id * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->markU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->markV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
         hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
         return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
     if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
@@ -521,8 +505,8 @@ int cf_destroy(cf_engine* e) {
     for (auto x : e->ev_pool) (void)hipEventDestroy(x);
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
-    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own); dfree(e->markU); dfree(e->markV);
-    dfree(e->occU); dfree(e->occV); dfree(e->flagU); dfree(e->flagV);
+    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own); dfree(e->cntU); dfree(e->cntV);
+    dfree(e->occU); dfree(e->occV); dfree(e->rankU); dfree(e->rankV);
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -652,7 +636,7 @@ int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32
     if (e->cfg.dense_item_apply && e->GV != e->GV_own)
         return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
     double* acc = loss_out ? e->loss + 1 : e->loss;
-    CF_TRY(run_step(e, B, pairs, negs, groups, acc, true));
+    CF_TRY(run_step(e, B, pairs, negs, groups, acc));
     if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
     if (loss_out) CF_TRY(read_loss(e, 1, loss_out));
     return CF_OK;
@@ -665,7 +649,7 @@ int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_ou
         return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
     double* acc = loss_sum_out ? e->loss + 1 : e->loss;
     for (int s = 0; s < n_steps; ++s) {
-        CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc, true));
+        CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc));
         if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
     }
     if (loss_sum_out) CF_TRY(read_loss(e, 1, loss_sum_out));
@@ -681,10 +665,9 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
     CF_TRY(ensure_batch(e, B));
     StepArgs a = base_step_args(e, B);
     CF_TRY(sampler_args(e, B, &a));
-    a.grads = 0;
-    a.mark_users = 0;
-    a.mark_items = 0;
-    CF_HIP(launch_step(a, e->stream));
+    a.count_users = 0;
+    a.count_items = 0;
+    CF_HIP(launch_prep(a, e->stream));
     const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
     std::vector<int32_t> hu(nU), hv(nV);
     CF_HIP(hipStreamSynchronize(e->stream));
@@ -754,7 +737,7 @@ int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
     CF_TRY(check_engine(e));
     if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_local needs dense_item_apply=1");
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
-    return run_step(e, B, pairs, negs, groups, e->loss, false);
+    return run_step(e, B, pairs, negs, groups, e->loss);
 }
 
 int cf_step_items(cf_engine* e) {

@@ -10,8 +10,10 @@ namespace cfk {
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kBlock = 256;        // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kPairsPerWave = 16;  // pairs one wave carries through a step
-constexpr int kPairsPerBlock = kPairsPerWave * kWavesPerBlock;
+constexpr int kGL = 16;            // lanes per pair / per row ("group")
+constexpr int kGroupsPerBlock = kBlock / kGL;   // 16
+constexpr int kPairsPerGroup = 2;  // pairs one group carries through the grad kernel
+constexpr int kPairsPerBlock = kGroupsPerBlock * kPairsPerGroup;  // 32
 constexpr int kMaxNeg = 64;
 constexpr int kMaxGroup = 16;
 constexpr int kMaxFactors = 256;
@@ -41,14 +43,14 @@ struct StepArgs {
     int use_rank_weight;
     float n_items_f;
     int64_t n_items;
+    float lr, clip_norm;
+    int clip;            // CML: clip every updated row
     // sampler
     int sample;          // 1: draw batch on device; 0: batch already in occ*
-    int mark_users;      // claim winner rows for the sparse user apply
-    int mark_items;      // claim winner rows for the sparse item apply
-    int grads;           // 0: sample only (cf_sample)
+    int count_users;     // count user-row occurrences (sparse user apply)
+    int count_items;     // count item-row occurrences (sparse item apply)
     uint64_t slot_base;  // position of this batch inside the epoch shuffle
     uint64_t rng_key;    // per-epoch draw key
-    uint32_t stamp;      // step id written into the winner marks
     PermKey perm;
     // graph
     const int2* __restrict__ pairs;         // [nnz] (u,i), CSR order
@@ -56,21 +58,18 @@ struct StepArgs {
     const int32_t* __restrict__ indices;    // [nnz] sorted per user
     const int64_t* __restrict__ indptr_t;   // [n_items+1] (GBPR)
     const int32_t* __restrict__ indices_t;  // [nnz] users of each item
-    // tables
-    const float* __restrict__ U;
-    const float* __restrict__ V;
-    const float* __restrict__ b;
-    float* __restrict__ GU;   // dense user-gradient accumulator
-    float* __restrict__ GV;   // dense item-gradient accumulator
-    float* __restrict__ Gb;   // dense bias-gradient accumulator
-    // batch (occurrence lists) and winner flags
+    // tables (updated in place for rows seen once in the batch)
+    float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
+    float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
+    float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;
+    // batch occurrence lists, per-occurrence rank, per-row counts
     int32_t* __restrict__ occU;   // [B*(1+G)] u | groups
     int32_t* __restrict__ occV;   // [B*(1+W)] i | negatives
-    uint8_t* __restrict__ flagU;  // 1 = first occurrence of its row
-    uint8_t* __restrict__ flagV;
-    uint32_t* __restrict__ markU; // [n_users]
-    uint32_t* __restrict__ markV; // [n_items]
-    double* __restrict__ loss_partial;  // [gridDim.x]
+    int32_t* __restrict__ rankU;  // arrival rank of the occurrence on its row
+    int32_t* __restrict__ rankV;
+    int32_t* __restrict__ cntU;   // [n_users] occurrences in this batch (0 between steps)
+    int32_t* __restrict__ cntV;   // [n_items]
+    double* __restrict__ loss_partial;  // [grad grid]
 };
 
 struct ApplyArgs {
@@ -78,13 +77,14 @@ struct ApplyArgs {
     float lr;
     float clip_norm;
     int clip;            // CML: clip updated rows
-    // sparse apply over occurrence lists
     int nU, nV;          // occurrences of each table
     int blocksU;         // blocks [0, blocksU) serve U, the rest serve V
     const int32_t* __restrict__ occU;
     const int32_t* __restrict__ occV;
-    const uint8_t* __restrict__ flagU;
-    const uint8_t* __restrict__ flagV;
+    const int32_t* __restrict__ rankU;
+    const int32_t* __restrict__ rankV;
+    int32_t* __restrict__ cntU;
+    int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
     float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
     float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;  // nullable
@@ -129,7 +129,9 @@ struct TopkArgs {
 };
 
 // ---- host launchers (cf_kernels.hip / cf_eval.hip) -------------------------
-hipError_t launch_step(const StepArgs& a, hipStream_t s);
+hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + count
+hipError_t launch_grad(const StepArgs& a, hipStream_t s);   // gather, loss, grads, apply
+int grad_blocks(int B);
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);

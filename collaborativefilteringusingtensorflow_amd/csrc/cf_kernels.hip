@@ -1,24 +1,29 @@
 // cf_kernels.hip -- the training hot path for gfx950 (MI355X / CDNA4).
 //
-// One optimizer step of BPRMF / GBPRMF / CML / AMF is two launches:
+// One optimizer step of BPRMF / GBPRMF / CML / AMF is three launches; the
+// unit of parallelism is a 16-lane group per (u,i) pair / per row, four per
+// wave, so a wave keeps four pairs' gathers in flight.
 //
-//  step_kernel   phase A (lane = pair): draw the batch on device -- epoch
-//                bijection over the nnz pairs, W negatives with rejection
-//                against the user's sorted CSR row, G group users from the
-//                item's CSC column -- or read a host-fed batch; claim each
-//                touched row's "winner" occurrence with one atomicExch on a
-//                per-row stamp (the first occurrence of a row in the batch
-//                applies its Adagrad update).
-//                phase B (lane = embedding dimension): gather U[u], V[i],
-//                V[j] (+U[g], b) rows, wave-reduce the dots / distances,
-//                evaluate the loss and dL/dx, and scatter-add every
-//                per-occurrence gradient row into dense fp32 accumulators
-//                (one 256-B float-atomic wave instruction per d=64 row).
-//                Duplicate rows therefore SUM before the update -- the TF1
-//                _deduplicate_indexed_slices semantics.
-//  apply_kernel  one wave per winner row: acc += g^2; w -= lr*g/sqrt(acc)
-//                (SparseApplyAdagrad), zero the accumulator row, and for
-//                CML clip the updated row to clip_norm (cml.py:119-129).
+//  prep_kernel   draw the batch on device -- epoch bijection over the nnz
+//                pairs, W negatives whose membership in Pos(u) the 16 lanes
+//                test cooperatively against the user's sorted CSR row
+//                (one coalesced pass, group-OR of hit masks, redraw only the
+//                rejected ones), G group users from the item's CSC column --
+//                or take a host-fed batch; then count every touched row's
+//                occurrences in the batch (one returning atomicAdd per
+//                occurrence: the value is its arrival rank).
+//  grad_kernel   gather U[u], V[i], V[j] (+U[g], b) rows, group-reduce the
+//                dots / distances, evaluate the loss and dL/dx, form every
+//                per-occurrence gradient row.  A row that occurs ONCE in the
+//                batch is updated right here with SparseApplyAdagrad
+//                (acc += g^2; w -= lr*g/sqrt(acc); CML: clip) -- its
+//                pre-update value is already in registers.  A row that
+//                occurs several times scatter-adds into a dense fp32
+//                accumulator (float atomics, 64-B segments), so duplicates
+//                SUM before the update: TF1's _deduplicate_indexed_slices
+//                (SURVEY 0.4).
+//  apply_kernel  the rank-0 occurrence of every duplicated row applies the
+//                summed gradient, zeroes the accumulator and the count.
 //
 // Reference semantics: src/models/pl/models/bprmf.py:52-88,
 // gbprmf.py:58-106, cml.py:55-129, src/models/others/models/amf.py:66-162;
@@ -28,34 +33,115 @@
 
 namespace cfk {
 
+// ---------------------------------------------------------------------------
+// 16-lane group helpers: element e of a row lives in lane (e % 16), slot
+// e / 16, so one load instruction reads 64 contiguous bytes of four rows.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float gsum(float v) {
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 1, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint32_t gor(uint32_t v) {
+    v |= (uint32_t)__shfl_xor((int)v, 8, 64);
+    v |= (uint32_t)__shfl_xor((int)v, 4, 64);
+    v |= (uint32_t)__shfl_xor((int)v, 2, 64);
+    v |= (uint32_t)__shfl_xor((int)v, 1, 64);
+    return v;
+}
+
 template <int EPL>
-__device__ __forceinline__ void load_row(const float* __restrict__ X, int64_t r, int d, int lane,
-                                         float (&x)[EPL]) {
+__device__ __forceinline__ void gload(const float* __restrict__ X, int64_t r, int d, int gl,
+                                      float (&x)[EPL]) {
     const float* row = X + r * (int64_t)d;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
-        const int e = s * kWave + lane;
+        const int e = s * kGL + gl;
         x[s] = (e < d) ? row[e] : 0.f;
     }
 }
 
 template <int EPL>
-__device__ __forceinline__ void atomic_row(float* __restrict__ G, int64_t r, int d, int lane,
-                                           const float (&g)[EPL]) {
+__device__ __forceinline__ void gatomic(float* __restrict__ G, int64_t r, int d, int gl,
+                                        const float (&g)[EPL]) {
     float* row = G + r * (int64_t)d;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
-        const int e = s * kWave + lane;
+        const int e = s * kGL + gl;
         if (e < d) unsafeAtomicAdd(row + e, g[s]);
     }
 }
 
 template <int EPL>
-__device__ __forceinline__ float dot_part(const float (&x)[EPL], const float (&y)[EPL]) {
+__device__ __forceinline__ float gdot(const float (&x)[EPL], const float (&y)[EPL]) {
     float t = 0.f;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) t = fmaf(x[s], y[s], t);
-    return t;
+    return gsum(t);
+}
+
+// SparseApplyAdagrad on one row whose pre-update value x0 is in registers
+// (+ tf.clip_by_norm for CML): acc += g^2; x = x0 - lr*g/sqrt(acc)
+template <int EPL>
+__device__ __forceinline__ void gapply(float* __restrict__ X, float* __restrict__ A, int64_t r,
+                                       int d, int gl, const float (&x0)[EPL],
+                                       const float (&g)[EPL], float lr, bool clip, float c) {
+    float* xr = X + r * (int64_t)d;
+    float* ar = A + r * (int64_t)d;
+    float acc[EPL], x[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = s * kGL + gl;
+        acc[s] = (e < d) ? ar[e] : 1.f;
+    }
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        acc[s] = fmaf(g[s], g[s], acc[s]);
+        x[s] = x0[s] - (lr * g[s]) / sqrtf(acc[s]);
+    }
+    if (clip) {
+        const float n = sqrtf(gdot<EPL>(x, x));
+        const float den = fmaxf(n, c);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
+    }
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = s * kGL + gl;
+        if (e < d) {
+            xr[e] = x[s];
+            ar[e] = acc[s];
+        }
+    }
+}
+
+// row r of X: singleton -> apply now; duplicated -> accumulate
+template <int EPL>
+__device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict__ A,
+                                        float* __restrict__ G, int32_t* __restrict__ cnt,
+                                        int64_t r, int count, int d, int gl,
+                                        const float (&x0)[EPL], const float (&g)[EPL],
+                                        const StepArgs& a) {
+    if (count == 1) {
+        gapply<EPL>(X, A, r, d, gl, x0, g, a.lr, a.clip != 0, a.clip_norm);
+        if (gl == 0) cnt[r] = 0;
+    } else {
+        gatomic<EPL>(G, r, d, gl, g);
+    }
+}
+
+__device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g) {
+    // GBPR item bias: one scalar row
+    if (count == 1) {
+        const float acc = fmaf(g, g, a.Ab[r]);
+        a.Ab[r] = acc;
+        a.b[r] -= (a.lr * g) / sqrtf(acc);
+    } else {
+        unsafeAtomicAdd(a.Gb + r, g);
+    }
 }
 
 __device__ __forceinline__ float neg_log_sigmoid(float x) {
@@ -68,126 +154,143 @@ __device__ __forceinline__ float softplus(float x) {
     return x > 0.f ? x + log1pf(expf(-x)) : log1pf(expf(x));
 }
 
-__device__ __forceinline__ int rfl(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t n_items) {
+    return (int32_t)uniform_below(mix64(key + ctr), (uint64_t)n_items);
+}
 
 // ---------------------------------------------------------------------------
-// fused step
+// prep: sample (or load) the batch and count row occurrences
 // ---------------------------------------------------------------------------
-template <int MODEL, int EPL>
-__global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    __shared__ double s_loss[kWavesPerBlock];
-
-    const int lane = lane_id();
-    const int wv = threadIdx.x >> 6;
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int p = blockIdx.x * kGroupsPerBlock + (threadIdx.x >> 4);
+    if (p >= a.B) return;  // whole group leaves; no block barrier below
     const int W = a.W;
     const int G = (MODEL == GBPR) ? a.G : 0;
-    const int stride = 2 + W + G;  // ints per pair record in LDS
-    int* sw = smem + wv * kPairsPerWave * stride;
-    const int p0 = (blockIdx.x * kWavesPerBlock + wv) * kPairsPerWave;
-
-    // ---- phase A: lane = pair ------------------------------------------------
-    if (lane < kPairsPerWave) {
-        const int p = p0 + lane;
-        int* rec = sw + lane * stride;
-        if (p < a.B) {
-            int u, i;
-            if (a.sample) {
-                const uint64_t slot = a.slot_base + (uint64_t)p;
-                const uint64_t idx = permute(slot, a.perm);
-                const int2 pr = a.pairs[idx];
-                u = pr.x;
-                i = pr.y;
-                const uint64_t key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
-                const int64_t rb = a.indptr[u], re = a.indptr[u + 1];
-                for (int w = 0; w < W; ++w) {
-                    // negItems = randint(0, n_items), redrawn while j in Pos(u)
-                    // (sampler_ranking.py:30-36)
-                    uint64_t ctr = (uint64_t)w << 32;
-                    int32_t j;
-                    do {
-                        j = (int32_t)uniform_below(mix64(key + ctr), (uint64_t)a.n_items);
-                        ++ctr;
-                    } while (sorted_contains(a.indices, rb, re, j));
-                    rec[2 + w] = j;
-                    a.occV[a.B + p * W + w] = j;
-                }
-                if (MODEL == GBPR) {
-                    // group = np.random.choice(item_posUserList[i], gsize)
-                    // -- uniform, with replacement, may contain u (sampler_gbpr.py:41)
-                    const int64_t cb = a.indptr_t[i], ce = a.indptr_t[i + 1];
-                    for (int k = 0; k < G; ++k) {
-                        const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + k) << 32));
-                        const int32_t g =
-                            a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
-                        rec[2 + W + k] = g;
-                        a.occU[a.B + p * G + k] = g;
+    const int B = a.B;
+    int u, i;
+    uint64_t key = 0;
+    int64_t rb = 0, re = 0;
+    if (a.sample) {
+        const uint64_t slot = a.slot_base + (uint64_t)p;
+        const uint64_t idx = permute(slot, a.perm);   // shuffled pair order (sampler_ranking.py:24)
+        const int2 pr = a.pairs[idx];
+        u = pr.x;
+        i = pr.y;
+        key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
+        rb = a.indptr[u];
+        re = a.indptr[u + 1];
+    } else {
+        u = a.occU[p];
+        i = a.occV[p];
+    }
+    const int nchunk = (int)((re - rb + kGL - 1) / kGL);
+    for (int w0 = 0; w0 < W; w0 += kGL) {
+        const int nw = (W - w0 < kGL) ? (W - w0) : kGL;
+        const int w = w0 + gl;
+        int32_t j = -1;
+        if (a.sample) {
+            // negItems = randint(0, n_items), redrawn while j in Pos(u)
+            // (sampler_ranking.py:30-36); lane w owns candidate w
+            uint64_t ctr = (uint64_t)w << 32;
+            if (gl < nw) j = draw_item(key, ctr++, a.n_items);
+            uint32_t pending = (nw >= 32) ? 0xFFFFFFFFu : ((1u << nw) - 1u);
+            for (;;) {
+                uint32_t hit = 0;
+                for (int c = 0; c < nchunk; ++c) {
+                    const int64_t t = rb + (int64_t)c * kGL + gl;
+                    const int32_t el = (t < re) ? a.indices[t] : -1;
+                    for (int k = 0; k < nw; ++k) {
+                        const int32_t cand = __shfl(j, k, kGL);
+                        hit |= (el == cand) ? (1u << k) : 0u;
                     }
                 }
-                a.occU[p] = u;
-                a.occV[p] = i;
-            } else {
-                u = a.occU[p];
-                i = a.occV[p];
-                for (int w = 0; w < W; ++w) rec[2 + w] = a.occV[a.B + p * W + w];
-                for (int k = 0; k < G; ++k) rec[2 + W + k] = a.occU[a.B + p * G + k];
+                hit = gor(hit) & pending;
+                if (hit == 0u) break;  // group-uniform
+                if ((hit >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
+                pending = hit;
             }
-            rec[0] = u;
-            rec[1] = i;
-            if (a.mark_users) {
-                a.flagU[p] = atomicExch(&a.markU[u], a.stamp) != a.stamp;
-                for (int k = 0; k < G; ++k)
-                    a.flagU[a.B + p * G + k] =
-                        atomicExch(&a.markU[rec[2 + W + k]], a.stamp) != a.stamp;
-            }
-            if (a.mark_items) {
-                a.flagV[p] = atomicExch(&a.markV[i], a.stamp) != a.stamp;
-                for (int w = 0; w < W; ++w)
-                    a.flagV[a.B + p * W + w] = atomicExch(&a.markV[rec[2 + w]], a.stamp) != a.stamp;
-            }
+            if (gl < nw) a.occV[B + p * W + w] = j;
+        } else if (gl < nw) {
+            j = a.occV[B + p * W + w];
         }
+        if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
     }
-    __syncthreads();
-    if (!a.grads) return;
+    if (MODEL == GBPR && gl < G) {
+        int32_t g;
+        if (a.sample) {
+            // group = np.random.choice(item_posUserList[i], gsize): uniform,
+            // with replacement, may contain u (sampler_gbpr.py:41)
+            const int64_t cb = a.indptr_t[i], ce = a.indptr_t[i + 1];
+            const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + gl) << 32));
+            g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
+            a.occU[B + p * G + gl] = g;
+        } else {
+            g = a.occU[B + p * G + gl];
+        }
+        if (a.count_users) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
+    }
+    if (gl == 0) {
+        if (a.sample) {
+            a.occU[p] = u;
+            a.occV[p] = i;
+        }
+        if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
+        if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
+    }
+}
 
-    // ---- phase B: lane = embedding dimension ------------------------------------
+// ---------------------------------------------------------------------------
+// grad: gather, loss, gradient rows, singleton apply / duplicate scatter
+// ---------------------------------------------------------------------------
+template <int MODEL, int EPL>
+__global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
+    __shared__ double s_loss[kGroupsPerBlock];
+    const int gl = threadIdx.x & (kGL - 1);
+    const int grp = threadIdx.x >> 4;
     const int d = a.d;
-    float loss_w = 0.f;   // wave-uniform: embedding loss (+ GBPR bias L2)
-    float sq = 0.f;       // lane-partial sum of squares for the L2 term
-    for (int pp = 0; pp < kPairsPerWave; ++pp) {
-        const int p = p0 + pp;
-        if (p >= a.B) break;
-        const int* rec = sw + pp * stride;
-        const int u = rfl(rec[0]);
-        const int i = rfl(rec[1]);
+    const int W = a.W;
+    const int G = (MODEL == GBPR) ? a.G : 0;
+    const int B = a.B;
+    float loss_g = 0.f;  // group-uniform: embedding loss (+ GBPR bias L2)
+    float sq = 0.f;      // lane-partial sum of squares for the L2 term
+
+    for (int k = 0; k < kPairsPerGroup; ++k) {
+        const int p = (blockIdx.x * kPairsPerGroup + k) * kGroupsPerBlock + grp;
+        if (p >= B) break;  // group-uniform
+        const int u = a.occU[p];
+        const int i = a.occV[p];
+        const int cu = a.count_users ? a.cntU[u] : 0;
+        const int ci = a.count_items ? a.cntV[i] : 0;
         float uu[EPL], vi[EPL];
-        load_row<EPL>(a.U, u, d, lane, uu);
-        load_row<EPL>(a.V, i, d, lane, vi);
+        gload<EPL>(a.U, u, d, gl, uu);
+        gload<EPL>(a.V, i, d, gl, vi);
 
         if (MODEL == BPR || MODEL == AMF) {
             // x = <u,i> - <u,j>;  c = dL/dx = sigmoid(x) - 1   (A.1, A.4)
-            const float ui = wave_sum(dot_part<EPL>(uu, vi));
+            const float ui = gdot<EPL>(uu, vi);
             float gu[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
             float sc = 0.f;
             for (int w = 0; w < W; ++w) {
-                const int j = rfl(rec[2 + w]);
+                const int j = a.occV[B + p * W + w];
+                const int cj = a.count_items ? a.cntV[j] : 0;
                 float vj[EPL];
-                load_row<EPL>(a.V, j, d, lane, vj);
-                const float uj = wave_sum(dot_part<EPL>(uu, vj));
-                const float x = ui - uj;
+                gload<EPL>(a.V, j, d, gl, vj);
+                const float x = ui - gdot<EPL>(uu, vj);
                 float c = -1.f / (1.f + expf(x));
                 if (MODEL == AMF) {
-                    loss_w += softplus(-x);
+                    loss_g += softplus(-x);
                     if (a.adversarial) {
                         // + reg_adv * softplus(-clip_by_value(x, -80, 1e8)), Δ == 0
                         const float xc = fmaxf(fminf(x, 1e8f), -80.f);
-                        loss_w += a.reg_adv * softplus(-xc);
+                        loss_g += a.reg_adv * softplus(-xc);
                         if (x >= -80.f && x <= 1e8f) c *= (1.f + a.reg_adv);
                     }
                 } else {
-                    loss_w += neg_log_sigmoid(x);
+                    loss_g += neg_log_sigmoid(x);
                 }
                 sc += c;
                 float gj[EPL];
@@ -197,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                     gj[s] = -c * uu[s] + a.reg * vj[s];
                     sq = fmaf(vj[s], vj[s], sq);
                 }
-                atomic_row<EPL>(a.GV, j, d, lane, gj);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -207,18 +310,18 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            atomic_row<EPL>(a.GU, u, d, lane, gu);
-            atomic_row<EPL>(a.GV, i, d, lane, gi);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
         } else if (MODEL == GBPR) {
             // ui = rho*mean_k<g_k,i> + (1-rho)<u,i> + b_i ; uj = <u,j> + b_j   (A.2)
             const float bi = a.b[i];
-            const float ui_u = wave_sum(dot_part<EPL>(uu, vi));
+            const float ui_u = gdot<EPL>(uu, vi);
             float sg[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) sg[s] = 0.f;
-            for (int k = 0; k < G; ++k) {
+            for (int k2 = 0; k2 < G; ++k2) {
                 float gk[EPL];
-                load_row<EPL>(a.U, rfl(rec[2 + W + k]), d, lane, gk);
+                gload<EPL>(a.U, a.occU[B + p * G + k2], d, gl, gk);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
                     sg[s] += gk[s];
@@ -226,21 +329,20 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                 }
             }
             const float Gf = (float)G;
-            const float ui_g = wave_sum(dot_part<EPL>(sg, vi)) / Gf;
-            const float ui = a.rho * ui_g + (1.f - a.rho) * ui_u + bi;
+            const float ui = a.rho * (gdot<EPL>(sg, vi) / Gf) + (1.f - a.rho) * ui_u + bi;
             float gu[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
             float sc = 0.f;
             for (int w = 0; w < W; ++w) {
-                const int j = rfl(rec[2 + w]);
+                const int j = a.occV[B + p * W + w];
+                const int cj = a.count_items ? a.cntV[j] : 0;
                 const float bj = a.b[j];
                 float vj[EPL];
-                load_row<EPL>(a.V, j, d, lane, vj);
-                const float uj = wave_sum(dot_part<EPL>(uu, vj)) + bj;
-                const float x = ui - uj;
+                gload<EPL>(a.V, j, d, gl, vj);
+                const float x = ui - (gdot<EPL>(uu, vj) + bj);
                 const float c = -1.f / (1.f + expf(x));
-                loss_w += neg_log_sigmoid(x) + 0.5f * a.reg * bj * bj;
+                loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj * bj;
                 sc += c;
                 float gj[EPL];
 #pragma unroll
@@ -248,8 +350,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                     gu[s] = fmaf(-c, vj[s], gu[s]);
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
-                atomic_row<EPL>(a.GV, j, d, lane, gj);
-                if (lane == 0) unsafeAtomicAdd(a.Gb + j, -c + a.reg * bj);
+                if (gl == 0) bias_finish(a, j, cj, -c + a.reg * bj);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
             }
             const float rg = a.rho / Gf;
             float gi[EPL];
@@ -260,42 +362,42 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            atomic_row<EPL>(a.GU, u, d, lane, gu);
-            for (int k = 0; k < G; ++k) {
-                const int g = rfl(rec[2 + W + k]);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
+            for (int k2 = 0; k2 < G; ++k2) {
+                const int g = a.occU[B + p * G + k2];
+                const int cg = a.cntU[g];
                 float gk[EPL], gg[EPL];
-                load_row<EPL>(a.U, g, d, lane, gk);
+                gload<EPL>(a.U, g, d, gl, gk);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) gg[s] = rg * sc * vi[s] + a.reg * gk[s];
-                atomic_row<EPL>(a.GU, g, d, lane, gg);
+                gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, g, cg, d, gl, gk, gg, a);
             }
-            atomic_row<EPL>(a.GV, i, d, lane, gi);
-            if (lane == 0) unsafeAtomicAdd(a.Gb + i, sc);
-        } else {  // CML (A.3)
+            if (gl == 0) bias_finish(a, i, ci, sc);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
+        } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) du[s] = uu[s] - vi[s];
-            const float dp = wave_sum(dot_part<EPL>(du, du));
-            float dn_lane = 0.f;  // lane w keeps dn_w
+            const float dp = gdot<EPL>(du, du);
+            float dn_lane = 0.f;
             float m = INFINITY;
             int imp = 0;
             for (int w = 0; w < W; ++w) {
-                float vj[EPL];
-                load_row<EPL>(a.V, rfl(rec[2 + w]), d, lane, vj);
-                float t[EPL];
+                float vj[EPL], t[EPL];
+                gload<EPL>(a.V, a.occV[B + p * W + w], d, gl, vj);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) t[s] = uu[s] - vj[s];
-                const float dn = wave_sum(dot_part<EPL>(t, t));
-                if (lane == w) dn_lane = dn;
+                const float dn = gdot<EPL>(t, t);
+                if (gl == w) dn_lane = dn;
                 m = fminf(m, dn);
                 imp += (dp - dn + a.margin > 0.f) ? 1 : 0;
             }
-            const unsigned long long tie = __ballot(lane < W && dn_lane == m);
-            const float cnt = (float)__popcll(tie);
+            const unsigned long long tie = __ballot(gl < W && dn_lane == m);
+            const float cnt = (float)__popcll((tie >> (threadIdx.x & 48)) & 0xFFFFull);
             const float z = dp - m + a.margin;
             const float lw =
                 a.use_rank_weight ? logf((float)imp / (float)W * a.n_items_f + 1.f) : 1.f;
-            loss_w += fmaxf(z, 0.f) * lw;
+            loss_g += fmaxf(z, 0.f) * lw;
             const float aa = (z > 0.f) ? lw : 0.f;
             const bool l2 = a.reg_cov > 0.f;
             float gu[EPL], gi[EPL];
@@ -305,12 +407,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                 gi[s] = -2.f * aa * du[s];
             }
             for (int w = 0; w < W; ++w) {
-                const float dnw = __shfl(dn_lane, w, 64);
+                const float dnw = __shfl(dn_lane, w, kGL);
                 const float share = (dnw == m) ? 1.f / cnt : 0.f;
-                if (share == 0.f && !l2) continue;  // wave-uniform
-                const int j = rfl(rec[2 + w]);
+                const int j = a.occV[B + p * W + w];
+                const int cj = a.count_items ? a.cntV[j] : 0;
                 float vj[EPL], gj[EPL];
-                load_row<EPL>(a.V, j, d, lane, vj);
+                gload<EPL>(a.V, j, d, gl, vj);
                 const float coef = 2.f * aa * share;
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
@@ -322,7 +424,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                         sq = fmaf(vj[s], vj[s], sq);
                     }
                 }
-                atomic_row<EPL>(a.GV, j, d, lane, gj);
+                // a touched row with a zero gradient is still clipped (cml.py:128-129)
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -333,71 +436,34 @@ __global__ __launch_bounds__(kBlock) void step_kernel(StepArgs a) {
                     sq = fmaf(vi[s], vi[s], sq);
                 }
             }
-            atomic_row<EPL>(a.GU, u, d, lane, gu);
-            atomic_row<EPL>(a.GV, i, d, lane, gi);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
         }
     }
 
-    // ---- per-block pre-update loss partial (deterministic order) -----------------
-    float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
-    const float sq_w = wave_sum(sq);
-    if (lane == 0) s_loss[wv] = (double)loss_w + 0.5 * (double)coef * (double)sq_w;
+    // ---- per-block pre-update loss partial (fixed summation order) --------------
+    const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
+    const float sq_g = gsum(sq);
+    if (gl == 0) s_loss[grp] = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < kWavesPerBlock; ++k) t += s_loss[k];
+        for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[k];
         a.loss_partial[blockIdx.x] = t;
     }
 }
 
 // ---------------------------------------------------------------------------
-// Adagrad apply over the winner rows of the batch
+// apply the summed gradient of every duplicated row (rank-0 occurrence)
 // ---------------------------------------------------------------------------
-template <int EPL, bool CLIP>
-__device__ __forceinline__ void apply_row(float* __restrict__ X, float* __restrict__ A,
-                                          float* __restrict__ G, int64_t r, int d, int lane,
-                                          float lr, float clip_norm) {
-    float* xr = X + r * (int64_t)d;
-    float* ar = A + r * (int64_t)d;
-    float* gr = G + r * (int64_t)d;
-    float x[EPL], acc[EPL], g[EPL];
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kWave + lane;
-        const bool ok = e < d;
-        g[s] = ok ? gr[e] : 0.f;
-        acc[s] = ok ? ar[e] : 1.f;
-        x[s] = ok ? xr[e] : 0.f;
-    }
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        acc[s] = fmaf(g[s], g[s], acc[s]);     // accum += grad^2
-        x[s] -= (lr * g[s]) / sqrtf(acc[s]);   // var -= lr*grad*rsqrt(accum)
-    }
-    if (CLIP) {
-        // tf.clip_by_norm(t, c, axes=[1]) = t*c / max(|t|, c)
-        const float n = sqrtf(wave_sum(dot_part<EPL>(x, x)));
-        const float den = fmaxf(n, clip_norm);
-#pragma unroll
-        for (int s = 0; s < EPL; ++s) x[s] = (x[s] * clip_norm) / den;
-    }
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kWave + lane;
-        if (e < d) {
-            xr[e] = x[s];
-            ar[e] = acc[s];
-            gr[e] = 0.f;
-        }
-    }
-}
-
-template <int EPL, bool CLIP>
+template <int EPL>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
     __shared__ double s_red[kWavesPerBlock];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
+    const int gw = lane >> 4;       // group inside the wave
+    const int gl = lane & (kGL - 1);
     if (blockIdx.x == 0 && a.loss_acc != nullptr) {
         double t = 0.0;
         for (int k = threadIdx.x; k < a.n_partial; k += kBlock) t += a.loss_partial[k];
@@ -410,14 +476,19 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
     const int blk = isU ? (int)blockIdx.x : (int)blockIdx.x - a.blocksU;
     const int n = isU ? a.nU : a.nV;
     const int32_t* occ = isU ? a.occU : a.occV;
-    const uint8_t* flag = isU ? a.flagU : a.flagV;
+    const int32_t* rank = isU ? a.rankU : a.rankV;
+    int32_t* cnt = isU ? a.cntU : a.cntV;
     float* X = isU ? a.U : a.V;
     float* A = isU ? a.AU : a.AV;
     float* G = isU ? a.GU : a.GV;
 
     const int o = (blk * kWavesPerBlock + wv) * kWave + lane;
-    const bool win = o < n && flag[o] != 0;
-    const int r_l = win ? occ[o] : 0;
+    int r_l = 0;
+    bool win = false;
+    if (o < n && rank[o] == 0) {
+        r_l = occ[o];
+        win = cnt[r_l] > 1;
+    }
     if (!isU && a.b != nullptr && win) {
         const float g = a.Gb[r_l];
         const float acc = fmaf(g, g, a.Ab[r_l]);
@@ -425,30 +496,56 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
         a.b[r_l] -= (a.lr * g) / sqrtf(acc);
         a.Gb[r_l] = 0.f;
     }
-    unsigned long long mask = __ballot(win);
-    while (mask) {
-        const int l = __ffsll((long long)mask) - 1;
-        mask &= mask - 1ull;
-        const int r = rfl(__shfl(r_l, l, 64));
-        apply_row<EPL, CLIP>(X, A, G, r, a.d, lane, a.lr, a.clip_norm);
+    const unsigned long long m = __ballot(win);
+    const int nwin = __popcll(m);
+    for (int base = 0; base < nwin; base += 4) {
+        const int my = base + gw;
+        unsigned long long mm = m;
+        for (int t = 0; t < my && mm; ++t) mm &= mm - 1ull;
+        const int pos = (my < nwin) ? __ffsll((long long)mm) - 1 : 0;
+        const int r = __shfl(r_l, pos, 64);
+        if (my < nwin) {  // group-uniform
+            float g[EPL], x[EPL];
+            gload<EPL>(G, r, a.d, gl, g);
+            gload<EPL>(X, r, a.d, gl, x);
+            float* gr = G + (int64_t)r * a.d;
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                const int e = s * kGL + gl;
+                if (e < a.d) gr[e] = 0.f;
+            }
+            gapply<EPL>(X, A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
+            if (gl == 0) cnt[r] = 0;
+        }
     }
 }
 
+// ---------------------------------------------------------------------------
 // dense item apply (multi-rank: after the all-reduce every replica applies the
-// identical update; rows with an all-zero gradient are exact no-ops in TF too)
-template <int EPL, bool CLIP>
+// identical update; a row whose summed gradient is all-zero is an exact no-op
+// of SparseApplyAdagrad, so it is skipped)
+// ---------------------------------------------------------------------------
+template <int EPL>
 __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
-    const int lane = lane_id();
-    const int64_t wave0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-    for (int64_t r = wave0; r < a.n_rows; r += nwaves) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int64_t g0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
+    const int64_t ng = ((int64_t)gridDim.x * kBlock) >> 4;
+    for (int64_t r = g0; r < a.n_rows; r += ng) {
         float g[EPL];
-        load_row<EPL>(a.G, r, a.d, lane, g);
-        bool nz = false;
+        gload<EPL>(a.G, r, a.d, gl, g);
+        uint32_t nz = 0;
 #pragma unroll
-        for (int s = 0; s < EPL; ++s) nz |= (g[s] != 0.f);
-        if (__ballot(nz) == 0ull) continue;
-        apply_row<EPL, CLIP>(a.X, a.A, a.G, r, a.d, lane, a.lr, a.clip_norm);
+        for (int s = 0; s < EPL; ++s) nz |= (g[s] != 0.f) ? 1u : 0u;
+        if (gor(nz) == 0u) continue;  // group-uniform
+        float x[EPL];
+        gload<EPL>(a.X, r, a.d, gl, x);
+        float* gr = a.G + r * (int64_t)a.d;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            const int e = s * kGL + gl;
+            if (e < a.d) gr[e] = 0.f;
+        }
+        gapply<EPL>(a.X, a.A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
     }
     if (a.b != nullptr) {
         const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -468,18 +565,18 @@ __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
 template <int EPL>
 __global__ __launch_bounds__(kBlock) void clip_full_kernel(float* __restrict__ X, int64_t n_rows,
                                                            int d, float c) {
-    const int lane = lane_id();
-    const int64_t wave0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-    for (int64_t r = wave0; r < n_rows; r += nwaves) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int64_t g0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
+    const int64_t ng = ((int64_t)gridDim.x * kBlock) >> 4;
+    for (int64_t r = g0; r < n_rows; r += ng) {
         float x[EPL];
-        load_row<EPL>(X, r, d, lane, x);
-        const float n = sqrtf(wave_sum(dot_part<EPL>(x, x)));
+        gload<EPL>(X, r, d, gl, x);
+        const float n = sqrtf(gdot<EPL>(x, x));
         const float den = fmaxf(n, c);
         float* xr = X + r * (int64_t)d;
 #pragma unroll
         for (int s = 0; s < EPL; ++s) {
-            const int e = s * kWave + lane;
+            const int e = s * kGL + gl;
             if (e < d) xr[e] = (x[s] * c) / den;
         }
     }
@@ -521,73 +618,90 @@ __global__ void build_pairs_kernel(const int64_t* __restrict__ indptr,
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-static int epl_for(int d) { return d <= 64 ? 1 : (d <= 128 ? 2 : 4); }
+static int epl_for(int d) {
+    const int e = (d + kGL - 1) / kGL;
+    return e <= 1 ? 1 : e <= 2 ? 2 : e <= 4 ? 4 : e <= 8 ? 8 : 16;
+}
 
-template <int MODEL>
-static hipError_t launch_step_m(const StepArgs& a, hipStream_t s) {
-    const int blocks = (a.B + kPairsPerBlock - 1) / kPairsPerBlock;
-    const int G = (MODEL == GBPR) ? a.G : 0;
-    const size_t lds = (size_t)kPairsPerBlock * (2 + a.W + G) * sizeof(int);
-    switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((step_kernel<MODEL, 1>), dim3(blocks), dim3(kBlock), lds, s, a); break;
-        case 2: hipLaunchKernelGGL((step_kernel<MODEL, 2>), dim3(blocks), dim3(kBlock), lds, s, a); break;
-        default: hipLaunchKernelGGL((step_kernel<MODEL, 4>), dim3(blocks), dim3(kBlock), lds, s, a); break;
+int grad_blocks(int B) { return (B + kPairsPerBlock - 1) / kPairsPerBlock; }
+
+hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    const int blocks = (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    switch (a.model) {
+        case GBPR: hipLaunchKernelGGL(prep_kernel<GBPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
+        default: hipLaunchKernelGGL(prep_kernel<BPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_step(const StepArgs& a, hipStream_t s) {
+template <int MODEL>
+static hipError_t launch_grad_m(const StepArgs& a, hipStream_t s) {
+    const dim3 grid(grad_blocks(a.B)), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16>), grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     switch (a.model) {
-        case BPR: return launch_step_m<BPR>(a, s);
-        case GBPR: return launch_step_m<GBPR>(a, s);
-        case CML: return launch_step_m<CML>(a, s);
-        default: return launch_step_m<AMF>(a, s);
+        case BPR: return launch_grad_m<BPR>(a, s);
+        case GBPR: return launch_grad_m<GBPR>(a, s);
+        case CML: return launch_grad_m<CML>(a, s);
+        default: return launch_grad_m<AMF>(a, s);
     }
 }
 
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
     const int per_block = kWavesPerBlock * kWave;
     const int bV = a.apply_items ? (a.nV + per_block - 1) / per_block : 0;
-    const int blocks = a.blocksU + bV;
-    if (blocks == 0) return hipSuccess;
-    const int e = epl_for(a.d);
-#define CF_APPLY(EPL, CL) \
-    hipLaunchKernelGGL((apply_kernel<EPL, CL>), dim3(blocks), dim3(kBlock), 0, s, a)
-    if (a.clip) {
-        if (e == 1) CF_APPLY(1, true); else if (e == 2) CF_APPLY(2, true); else CF_APPLY(4, true);
-    } else {
-        if (e == 1) CF_APPLY(1, false); else if (e == 2) CF_APPLY(2, false); else CF_APPLY(4, false);
+    int blocks = a.blocksU + bV;
+    if (blocks == 0) blocks = 1;  // block 0 still reduces the loss
+    const dim3 grid(blocks), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL(apply_kernel<1>, grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(apply_kernel<2>, grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL(apply_kernel<4>, grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL(apply_kernel<8>, grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL(apply_kernel<16>, grid, block, 0, s, a); break;
     }
-#undef CF_APPLY
     return hipGetLastError();
 }
 
+static int row_grid(int64_t n_rows) {
+    int64_t b = (n_rows + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    if (b > 8192) b = 8192;
+    if (b < 1) b = 1;
+    return (int)b;
+}
+
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s) {
-    const int64_t waves = a.n_rows;
-    int blocks = (int)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
-    if (blocks > 4096) blocks = 4096;
-    if (blocks < 1) blocks = 1;
-    const int e = epl_for(a.d);
-#define CF_DENSE(EPL, CL) \
-    hipLaunchKernelGGL((apply_dense_kernel<EPL, CL>), dim3(blocks), dim3(kBlock), 0, s, a)
-    if (a.clip) {
-        if (e == 1) CF_DENSE(1, true); else if (e == 2) CF_DENSE(2, true); else CF_DENSE(4, true);
-    } else {
-        if (e == 1) CF_DENSE(1, false); else if (e == 2) CF_DENSE(2, false); else CF_DENSE(4, false);
+    const dim3 grid(row_grid(a.n_rows)), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL(apply_dense_kernel<1>, grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(apply_dense_kernel<2>, grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL(apply_dense_kernel<4>, grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL(apply_dense_kernel<8>, grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL(apply_dense_kernel<16>, grid, block, 0, s, a); break;
     }
-#undef CF_DENSE
     return hipGetLastError();
 }
 
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float c, hipStream_t s) {
-    int blocks = (int)((n_rows + kWavesPerBlock - 1) / kWavesPerBlock);
-    if (blocks > 4096) blocks = 4096;
-    if (blocks < 1) blocks = 1;
-    const int e = epl_for(d);
-    if (e == 1) hipLaunchKernelGGL((clip_full_kernel<1>), dim3(blocks), dim3(kBlock), 0, s, X, n_rows, d, c);
-    else if (e == 2) hipLaunchKernelGGL((clip_full_kernel<2>), dim3(blocks), dim3(kBlock), 0, s, X, n_rows, d, c);
-    else hipLaunchKernelGGL((clip_full_kernel<4>), dim3(blocks), dim3(kBlock), 0, s, X, n_rows, d, c);
+    const dim3 grid(row_grid(n_rows)), block(kBlock);
+    switch (epl_for(d)) {
+        case 1: hipLaunchKernelGGL(clip_full_kernel<1>, grid, block, 0, s, X, n_rows, d, c); break;
+        case 2: hipLaunchKernelGGL(clip_full_kernel<2>, grid, block, 0, s, X, n_rows, d, c); break;
+        case 4: hipLaunchKernelGGL(clip_full_kernel<4>, grid, block, 0, s, X, n_rows, d, c); break;
+        case 8: hipLaunchKernelGGL(clip_full_kernel<8>, grid, block, 0, s, X, n_rows, d, c); break;
+        default: hipLaunchKernelGGL(clip_full_kernel<16>, grid, block, 0, s, X, n_rows, d, c); break;
+    }
     return hipGetLastError();
 }
 
@@ -627,7 +741,7 @@ PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch) {
     p.n = n;
     uint32_t bits = 1;
     while (bits < 63 && (1ull << bits) < n) ++bits;
-    p.mask = (bits >= 64) ? ~0ull : ((1ull << bits) - 1ull);
+    p.mask = (1ull << bits) - 1ull;
     p.shift = bits / 2 > 0 ? bits / 2 : 1;
     uint64_t h = mix64(seed ^ mix64(epoch + 0x5851F42D4C957F2Dull));
     for (int r = 0; r < 3; ++r) {

@@ -62,13 +62,14 @@ enum cf_table {
 
 /* kernels timed by the built-in HIP-event profiler */
 enum cf_kernel_id {
-    CF_K_STEP = 0,       /* fused sample + gather + loss + gradient scatter */
-    CF_K_APPLY = 1,      /* dedup'd Adagrad apply over touched rows         */
-    CF_K_APPLY_DENSE = 2,/* dense item Adagrad (after cross-rank all-reduce) */
-    CF_K_CLIP = 3,       /* CML full-table clip_by_norm                     */
-    CF_K_SCORE = 4,      /* user x item scoring tile kernel                 */
-    CF_K_TOPK = 5,       /* masked per-user top-k                           */
-    CF_K_COUNT = 6
+    CF_K_SAMPLE = 0,     /* batch draw / load + per-row occurrence counts     */
+    CF_K_STEP = 1,       /* gather + loss + gradients + singleton-row Adagrad  */
+    CF_K_APPLY = 2,      /* Adagrad of duplicated rows from summed gradients  */
+    CF_K_APPLY_DENSE = 3,/* dense item Adagrad (after cross-rank all-reduce)  */
+    CF_K_CLIP = 4,       /* CML full-table clip_by_norm                       */
+    CF_K_SCORE = 5,      /* user x item scoring tile kernel                   */
+    CF_K_TOPK = 6,       /* masked per-user top-k                             */
+    CF_K_COUNT = 7
 };
 
 /*
@@ -89,7 +90,7 @@ typedef struct cf_config {
     int32_t n_factors;        /* d, 1..256                                      */
     int64_t n_users;          /* rows of U held by THIS engine (a user shard)   */
     int64_t n_items;          /* rows of V (replicated on every rank)           */
-    int32_t n_neg;            /* W negatives per (u,i) pair, 1..64              */
+    int32_t n_neg;            /* W negatives per (u,i) pair, 1..64 (CML 1..16)  */
     int32_t gsize;            /* G group users per pair (GBPR), 1..16           */
     float lr;                 /* Adagrad learning rate (constant; see DESIGN)   */
     float reg;                /* L2 coefficient (BPR/GBPR/AMF)                  */
