@@ -31,7 +31,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph  # noqa: E402
+from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_degrees, synth_graph  # noqa: E402,E501
+from collaborativefilteringusingtensorflow_amd.distributed import make_gpu_sharded, shard_users  # noqa: E402,E501
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -137,8 +138,8 @@ def main():
 
     # ---- inputs: this rank's user shard of the synthetic graph ----------------
     nu_all, ni, d, W, B = cfg["n_users"], cfg["n_items"], cfg["d"], cfg["W"], cfg["B"]
-    u0, u1 = rank * nu_all // world, (rank + 1) * nu_all // world
     t0 = time.perf_counter()
+    u0, u1 = shard_users(synth_degrees(nu_all, cfg["mean_degree"], cfg["graph_seed"]), world, rank)
     indptr, indices = synth_graph(nu_all, ni, cfg["mean_degree"], cfg["zipf"], cfg["graph_seed"],
                                   u_begin=u0, u_end=u1, n_threads=min(16, os.cpu_count() or 1))
     log("rank %d: users [%d,%d) nnz %d generated in %.1fs" % (rank, u0, u1, len(indices),
@@ -155,16 +156,12 @@ def main():
         eng.begin_phase(1)
 
     if world > 1:
-        n_grad = ni * d + (ni if cfg["model"] == "gbpr" else 0)
-        gv = torch.zeros(n_grad, dtype=torch.float32, device="cuda:%d" % local_rank)
-        eng.set_stream(torch.cuda.current_stream().cuda_stream)
-        eng.bind_item_grad(gv.data_ptr(), n_grad)
+        step, _grad = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
+                                       torch.device("cuda", local_rank))
 
         def run(k):
             for _ in range(k):
-                eng.step_local(B)
-                dist.all_reduce(gv)
-                eng.step_items()
+                step(B)
 
         def sync():
             torch.cuda.synchronize()

@@ -56,6 +56,7 @@ class PairwiseModel(object):
         self._verbose = verbose
         self._engine = None
         self._train_lr = float(lr)  # the value the optimizer is built with
+        self._init_tables = None
 
     # ---- hooks ----------------------------------------------------------------
     def _engine_kwargs(self):
@@ -129,6 +130,9 @@ class PairwiseModel(object):
         init_seed = self._seed if self._seed is not None else (seed ^ 0x1234567)
         eng.init_params(self._init_mean, self._init_stddev, truncated=self.TRUNCATED_INIT,
                         seed=init_seed)
+        if self._init_tables is not None:
+            for name, arr in self._init_tables.items():
+                eng.set_table(name, arr)
         if device_fed:
             eng.set_sampler_state(*sampler.state())
 
@@ -166,3 +170,12 @@ class PairwiseModel(object):
     @property
     def engine(self):
         return self._engine
+
+    def set_initial_tables(self, user=None, item=None, bias=None):
+        """Start the next ``train`` from these tables instead of the seeded
+        initializer (the reference's TF initializers are unseeded)."""
+        t = {}
+        for name, arr in (("user", user), ("item", item), ("bias", bias)):
+            if arr is not None:
+                t[name] = np.asarray(arr, dtype=np.float32)
+        self._init_tables = t or None

@@ -212,6 +212,15 @@ class Engine(object):
         N.check(self._L.cf_profile_reset(self._h), "cf_profile_reset")
 
 
+def synth_degrees(n_users, mean_degree, seed):
+    """Global indptr (int64, n_users+1) of the synthetic graph's degrees."""
+    L = N.lib()
+    indptr = np.empty(int(n_users) + 1, dtype=np.int64)
+    N.check(L.cf_synth_degrees(int(n_users), float(mean_degree), int(seed), 0, int(n_users),
+                               _ptr(indptr, ctypes.c_int64)), "cf_synth_degrees")
+    return indptr
+
+
 def synth_graph(n_users, n_items, mean_degree, zipf_s, seed, u_begin=0, u_end=None, n_threads=0):
     """CSR (indptr int64, indices int32) of users [u_begin, u_end) of the
     synthetic implicit-feedback graph; host-side, deterministic."""

@@ -1,0 +1,261 @@
+"""Pinning the CPU oracle (no GPU needed).
+
+TF1 is not installable, so the numpy restatement is checked
+against an independent restatement: torch-CPU autograd over a LITERAL
+transcription of the reference's loss graphs (bprmf.py:52-71,
+gbprmf.py:58-89, cml.py:55-109, amf.py:73-115), dense gradients (= the
+dedup-summed IndexedSlices) and TF1 Adagrad; plus finite differences, the C
+restatement (oracle/cf_oracle.c) and the reference's captured batch streams.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import get_stream
+from oracle import cf_oracle as O
+
+TOL = 1e-11
+
+
+def literal_loss(model, U, V, b, pairs, negs, groups, hp, adversarial=False):
+    """Torch transcription of the reference TF graphs."""
+    p = torch.as_tensor(pairs, dtype=torch.long)
+    n = torch.as_tensor(negs, dtype=torch.long)
+    l2 = lambda t: 0.5 * (t * t).sum()                       # tf.nn.l2_loss
+    if model in ("bpr", "amf"):
+        u, i, js = U[p[:, 0]], V[p[:, 1]], V[n]
+        ui = (u * i).sum(1)
+        uj = (u[:, None, :] * js).sum(-1)
+        x = ui[:, None] - uj
+        reg = hp["reg"] * (l2(U[p[:, 0]]) + l2(V[p[:, 1]]) + l2(V[n]))
+        if model == "bpr":
+            return (-torch.log(torch.sigmoid(x))).sum() + reg
+        loss = torch.nn.functional.softplus(-x).sum() + reg
+        if adversarial:   # Δ == 0 (amf.py:117-137 never runs its assigns)
+            xc = torch.clamp(x, -80.0, 1e8)
+            loss = loss + hp["reg_adv"] * torch.nn.functional.softplus(-xc).sum()
+        return loss
+    if model == "gbpr":
+        g = torch.as_tensor(groups, dtype=torch.long)
+        u, i, js, gg = U[p[:, 0]], V[p[:, 1]], V[n], U[g]
+        ui_u = (u * i).sum(-1)
+        ui_g = (gg * i[:, None, :]).sum(dim=(1, 2)) / float(g.shape[1])
+        ui = hp["rho"] * ui_g + (1 - hp["rho"]) * ui_u + b[p[:, 1]]
+        uj = (u[:, None, :] * js).sum(-1) + b[n]
+        reg = hp["reg"] * (l2(U[p[:, 0]]) + l2(U[g]) + l2(V[p[:, 1]]) + l2(b[n]))
+        return (-torch.log(torch.sigmoid(ui[:, None] - uj))).sum() + reg
+    # cml
+    u, i, js = U[p[:, 0]], V[p[:, 1]], V[n]
+    dp = ((u - i) ** 2).sum(1)
+    dn = ((u[:, None, :] - js) ** 2).sum(-1)
+    m = torch.amin(dn, 1)                                    # ties share the gradient
+    loss_pair = torch.relu(dp - m + hp["margin"])
+    if hp["use_rank_weight"]:
+        imp = ((dp[:, None] - dn + hp["margin"]) > 0).double()
+        rw = (imp.mean(1) * V.shape[0]).detach()
+        loss_pair = loss_pair * torch.log(rw + 1.0)
+    loss = loss_pair.sum()
+    if hp["reg_cov"] > 0:
+        loss = loss + hp["reg_cov"] * (l2(U[p[:, 0]]) + l2(V[p[:, 1]]) + l2(V[n]))
+    return loss
+
+
+def torch_step(model, tabs, accs, batch, hp, adversarial=False, lr=0.1):
+    T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tabs.items()}
+    loss = literal_loss(model, T["U"], T["V"], T.get("b"), *batch, hp, adversarial)
+    loss.backward()
+    out = {}
+    for k, t in T.items():
+        g = t.grad.numpy()
+        acc = accs[k] + g * g                                # SparseApplyAdagrad, untouched
+        out[k] = t.detach().numpy() - lr * g / np.sqrt(acc)  # rows have g == 0: exact no-op
+        accs[k] = acc
+    if model == "cml":
+        for k in ("U", "V"):
+            O.clip_rows(out[k], hp["clip_norm"])
+    return float(loss.detach()), out
+
+
+def init(seed, nu=943, ni=1682, d=12, bias=False):
+    rng = np.random.RandomState(seed)
+    t = {"U": O.init_table(rng, (nu, d), dtype=np.float64),
+         "V": O.init_table(rng, (ni, d), dtype=np.float64)}
+    if bias:
+        t["b"] = O.init_table(rng, (ni,), dtype=np.float64)
+    return t
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.mark.parametrize("model,stream,hp", [
+    ("bpr", "rank_b100_w1", dict(reg=0.1)),
+    ("bpr", "rank_b100_w5", dict(reg=0.05)),
+    ("amf", "rank_b100_w5", dict(reg=0.05, reg_adv=1.0)),
+    ("gbpr", "gbpr_b100_g1_w5", dict(reg=0.01, rho=0.4)),
+    ("gbpr", "gbpr_b100_g3_w2", dict(reg=0.02, rho=0.5)),
+    ("cml", "rank_b50_w5", dict(margin=1.0, reg_cov=1.0, use_rank_weight=True, clip_norm=1.0)),
+    ("cml", "rank_b50_w5", dict(margin=0.5, reg_cov=0.0, use_rank_weight=False, clip_norm=0.9)),
+])
+def test_oracle_matches_literal_autograd(streams, model, stream, hp):
+    st = get_stream(streams, stream)
+    tabs = init(3, bias=(model == "gbpr"))
+    ora = {k: v.copy() for k, v in tabs.items()}
+    oacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    tacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    for s in range(6):
+        adv = (model == "amf" and s >= 3)
+        if model == "amf" and s == 3:
+            for acc in (oacc, tacc):
+                for k in acc:
+                    acc[k][...] = 0.1
+        batch = (st["pairs"][s], st["negs"][s], st.get("groups", [None] * 40)[s])
+        lt, tabs = torch_step(model, tabs, tacc, batch, hp, adversarial=adv)
+        if model == "bpr":
+            lo = O.bpr_step(ora["U"], ora["V"], oacc["U"], oacc["V"], batch[0], batch[1], hp["reg"])
+        elif model == "amf":
+            lo = O.amf_step(ora["U"], ora["V"], oacc["U"], oacc["V"], batch[0], batch[1],
+                            hp["reg"], adv, reg_adv=hp["reg_adv"])
+        elif model == "gbpr":
+            lo = O.gbpr_step(ora["U"], ora["V"], ora["b"], oacc["U"], oacc["V"], oacc["b"],
+                             batch[0], batch[1], batch[2], hp["rho"], hp["reg"])
+        else:
+            lo = O.cml_step(ora["U"], ora["V"], oacc["U"], oacc["V"], batch[0], batch[1],
+                            hp["margin"], hp["reg_cov"], hp["clip_norm"],
+                            use_rank_weight=hp["use_rank_weight"])
+        assert abs(lo - lt) <= TOL * abs(lt), (s, lo, lt)
+        for k in tabs:
+            assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
+            assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
+
+
+def test_cml_min_ties_share_gradient():
+    """reduce_min's gradient is split equally between tied negatives."""
+    tabs = init(5, nu=3, ni=6, d=4)
+    tabs["V"][4] = tabs["V"][3]                   # negatives 3 and 4 tie exactly
+    pairs = np.array([[0, 1]])
+    negs = np.array([[3, 4, 5]])
+    hp = dict(margin=10.0, reg_cov=0.0, use_rank_weight=False, clip_norm=100.0)
+    ora = {k: v.copy() for k, v in tabs.items()}
+    acc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    O.cml_step(ora["U"], ora["V"], acc["U"], acc["V"], pairs, negs, 10.0, 0.0, 100.0,
+               use_rank_weight=False)
+    _, out = torch_step("cml", tabs, {k: np.full_like(v, 0.1) for k, v in tabs.items()},
+                        (pairs, negs, None), hp)
+    assert rel(ora["V"], out["V"]) < 1e-12
+    assert np.allclose(ora["V"][3], ora["V"][4])
+
+
+def test_bpr_gradient_finite_differences():
+    rng = np.random.RandomState(0)
+    U = rng.randn(5, 3) * 0.3
+    V = rng.randn(7, 3) * 0.3
+    pairs = np.array([[0, 1], [2, 3], [0, 1], [4, 6]])
+    negs = np.array([[2, 5], [0, 0], [5, 2], [1, 3]])
+    reg = 0.07
+
+    def loss(U_, V_):
+        x, rl, _, _ = O.bpr_loss_grads(U_, V_, pairs, negs, reg)
+        return np.sum(O._neg_log_sigmoid(x)) + rl
+
+    _, _, (ur, ug), (vr, vg) = O.bpr_loss_grads(U, V, pairs, negs, reg)
+    GU = np.zeros_like(U)
+    np.add.at(GU, ur, ug)
+    GV = np.zeros_like(V)
+    np.add.at(GV, vr, vg)
+    h = 1e-6
+    for X, G in ((U, GU), (V, GV)):
+        for idx in np.ndindex(X.shape):
+            old = X[idx]
+            X[idx] = old + h
+            lp = loss(U, V)
+            X[idx] = old - h
+            lm = loss(U, V)
+            X[idx] = old
+            assert abs((lp - lm) / (2 * h) - G[idx]) < 1e-7
+
+
+@pytest.mark.parametrize("model,stream,kw", [
+    ("bpr", "rank_b100_w1", dict(reg=0.1)),
+    ("amf", "rank_b100_w5", dict(reg=0.05)),
+    ("gbpr", "gbpr_b100_g3_w2", dict(reg=0.02, rho=0.5)),
+    ("cml", "rank_b50_w5", dict(margin=1.0, reg_cov=1.0)),
+])
+def test_c_oracle_matches_numpy_oracle(streams, model, stream, kw):
+    from oracle.build_oracle import COracle
+    st = get_stream(streams, stream)
+    W = st["negs"].shape[2]
+    G = st["groups"].shape[2] if "groups" in st else 1
+    tabs = init(7, d=20, bias=(model == "gbpr"))
+    c = COracle(model, tabs["U"], tabs["V"], tabs.get("b"), W=W, G=G, **kw)
+    U, V = tabs["U"].copy(), tabs["V"].copy()
+    b = tabs["b"].copy() if model == "gbpr" else None
+    AU, AV = np.full_like(U, 0.1), np.full_like(V, 0.1)
+    Ab = np.full_like(b, 0.1) if b is not None else None
+    for s in range(15):
+        if model == "amf" and s == 8:
+            c.set_adversarial(True)
+            AU[...] = 0.1
+            AV[...] = 0.1
+        pr, ng = st["pairs"][s], st["negs"][s]
+        gr = st["groups"][s] if "groups" in st else None
+        lc = c.step(pr, ng, gr)
+        if model == "bpr":
+            lo = O.bpr_step(U, V, AU, AV, pr, ng, kw["reg"])
+        elif model == "amf":
+            lo = O.amf_step(U, V, AU, AV, pr, ng, kw["reg"], s >= 8)
+        elif model == "gbpr":
+            lo = O.gbpr_step(U, V, b, AU, AV, Ab, pr, ng, gr, kw["rho"], kw["reg"])
+        else:
+            lo = O.cml_step(U, V, AU, AV, pr, ng, kw["margin"], kw["reg_cov"], 1.0)
+        assert abs(lc - lo) <= 2e-5 * abs(lo), (s, lc, lo)
+    assert rel(c.U, U) < 2e-5 and rel(c.V, V) < 2e-5 and rel(c.AV, AV) < 2e-5
+
+
+@pytest.mark.parametrize("name", ["rank_b100_w1", "rank_b100_w5", "rank_b50_w5", "uij_b100",
+                                  "gbpr_b100_g1_w5", "gbpr_b100_g3_w2"])
+def test_reference_streams_satisfy_sampler_invariants(fold1, streams, name):
+    st = get_stream(streams, name)
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    pos = [set(ix[ip[u]:ip[u + 1]].tolist()) for u in range(943)]
+    tp, tu = O.transpose_csr(ip, ix, 1682)
+    seen = set()
+    for s in range(st["pairs"].shape[0]):
+        for b, (u, i) in enumerate(st["pairs"][s]):
+            assert i in pos[u]
+            assert not any(int(j) in pos[u] for j in st["negs"][s][b])
+            seen.add((int(u), int(i)))
+            if "groups" in st:
+                us = set(tu[tp[i]:tp[i + 1]].tolist())
+                assert all(int(g) in us for g in st["groups"][s][b])
+    assert len(seen) == st["pairs"].shape[0] * st["pairs"].shape[1]   # one epoch: no repeats
+
+
+def test_oracle_stream_restatement(fold1):
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    tp, tu = O.transpose_csr(ip, ix, 1682)
+    rng = np.random.RandomState(0)
+    B = 100
+    per_epoch = len(ix) // B
+    gen = O.sample_stream(ip, ix, 1682, B, 3, per_epoch, rng, gsize=2, indptr_t=tp, indices_t=tu)
+    pos = [set(ix[ip[u]:ip[u + 1]].tolist()) for u in range(943)]
+    keys = set()
+    for pairs, negs, groups in gen:
+        for (u, i), js, gs in zip(pairs, negs, groups):
+            assert i in pos[u] and not any(int(j) in pos[u] for j in js)
+            assert all(int(i) in pos[int(g)] for g in gs)
+            keys.add((int(u), int(i)))
+    assert len(keys) == per_epoch * B
+
+
+def test_recommend_filter_equivalence():
+    rng = np.random.RandomState(1)
+    S = rng.randn(30, 200)
+    S[:, 50] = S[:, 51]                                     # a tie: lower id first
+    sets = [set(rng.choice(200, rng.randint(1, 60), replace=False).tolist()) for _ in range(30)]
+    ip = np.concatenate([[0], np.cumsum([len(s) for s in sets])])
+    ix = np.concatenate([sorted(s) for s in sets]).astype(np.int32)
+    a = O.recommend(S, ip, ix, list(range(30)), 10)
+    b = O.recommend_literal(S, sets, 10)
+    assert a == b
