@@ -59,11 +59,12 @@ class COracle(object):
         self.L.oracle_train.argtypes = ([ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_void_p])
-        self.U = np.ascontiguousarray(U, np.float32)
-        self.V = np.ascontiguousarray(V, np.float32)
+        self.U = np.array(U, dtype=np.float32, order="C", copy=True)   # never alias the caller
+        self.V = np.array(V, dtype=np.float32, order="C", copy=True)
         nu, d = self.U.shape
         ni = self.V.shape[0]
-        self.b = np.ascontiguousarray(b, np.float32) if b is not None else np.zeros(1, np.float32)
+        self.b = (np.array(b, dtype=np.float32, copy=True) if b is not None
+                  else np.zeros(1, np.float32))
         self.AU = np.full_like(self.U, 0.1)
         self.AV = np.full_like(self.V, 0.1)
         self.Ab = np.full_like(self.b, 0.1)
