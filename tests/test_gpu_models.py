@@ -102,8 +102,12 @@ def test_device_sampled_drivers_train(fold1):
     for model, sampler in runs:
         scores = model.train(1, tra, tst, sampler)
         assert len(scores) == 5
-        # random recommendation on ml-100k gives precision@10 ~ 0.01
-        assert scores[0] > 0.05, (type(model).__name__, scores)
+        if isinstance(model, CML):
+            # CML returns the topN=1000 scores (cml.py:203-212): recall@1000
+            assert scores[1] > 0.5, scores
+        else:
+            # random recommendation on ml-100k gives precision@10 ~ 0.01
+            assert scores[0] > 0.05, (type(model).__name__, scores)
         st = sampler.state()
         assert st[0] >= 3  # the sampler stream advanced with training
         model.close()
