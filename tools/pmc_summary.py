@@ -1,0 +1,89 @@
+"""Summarise rocprofv3 PMC passes into profiles/pmc_traffic.json.
+
+    python tools/pmc_summary.py <tag> <fetch_dir> <write_dir> [trace_dir]
+
+HBM bytes per launch, per kernel, from the TCC counters as
+MI355X_MICROARCH.md prescribes: FETCH_SIZE and WRITE_SIZE come from separate
+passes (they cannot share the TCC slots); both are in KiB; on gfx950
+FETCH_SIZE reports exactly half of the bytes of a WIDE COALESCED streaming
+read, so ``fetch_bytes_corrected = 2 * FETCH_SIZE * 1024`` is reported next
+to the raw value (our row gathers are 64-B segments per 16-lane group, an
+access width the guide lists as uncalibrated -- see DESIGN.md).  Infinity
+Cache hits are counted by these counters, not excluded.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SHORT = {"grad_kernel": "step", "prep_kernel": "sample", "apply_kernel": "apply",
+         "apply_dense_kernel": "apply_dense", "clip_full_kernel": "clip",
+         "score_kernel": "score", "topk_kernel": "topk"}
+
+
+def short(name):
+    for k, v in SHORT.items():
+        if k in name:
+            return v
+    return None
+
+
+def per_kernel(d, counter):
+    acc = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] != counter:
+                    continue
+                k = short(row["Kernel_Name"])
+                if k:
+                    acc[k].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def durations(d):
+    out = {}
+    for path in glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = short(row["Name"])
+                if k:
+                    out[k] = float(row["AverageNs"])
+    return out
+
+
+def main():
+    tag, fdir, wdir = sys.argv[1:4]
+    tdir = sys.argv[4] if len(sys.argv) > 4 else None
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    dur = durations(tdir) if tdir else {}
+    rec = {}
+    for k in sorted(set(fetch) | set(write)):
+        f_raw = fetch.get(k, 0.0) * 1024.0
+        w = write.get(k, 0.0) * 1024.0
+        r = {"fetch_bytes_raw": f_raw, "fetch_bytes_corrected": 2.0 * f_raw,
+             "write_bytes": w, "hbm_bytes_corrected": 2.0 * f_raw + w}
+        if k in dur:
+            r["rocprof_avg_ns"] = dur[k]
+            r["hbm_GBps_corrected"] = r["hbm_bytes_corrected"] / dur[k]
+        rec[k] = r
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    data = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            data = json.load(f)
+    data[tag] = {"kernels": rec,
+                 "step_hbm_bytes_per_launch": rec.get("step", {}).get("hbm_bytes_corrected"),
+                 "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+                           "KiB -> bytes, FETCH x2 gfx950 correction"}
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1)
+    print(json.dumps(data[tag], indent=1))
+
+
+if __name__ == "__main__":
+    main()
