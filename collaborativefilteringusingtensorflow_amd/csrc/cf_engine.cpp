@@ -76,12 +76,18 @@ struct cf_engine {
     float *AU = nullptr, *AV = nullptr, *Ab = nullptr;
     float *GU = nullptr, *GV = nullptr, *Gb = nullptr;
     float *GV_own = nullptr, *Gb_own = nullptr;
-    int32_t *cntU = nullptr, *cntV = nullptr;  // per-row occurrence counts (0 between steps)
+    int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
+    int32_t* cntV_[2] = {nullptr, nullptr};
 
-    // batch
+    // batch: two buffer sets, so that the sampler of step s+1 runs on the side
+    // stream while step s's gradient and apply kernels run on the main stream
     int Bcap = 0;
-    int32_t *occU = nullptr, *occV = nullptr;
-    int32_t *rankU = nullptr, *rankV = nullptr;
+    int32_t* occU_[2] = {nullptr, nullptr};
+    int32_t* occV_[2] = {nullptr, nullptr};
+    int set = 0;
+    hipStream_t side = nullptr;
+    hipEvent_t prep_done[2] = {nullptr, nullptr};
+    hipEvent_t apply_done[2] = {nullptr, nullptr};
     double* loss_partial = nullptr;
     double* loss = nullptr;   // [0] running accumulator, [1] per-call scratch
     double* h_loss = nullptr; // pinned
@@ -117,6 +123,7 @@ int set_dev(cf_engine* e) {
 struct ProfScope {
     cf_engine* e;
     int k;
+    hipStream_t s;
     hipEvent_t a = nullptr, z = nullptr;
     static hipEvent_t get(cf_engine* e) {
         hipEvent_t x = nullptr;
@@ -128,15 +135,16 @@ struct ProfScope {
         }
         return x;
     }
-    ProfScope(cf_engine* e_, int k_) : e(e_), k(k_) {
+    ProfScope(cf_engine* e_, int k_, hipStream_t s_ = nullptr) : e(e_), k(k_), s(s_) {
         if (!e->prof) return;
+        if (!s) s = e->stream;
         a = get(e);
         z = get(e);
-        if (a) (void)hipEventRecord(a, e->stream);
+        if (a) (void)hipEventRecord(a, s);
     }
     ~ProfScope() {
         if (!a || !z) return;
-        (void)hipEventRecord(z, e->stream);
+        (void)hipEventRecord(z, s);
         e->ev[k].emplace_back(a, z);
     }
 };
@@ -147,23 +155,23 @@ int group_count(const cf_config& c) { return c.model == CF_GBPR ? c.gsize : 0; }
 
 int ensure_batch(cf_engine* e, int B) {
     if (B <= e->Bcap) return CF_OK;
-    dfree(e->occU);
-    dfree(e->occV);
-    dfree(e->rankU);
-    dfree(e->rankV);
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipStreamSynchronize(e->side));
     dfree(e->loss_partial);
     const size_t nU = (size_t)B * users_per_pair(e->cfg);
     const size_t nV = (size_t)B * items_per_pair(e->cfg);
-    CF_TRY(dalloc(&e->occU, nU));
-    CF_TRY(dalloc(&e->occV, nV));
-    CF_TRY(dalloc(&e->rankU, nU));
-    CF_TRY(dalloc(&e->rankV, nV));
+    for (int k = 0; k < 2; ++k) {
+        dfree(e->occU_[k]);
+        dfree(e->occV_[k]);
+        CF_TRY(dalloc(&e->occU_[k], nU));
+        CF_TRY(dalloc(&e->occV_[k], nV));
+    }
     CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks(B)));
     e->Bcap = B;
     return CF_OK;
 }
 
-StepArgs base_step_args(cf_engine* e, int B) {
+StepArgs base_step_args(cf_engine* e, int B, int k) {
     const cf_config& c = e->cfg;
     StepArgs a{};
     a.model = c.model;
@@ -191,12 +199,10 @@ StepArgs base_step_args(cf_engine* e, int B) {
     a.lr = c.lr;
     a.clip_norm = c.clip_norm;
     a.clip = c.model == CF_CML ? 1 : 0;
-    a.occU = e->occU;
-    a.occV = e->occV;
-    a.rankU = e->rankU;
-    a.rankV = e->rankV;
-    a.cntU = e->cntU;
-    a.cntV = e->cntV;
+    a.occU = e->occU_[k];
+    a.occV = e->occV_[k];
+    a.cntU = e->cntU_[k];
+    a.cntV = e->cntV_[k];
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
     a.count_items = c.dense_item_apply ? 0 : 1;
@@ -229,7 +235,7 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
 }
 
 int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
-                     const int32_t* groups, int B) {
+                     const int32_t* groups, int B, int k) {
     const cf_config& c = e->cfg;
     const int W = c.n_neg, G = group_count(c);
     if (!pairs || !negs) return fail(CF_EINVAL, "pairs and negs are required");
@@ -267,28 +273,36 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
             su[B + (size_t)p * G + k] = g;
         }
     }
-    CF_HIP(hipMemcpyAsync(e->occU, su, nU * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
-    CF_HIP(hipMemcpyAsync(e->occV, sv, nV * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
-    CF_HIP(hipEventRecord(e->stage_ev, e->stream));
+    CF_HIP(hipMemcpyAsync(e->occU_[k], su, nU * sizeof(int32_t), hipMemcpyHostToDevice, e->side));
+    CF_HIP(hipMemcpyAsync(e->occV_[k], sv, nV * sizeof(int32_t), hipMemcpyHostToDevice, e->side));
+    CF_HIP(hipEventRecord(e->stage_ev, e->side));
     return CF_OK;
 }
 
-// step kernel + user (and, in sparse mode, item) apply; loss added to *loss_acc
+// One step: [side] sample/load + count into buffer set k; [main] gradient +
+// singleton apply, duplicate apply (+ CML clip).  The side stream runs one
+// step ahead: prep(s+1) overlaps grad/apply(s).  Loss added to *loss_acc.
 int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
              const int32_t* groups, double* loss_acc) {
     const cf_config& c = e->cfg;
     CF_TRY(ensure_batch(e, B));
-    StepArgs a = base_step_args(e, B);
+    const int k = e->set;
+    e->set ^= 1;
+    StepArgs a = base_step_args(e, B, k);
+    // set k was last used by step s-2: its apply must be done before reuse
+    CF_HIP(hipStreamWaitEvent(e->side, e->apply_done[k], 0));
     if (pairs) {
-        CF_TRY(stage_host_batch(e, pairs, negs, groups, B));
+        CF_TRY(stage_host_batch(e, pairs, negs, groups, B, k));
         a.sample = 0;
     } else {
         CF_TRY(sampler_args(e, B, &a));
     }
     {
-        ProfScope ps(e, CF_K_SAMPLE);
-        CF_HIP(launch_prep(a, e->stream));
+        ProfScope ps(e, CF_K_SAMPLE, e->side);
+        CF_HIP(launch_prep(a, e->side));
     }
+    CF_HIP(hipEventRecord(e->prep_done[k], e->side));
+    CF_HIP(hipStreamWaitEvent(e->stream, e->prep_done[k], 0));
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
@@ -298,16 +312,11 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
     p.clip = c.model == CF_CML ? 1 : 0;
-    p.nU = B * users_per_pair(c);
-    p.nV = B * items_per_pair(c);
-    const int per_block = kWavesPerBlock * kWave;
-    p.blocksU = (p.nU + per_block - 1) / per_block;
-    p.occU = e->occU;
-    p.occV = e->occV;
-    p.rankU = e->rankU;
-    p.rankV = e->rankV;
-    p.cntU = e->cntU;
-    p.cntV = e->cntV;
+    p.n_users = c.n_users;
+    p.n_items = c.n_items;
+    p.blocksU = (int)((c.n_users + kApplyRowsPerBlock - 1) / kApplyRowsPerBlock);
+    p.cntU = e->cntU_[k];
+    p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
     p.V = e->V; p.AV = e->AV; p.GV = e->GV;
     p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
@@ -319,17 +328,16 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
         ProfScope ps(e, CF_K_APPLY);
         CF_HIP(launch_apply(p, e->stream));
     }
+    CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
     if (e->need_clip_U) {
         ProfScope ps(e, CF_K_CLIP);
         CF_HIP(launch_clip_full(e->U, c.n_users, c.n_factors, c.clip_norm, e->stream));
         e->need_clip_U = false;
     }
-    if (!c.dense_item_apply) {
-        if (e->need_clip_V) {
-            ProfScope ps(e, CF_K_CLIP);
-            CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
-            e->need_clip_V = false;
-        }
+    if (!c.dense_item_apply && e->need_clip_V) {
+        ProfScope ps(e, CF_K_CLIP);
+        CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
+        e->need_clip_V = false;
     }
     return CF_OK;
 }
@@ -451,13 +459,20 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(CF_EHIP, "hipStreamCreate failed"));
     e->own_stream = true;
+    if (hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(CF_EHIP, "hipStreamCreate failed"));
     if (hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail(CF_EHIP, "hipEventCreate failed"));
+    for (int k = 0; k < 2; ++k)
+        if (hipEventCreateWithFlags(&e->prep_done[k], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e->apply_done[k], hipEventDisableTiming) != hipSuccess)
+            return bail(fail(CF_EHIP, "hipEventCreate failed"));
     (void)hipEventRecord(e->stage_ev, e->stream);
     const size_t ud = (size_t)c.n_users * c.n_factors, id = (size_t)c.n_items * c.n_factors;
     if ((r = dalloc(&e->U, ud)) || (r = dalloc(&e->AU, ud)) || (r = dalloc(&e->GU, ud)) ||
         (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
-        (r = dalloc(&e->cntU, (size_t)c.n_users)) || (r = dalloc(&e->cntV, (size_t)c.n_items)) ||
+        (r = dalloc(&e->cntU_[0], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[0], (size_t)c.n_items)) ||
+        (r = dalloc(&e->cntU_[1], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[1], (size_t)c.n_items)) ||
         (r = dalloc(&e->loss, 2)))
         return bail(r);
     if (c.model == CF_GBPR) {
@@ -474,8 +489,10 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         hipMemsetAsync(e->GV, 0, id * 4, s) != hipSuccess ||
         hipMemsetAsync(e->U, 0, ud * 4, s) != hipSuccess ||
         hipMemsetAsync(e->V, 0, id * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->cntU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->cntV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntU_[0], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->cntV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
         hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
         return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
     if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
@@ -497,6 +514,7 @@ int cf_destroy(cf_engine* e) {
     if (!e) return CF_OK;
     (void)hipSetDevice(e->cfg.device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->side) (void)hipStreamSynchronize(e->side);
     for (auto& v : e->ev)
         for (auto& pr : v) {
             (void)hipEventDestroy(pr.first);
@@ -505,13 +523,18 @@ int cf_destroy(cf_engine* e) {
     for (auto x : e->ev_pool) (void)hipEventDestroy(x);
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
-    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own); dfree(e->cntU); dfree(e->cntV);
-    dfree(e->occU); dfree(e->occV); dfree(e->rankU); dfree(e->rankV);
+    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
+    for (int k = 0; k < 2; ++k) {
+        dfree(e->cntU_[k]); dfree(e->cntV_[k]); dfree(e->occU_[k]); dfree(e->occV_[k]);
+        if (e->prep_done[k]) (void)hipEventDestroy(e->prep_done[k]);
+        if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
+    }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->side) (void)hipStreamDestroy(e->side);
     delete e;
     return CF_OK;
 }
@@ -532,6 +555,7 @@ int cf_set_stream(cf_engine* e, void* s) {
 
 int cf_synchronize(cf_engine* e) {
     CF_TRY(check_engine(e));
+    CF_HIP(hipStreamSynchronize(e->side));
     CF_HIP(hipStreamSynchronize(e->stream));
     return CF_OK;
 }
@@ -619,6 +643,7 @@ int cf_set_table(cf_engine* e, int32_t t, const float* src, int64_t n) {
 
 int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
     CF_TRY(check_engine(e));
+    CF_HIP(hipStreamSynchronize(e->side));
     int64_t want = 0;
     float* p = table_ptr(e, t, &want);
     if (!p) return fail(CF_EINVAL, "table not present in this model");
@@ -663,16 +688,19 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
     const int W = c.n_neg, G = group_count(c);
     if (G > 0 && !groups) return fail(CF_EINVAL, "GBPR needs a groups buffer");
     CF_TRY(ensure_batch(e, B));
-    StepArgs a = base_step_args(e, B);
+    const int k = e->set;
+    e->set ^= 1;
+    StepArgs a = base_step_args(e, B, k);
     CF_TRY(sampler_args(e, B, &a));
     a.count_users = 0;
     a.count_items = 0;
-    CF_HIP(launch_prep(a, e->stream));
+    CF_HIP(hipStreamWaitEvent(e->side, e->apply_done[k], 0));
+    CF_HIP(launch_prep(a, e->side));
     const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
     std::vector<int32_t> hu(nU), hv(nV);
-    CF_HIP(hipStreamSynchronize(e->stream));
-    CF_HIP(hipMemcpy(hu.data(), e->occU, nU * 4, hipMemcpyDeviceToHost));
-    CF_HIP(hipMemcpy(hv.data(), e->occV, nV * 4, hipMemcpyDeviceToHost));
+    CF_HIP(hipStreamSynchronize(e->side));
+    CF_HIP(hipMemcpy(hu.data(), e->occU_[k], nU * 4, hipMemcpyDeviceToHost));
+    CF_HIP(hipMemcpy(hv.data(), e->occV_[k], nV * 4, hipMemcpyDeviceToHost));
     for (int p = 0; p < B; ++p) {
         pairs[2 * p] = hu[p];
         pairs[2 * p + 1] = hv[p];

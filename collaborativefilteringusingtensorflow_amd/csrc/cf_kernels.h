@@ -62,11 +62,9 @@ struct StepArgs {
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
     float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
     float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;
-    // batch occurrence lists, per-occurrence rank, per-row counts
+    // batch occurrence lists and per-row counts
     int32_t* __restrict__ occU;   // [B*(1+G)] u | groups
     int32_t* __restrict__ occV;   // [B*(1+W)] i | negatives
-    int32_t* __restrict__ rankU;  // arrival rank of the occurrence on its row
-    int32_t* __restrict__ rankV;
     int32_t* __restrict__ cntU;   // [n_users] occurrences in this batch (0 between steps)
     int32_t* __restrict__ cntV;   // [n_items]
     double* __restrict__ loss_partial;  // [grad grid]
@@ -77,12 +75,9 @@ struct ApplyArgs {
     float lr;
     float clip_norm;
     int clip;            // CML: clip updated rows
-    int nU, nV;          // occurrences of each table
-    int blocksU;         // blocks [0, blocksU) serve U, the rest serve V
-    const int32_t* __restrict__ occU;
-    const int32_t* __restrict__ occV;
-    const int32_t* __restrict__ rankU;
-    const int32_t* __restrict__ rankV;
+    // row ranges scanned for duplicated rows (count > 1): users then items
+    int64_t n_users, n_items;
+    int blocksU;         // blocks [0, blocksU) scan user rows, the rest item rows
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -94,6 +89,8 @@ struct ApplyArgs {
     int n_partial;
     double* __restrict__ loss_acc;
 };
+
+constexpr int kApplyRowsPerBlock = kBlock * 4;   // one int4 of counts per thread
 
 struct DenseArgs {
     int d;

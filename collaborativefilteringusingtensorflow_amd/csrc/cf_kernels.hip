@@ -10,8 +10,7 @@
 //                (one coalesced pass, group-OR of hit masks, redraw only the
 //                rejected ones), G group users from the item's CSC column --
 //                or take a host-fed batch; then count every touched row's
-//                occurrences in the batch (one returning atomicAdd per
-//                occurrence: the value is its arrival rank).
+//                occurrences in the batch (one no-return atomicAdd each).
 //  grad_kernel   gather U[u], V[i], V[j] (+U[g], b) rows, group-reduce the
 //                dots / distances, evaluate the loss and dL/dx, form every
 //                per-occurrence gradient row.  A row that occurs ONCE in the
@@ -22,8 +21,9 @@
 //                accumulator (float atomics, 64-B segments), so duplicates
 //                SUM before the update: TF1's _deduplicate_indexed_slices
 //                (SURVEY 0.4).
-//  apply_kernel  the rank-0 occurrence of every duplicated row applies the
-//                summed gradient, zeroes the accumulator and the count.
+//  apply_kernel  scans the count arrays (int4 per lane) and applies the
+//                summed gradient of every duplicated row (count > 1), then
+//                zeroes its accumulator row and count.
 //
 // Reference semantics: src/models/pl/models/bprmf.py:52-88,
 // gbprmf.py:58-106, cml.py:55-129, src/models/others/models/amf.py:66-162;
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
         } else if (gl < nw) {
             j = a.occV[B + p * W + w];
         }
-        if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
+        if (a.count_items && gl < nw) atomicAdd(&a.cntV[j], 1);
     }
     if (MODEL == GBPR && gl < G) {
         int32_t g;
@@ -229,15 +229,15 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
         } else {
             g = a.occU[B + p * G + gl];
         }
-        if (a.count_users) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
+        if (a.count_users) atomicAdd(&a.cntU[g], 1);
     }
     if (gl == 0) {
         if (a.sample) {
             a.occU[p] = u;
             a.occV[p] = i;
         }
-        if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
-        if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
+        if (a.count_users) atomicAdd(&a.cntU[u], 1);
+        if (a.count_items) atomicAdd(&a.cntV[i], 1);
     }
 }
 
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// apply the summed gradient of every duplicated row (rank-0 occurrence)
+// apply the summed gradient of every duplicated row (count > 1)
 // ---------------------------------------------------------------------------
 template <int EPL>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
@@ -473,50 +473,57 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
         if (threadIdx.x == 0) a.loss_acc[0] += (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
     const bool isU = (int)blockIdx.x < a.blocksU;
-    const int blk = isU ? (int)blockIdx.x : (int)blockIdx.x - a.blocksU;
-    const int n = isU ? a.nU : a.nV;
-    const int32_t* occ = isU ? a.occU : a.occV;
-    const int32_t* rank = isU ? a.rankU : a.rankV;
+    const int64_t blk = isU ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - a.blocksU;
+    const int64_t n = isU ? a.n_users : a.n_items;
     int32_t* cnt = isU ? a.cntU : a.cntV;
     float* X = isU ? a.U : a.V;
     float* A = isU ? a.AU : a.AV;
     float* G = isU ? a.GU : a.GV;
+    const bool bias = !isU && a.b != nullptr;
 
-    const int o = (blk * kWavesPerBlock + wv) * kWave + lane;
-    int r_l = 0;
-    bool win = false;
-    if (o < n && rank[o] == 0) {
-        r_l = occ[o];
-        win = cnt[r_l] > 1;
-    }
-    if (!isU && a.b != nullptr && win) {
-        const float g = a.Gb[r_l];
-        const float acc = fmaf(g, g, a.Ab[r_l]);
-        a.Ab[r_l] = acc;
-        a.b[r_l] -= (a.lr * g) / sqrtf(acc);
-        a.Gb[r_l] = 0.f;
-    }
-    const unsigned long long m = __ballot(win);
-    const int nwin = __popcll(m);
-    for (int base = 0; base < nwin; base += 4) {
-        const int my = base + gw;
-        unsigned long long mm = m;
-        for (int t = 0; t < my && mm; ++t) mm &= mm - 1ull;
-        const int pos = (my < nwin) ? __ffsll((long long)mm) - 1 : 0;
-        const int r = __shfl(r_l, pos, 64);
-        if (my < nwin) {  // group-uniform
-            float g[EPL], x[EPL];
-            gload<EPL>(G, r, a.d, gl, g);
-            gload<EPL>(X, r, a.d, gl, x);
-            float* gr = G + (int64_t)r * a.d;
+    const int64_t r0 = blk * kApplyRowsPerBlock + (int64_t)threadIdx.x * 4;
+    int c4[4];
+    if (r0 + 3 < n) {
+        const int4 v = *reinterpret_cast<const int4*>(cnt + r0);
+        c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
+    } else {
 #pragma unroll
-            for (int s = 0; s < EPL; ++s) {
-                const int e = s * kGL + gl;
-                if (e < a.d) gr[e] = 0.f;
-            }
-            gapply<EPL>(X, A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
-            if (gl == 0) cnt[r] = 0;
+        for (int q = 0; q < 4; ++q) c4[q] = (r0 + q < n) ? cnt[r0 + q] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bool win = c4[q] > 1;
+        const int64_t r_l = r0 + q;
+        if (bias && win) {
+            const float g = a.Gb[r_l];
+            const float acc = fmaf(g, g, a.Ab[r_l]);
+            a.Ab[r_l] = acc;
+            a.b[r_l] -= (a.lr * g) / sqrtf(acc);
+            a.Gb[r_l] = 0.f;
         }
+        const unsigned long long m = __ballot(win);
+        const int nwin = __popcll(m);
+        for (int base = 0; base < nwin; base += 4) {  // wave-uniform
+            const int my = base + gw;
+            unsigned long long mm = m;
+            for (int t = 0; t < my && mm; ++t) mm &= mm - 1ull;
+            const int pos = (my < nwin) ? __ffsll((long long)mm) - 1 : 0;
+            const int64_t r = blk * kApplyRowsPerBlock +
+                              __shfl((int)threadIdx.x * 4 + q, pos, 64);  // row of lane pos
+            if (my < nwin) {  // group-uniform
+                float g[EPL], x[EPL];
+                gload<EPL>(G, r, a.d, gl, g);
+                gload<EPL>(X, r, a.d, gl, x);
+                float* gr = G + r * a.d;
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    const int e = s * kGL + gl;
+                    if (e < a.d) gr[e] = 0.f;
+                }
+                gapply<EPL>(X, A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
+            }
+        }
+        if (win) cnt[r_l] = 0;
     }
 }
 
@@ -659,8 +666,7 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
-    const int per_block = kWavesPerBlock * kWave;
-    const int bV = a.apply_items ? (a.nV + per_block - 1) / per_block : 0;
+    const int bV = a.apply_items ? (int)((a.n_items + kApplyRowsPerBlock - 1) / kApplyRowsPerBlock) : 0;
     int blocks = a.blocksU + bV;
     if (blocks == 0) blocks = 1;  // block 0 still reduces the loss
     const dim3 grid(blocks), block(kBlock);
