@@ -244,13 +244,46 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 // grad: gather, loss, gradient rows, singleton apply / duplicate scatter
 // ---------------------------------------------------------------------------
-template <int MODEL, int EPL>
+// Negative-item rows of one pair.  With a compile-time W (WT > 0) every index,
+// count and row is fetched up front -- the whole pair's gather is in flight
+// at once; WT == 0 is the generic runtime-W path that loads per negative.
+template <int EPL, int WT>
+struct NegRows {
+    static constexpr int N = WT > 0 ? WT : 1;
+    int j[N];
+    int c[N];
+    float v[N][EPL];
+    __device__ __forceinline__ void prefetch(const StepArgs& a, int p, int gl) {
+        if constexpr (WT > 0) {
+#pragma unroll
+            for (int w = 0; w < WT; ++w) j[w] = a.occV[a.B + p * WT + w];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                c[w] = a.count_items ? a.cntV[j[w]] : 0;
+                gload<EPL>(a.V, j[w], a.d, gl, v[w]);
+            }
+        }
+    }
+    // slot holding negative w (loads it first on the generic path)
+    __device__ __forceinline__ int get(const StepArgs& a, int p, int w, int gl) {
+        if constexpr (WT > 0) {
+            return w;
+        } else {
+            j[0] = a.occV[a.B + p * a.W + w];
+            c[0] = a.count_items ? a.cntV[j[0]] : 0;
+            gload<EPL>(a.V, j[0], a.d, gl, v[0]);
+            return 0;
+        }
+    }
+};
+
+template <int MODEL, int EPL, int WT>
 __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
     __shared__ double s_loss[kGroupsPerBlock];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
     const int d = a.d;
-    const int W = a.W;
+    const int W = WT > 0 ? WT : a.W;
     const int G = (MODEL == GBPR) ? a.G : 0;
     const int B = a.B;
     float loss_g = 0.f;  // group-uniform: embedding loss (+ GBPR bias L2)
@@ -261,6 +294,8 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
         if (p >= B) break;  // group-uniform
         const int u = a.occU[p];
         const int i = a.occV[p];
+        NegRows<EPL, WT> J;
+        J.prefetch(a, p, gl);
         const int cu = a.count_users ? a.cntU[u] : 0;
         const int ci = a.count_items ? a.cntV[i] : 0;
         float uu[EPL], vi[EPL];
@@ -274,12 +309,10 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
             float sc = 0.f;
+#pragma unroll
             for (int w = 0; w < W; ++w) {
-                const int j = a.occV[B + p * W + w];
-                const int cj = a.count_items ? a.cntV[j] : 0;
-                float vj[EPL];
-                gload<EPL>(a.V, j, d, gl, vj);
-                const float x = ui - gdot<EPL>(uu, vj);
+                const int sl = J.get(a, p, w, gl);
+                const float x = ui - gdot<EPL>(uu, J.v[sl]);
                 float c = -1.f / (1.f + expf(x));
                 if (MODEL == AMF) {
                     loss_g += softplus(-x);
@@ -296,11 +329,11 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                 float gj[EPL];
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
-                    gu[s] = fmaf(c, vi[s] - vj[s], gu[s]);
-                    gj[s] = -c * uu[s] + a.reg * vj[s];
-                    sq = fmaf(vj[s], vj[s], sq);
+                    gu[s] = fmaf(c, vi[s] - J.v[sl][s], gu[s]);
+                    gj[s] = -c * uu[s] + a.reg * J.v[sl][s];
+                    sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
                 }
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], d, gl, J.v[sl], gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -334,24 +367,23 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
             float sc = 0.f;
+#pragma unroll
             for (int w = 0; w < W; ++w) {
-                const int j = a.occV[B + p * W + w];
-                const int cj = a.count_items ? a.cntV[j] : 0;
+                const int sl = J.get(a, p, w, gl);
+                const int j = J.j[sl];
                 const float bj = a.b[j];
-                float vj[EPL];
-                gload<EPL>(a.V, j, d, gl, vj);
-                const float x = ui - (gdot<EPL>(uu, vj) + bj);
+                const float x = ui - (gdot<EPL>(uu, J.v[sl]) + bj);
                 const float c = -1.f / (1.f + expf(x));
                 loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj * bj;
                 sc += c;
                 float gj[EPL];
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
-                    gu[s] = fmaf(-c, vj[s], gu[s]);
+                    gu[s] = fmaf(-c, J.v[sl][s], gu[s]);
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
-                if (gl == 0) bias_finish(a, j, cj, -c + a.reg * bj);
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
+                if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, J.c[sl], d, gl, J.v[sl], gj, a);
             }
             const float rg = a.rho / Gf;
             float gi[EPL];
@@ -382,11 +414,12 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
             float dn_lane = 0.f;
             float m = INFINITY;
             int imp = 0;
-            for (int w = 0; w < W; ++w) {
-                float vj[EPL], t[EPL];
-                gload<EPL>(a.V, a.occV[B + p * W + w], d, gl, vj);
 #pragma unroll
-                for (int s = 0; s < EPL; ++s) t[s] = uu[s] - vj[s];
+            for (int w = 0; w < W; ++w) {
+                const int sl = J.get(a, p, w, gl);
+                float t[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) t[s] = uu[s] - J.v[sl][s];
                 const float dn = gdot<EPL>(t, t);
                 if (gl == w) dn_lane = dn;
                 m = fminf(m, dn);
@@ -406,26 +439,25 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                 gu[s] = 2.f * aa * du[s];
                 gi[s] = -2.f * aa * du[s];
             }
+#pragma unroll
             for (int w = 0; w < W; ++w) {
                 const float dnw = __shfl(dn_lane, w, kGL);
                 const float share = (dnw == m) ? 1.f / cnt : 0.f;
-                const int j = a.occV[B + p * W + w];
-                const int cj = a.count_items ? a.cntV[j] : 0;
-                float vj[EPL], gj[EPL];
-                gload<EPL>(a.V, j, d, gl, vj);
+                const int sl = J.get(a, p, w, gl);  // generic path reloads the row
+                float gj[EPL];
                 const float coef = 2.f * aa * share;
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
-                    const float dv = uu[s] - vj[s];
+                    const float dv = uu[s] - J.v[sl][s];
                     gu[s] = fmaf(-coef, dv, gu[s]);
                     gj[s] = coef * dv;
                     if (l2) {
-                        gj[s] += a.reg_cov * vj[s];
-                        sq = fmaf(vj[s], vj[s], sq);
+                        gj[s] += a.reg_cov * J.v[sl][s];
+                        sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
                     }
                 }
                 // a touched row with a zero gradient is still clipped (cml.py:128-129)
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, cj, d, gl, vj, gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], d, gl, J.v[sl], gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -642,17 +674,27 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int MODEL>
-static hipError_t launch_grad_m(const StepArgs& a, hipStream_t s) {
+template <int MODEL, int WT>
+static hipError_t launch_grad_w(const StepArgs& a, hipStream_t s) {
     const dim3 grid(grad_blocks(a.B)), block(kBlock);
     switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4, WT>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8, WT>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16, WT>), grid, block, 0, s, a); break;
     }
     return hipGetLastError();
+}
+
+// W = 1 (BPRMF driver) and W = 5 (AMF / CML / GBPR drivers) get the
+// fully-prefetched specialisation; other W and d = 256 use the generic path
+template <int MODEL>
+static hipError_t launch_grad_m(const StepArgs& a, hipStream_t s) {
+    const int e = epl_for(a.d);
+    if (a.W == 1) return launch_grad_w<MODEL, 1>(a, s);
+    if (a.W == 5 && e <= 8) return launch_grad_w<MODEL, 5>(a, s);
+    return launch_grad_w<MODEL, 0>(a, s);
 }
 
 hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
