@@ -130,11 +130,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     torch = None
+    # CF_DIST_BACKEND=gloo + CF_SHARE_DEVICE=1 rehearse the N>1 path with all
+    # ranks on device 0 of a one-GPU box (RCCL refuses duplicate devices)
+    backend = os.environ.get("CF_DIST_BACKEND", "nccl")
+    if os.environ.get("CF_SHARE_DEVICE") == "1":
+        local_rank = 0
     if world > 1:
         import torch  # noqa: F811
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     # ---- inputs: this rank's user shard of the synthetic graph ----------------
     nu_all, ni, d, W, B = cfg["n_users"], cfg["n_items"], cfg["d"], cfg["W"], cfg["B"]

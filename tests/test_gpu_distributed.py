@@ -1,0 +1,91 @@
+"""Two ranks of the user-sharded data-parallel step on the REAL engine.
+
+Both ranks share device 0 of the one-GPU test box and all-reduce the bound
+item-gradient tensor with gloo (RCCL refuses two ranks on one device; on the
+8-GPU node bench.py uses nccl = RCCL with the same ShardedStep).  After K
+steps every rank's user shard and the replicated item table must equal the
+float64 oracle run on the concatenated batches (1e-5 relative).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fold, batches, U0, V0, model, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_sharded,
+                                                                       shard_users, local_csr)
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    ip, ix = fold["train_indptr"], fold["train_indices"]
+    u0, u1 = shard_users(ip, world, rank)
+    lip, lix = local_csr(ip, ix, u0, u1)
+    W = batches[0][1].shape[1]
+    kw = dict(reg=0.05) if model == "bpr" else dict(margin=1.0, reg_cov=1.0, clip_norm=1.0)
+    e = Engine(model, u1 - u0, 1682, U0.shape[1], n_neg=W, dense_item_apply=True,
+               seed=10 + rank, **kw)
+    e.set_interactions(lip, lix)
+    e.set_table("user", U0[u0:u1])
+    e.set_table("item", V0)
+    step, grad = make_gpu_sharded(e, 1682, U0.shape[1], False, torch.device("cuda", 0))
+    for pairs, negs in batches:
+        mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
+        lp = pairs[mine].copy()
+        lp[:, 0] -= u0
+        step(pairs=lp, negs=negs[mine])
+    torch.cuda.synchronize()
+    q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("acc_item")))
+    e.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
+def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream):
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(8)
+    d = 24
+    U0 = O.init_table(rng, (943, d), truncated=(model != "cml"))
+    V0 = O.init_table(rng, (1682, d), truncated=(model != "cml"))
+    batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s]) for s in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    U, V = U0.astype(np.float64), V0.astype(np.float64)
+    AU, AV = np.full_like(U, 0.1), np.full_like(V, 0.1)
+    for pairs, negs in batches:
+        if model == "bpr":
+            O.bpr_step(U, V, AU, AV, pairs, negs, 0.05)
+        else:
+            O.cml_step(U, V, AU, AV, pairs, negs, 1.0, 1.0, 1.0)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    for rank, u0, u1, Ul, Vr, AVr in res:
+        assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
+        assert rel(Vr, V) <= 1e-5 and rel(AVr, AV) <= 1e-5
+    assert np.array_equal(res[0][4], res[1][4])   # replicas bit-identical

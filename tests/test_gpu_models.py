@@ -147,3 +147,25 @@ def test_cfg2_full_size_step_parity():
         err = np.abs(got - ref).max() / np.abs(ref).max()
         assert err <= 1e-5, (name, err)
     e.close()
+
+
+def test_driver_worker_end_to_end(fold1, tmp_path):
+    """The testbprmf-structured driver: text folds -> loadSparseR ->
+    matBinarize -> device Sampler -> BPRMF.train -> scores (testbprmf.py:32-52)."""
+    from collaborativefilteringusingtensorflow_amd.drivers import testbprmf
+    for tag in ("train", "test"):
+        ip, ix = fold1[tag + "_indptr"], fold1[tag + "_indices"]
+        name = "ratings__1_%s.txt" % ("tra" if tag == "train" else "tst")
+        with open(tmp_path / name, "w") as f:
+            for u in range(943):
+                for it in ix[ip[u]:ip[u + 1]]:
+                    f.write("%d\t%d\t4.0\n" % (u, it))
+            f.write("0\t0\t2.0\n")            # below the threshold: dropped by matBinarize
+    testbprmf.max_iter = None
+    old = testbprmf.n_factors
+    testbprmf.n_factors = 32
+    try:
+        scores = testbprmf.worker(0, 943, 1682, str(tmp_path) + "/")
+    finally:
+        testbprmf.n_factors = old
+    assert len(scores) == 5 and scores[4] > 0.2   # ndcg@10 after 50 epochs
