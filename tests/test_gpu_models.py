@@ -161,7 +161,6 @@ def test_driver_worker_end_to_end(fold1, tmp_path):
                 for it in ix[ip[u]:ip[u + 1]]:
                     f.write("%d\t%d\t4.0\n" % (u, it))
             f.write("0\t0\t2.0\n")            # below the threshold: dropped by matBinarize
-    testbprmf.max_iter = None
     old = testbprmf.n_factors
     testbprmf.n_factors = 32
     try:
