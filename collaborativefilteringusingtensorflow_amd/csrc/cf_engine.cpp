@@ -314,7 +314,7 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
     p.clip = c.model == CF_CML ? 1 : 0;
     p.n_users = c.n_users;
     p.n_items = c.n_items;
-    p.blocksU = (int)((c.n_users + kApplyRowsPerBlock - 1) / kApplyRowsPerBlock);
+    p.blocksU = (int)((c.n_users + kApplyRowsPerBlockU - 1) / kApplyRowsPerBlockU);
     p.cntU = e->cntU_[k];
     p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;

@@ -90,7 +90,10 @@ struct ApplyArgs {
     double* __restrict__ loss_acc;
 };
 
-constexpr int kApplyRowsPerBlock = kBlock * 4;   // one int4 of counts per thread
+// duplicated-row scan: users are sparse (one int4 of counts per thread), items
+// are dense in duplicates (one count per thread keeps each group's row list short)
+constexpr int kApplyRowsPerBlockU = kBlock * 4;
+constexpr int kApplyRowsPerBlockV = kBlock;
 
 struct DenseArgs {
     int d;

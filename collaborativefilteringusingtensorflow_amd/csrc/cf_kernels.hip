@@ -513,17 +513,19 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
     float* G = isU ? a.GU : a.GV;
     const bool bias = !isU && a.b != nullptr;
 
-    const int64_t r0 = blk * kApplyRowsPerBlock + (int64_t)threadIdx.x * 4;
-    int c4[4];
-    if (r0 + 3 < n) {
+    const int rpt = isU ? 4 : 1;                   // rows per thread
+    const int64_t base_row = blk * (isU ? kApplyRowsPerBlockU : kApplyRowsPerBlockV);
+    const int64_t r0 = base_row + (int64_t)threadIdx.x * rpt;
+    int c4[4] = {0, 0, 0, 0};
+    if (rpt == 4 && r0 + 3 < n) {
         const int4 v = *reinterpret_cast<const int4*>(cnt + r0);
         c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
     } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) c4[q] = (r0 + q < n) ? cnt[r0 + q] : 0;
+        for (int q = 0; q < rpt; ++q) c4[q] = (r0 + q < n) ? cnt[r0 + q] : 0;
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+        if (q >= rpt) break;  // block-uniform
         const bool win = c4[q] > 1;
         const int64_t r_l = r0 + q;
         if (bias && win) {
@@ -540,8 +542,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
             unsigned long long mm = m;
             for (int t = 0; t < my && mm; ++t) mm &= mm - 1ull;
             const int pos = (my < nwin) ? __ffsll((long long)mm) - 1 : 0;
-            const int64_t r = blk * kApplyRowsPerBlock +
-                              __shfl((int)threadIdx.x * 4 + q, pos, 64);  // row of lane pos
+            const int64_t r = base_row + __shfl((int)threadIdx.x * rpt + q, pos, 64);
             if (my < nwin) {  // group-uniform
                 float g[EPL], x[EPL];
                 gload<EPL>(G, r, a.d, gl, g);
@@ -708,7 +709,7 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
-    const int bV = a.apply_items ? (int)((a.n_items + kApplyRowsPerBlock - 1) / kApplyRowsPerBlock) : 0;
+    const int bV = a.apply_items ? (int)((a.n_items + kApplyRowsPerBlockV - 1) / kApplyRowsPerBlockV) : 0;
     int blocks = a.blocksU + bV;
     if (blocks == 0) blocks = 1;  // block 0 still reduces the loss
     const dim3 grid(blocks), block(kBlock);
