@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step (0 = config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--score-pass", action="store_true",
+                    help="also time one full scoring + top-10 pass over this rank's users")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -235,6 +237,23 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
     }
+    if args.score_pass or args.config == "cfg5":
+        users = np.arange(u1 - u0, dtype=np.int32)
+        eng.score_topk(users[:1024], 10)          # warm-up
+        sync()
+        t0 = time.perf_counter()
+        eng.score_topk(users, 10, exclude_train=True)
+        sync()
+        ts = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([ts], dtype=torch.float64, device="cuda:%d" % local_rank)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ts = float(t.item())
+        flop = 2.0 * nu_all * ni * d
+        out["score_pass"] = {"users": nu_all, "items": ni, "d": d, "k": 10, "seconds": ts,
+                             "TFLOPs": flop / ts / 1e12,
+                             "frac_fp32_mfma_peak": flop / ts / 1e12 / (157.3 * world),
+                             "kernel": "fused_topk_kernel (v_mfma_f32_32x32x2_f32 + streaming top-k)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, indptr, indices)

@@ -84,6 +84,7 @@ SIGNATURES = {
     "cf_step_items": (ctypes.c_int, [_P]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
     "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
+    "cf_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, _I64]),
     "cf_profile_enable": (ctypes.c_int, [_P, _I32]),
     "cf_profile_read": (ctypes.c_int, [_P, _I32, _PD, _PI64]),
     "cf_profile_reset": (ctypes.c_int, [_P]),

@@ -107,6 +107,8 @@ struct cf_engine {
     uint32_t* keys = nullptr;
     size_t keys_cap = 0;
 
+    int topk_path = 0;  // cf_set_option("topk_path")
+
     // profiling
     bool prof = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CF_K_COUNT];
@@ -390,6 +392,51 @@ float* table_ptr(cf_engine* e, int t, int64_t* n) {
         case CF_TABLE_ACC_BIAS: *n = c.n_items; return e->Ab;
         default: *n = 0; return nullptr;
     }
+}
+
+
+// fused fp32-MFMA scoring + streaming top-k: no score matrix in HBM
+int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclude_train,
+                     int32_t* idx_out, float* val_out) {
+    const cf_config& c = e->cfg;
+    int32_t* d_users = nullptr;
+    int32_t* d_idx = nullptr;
+    float* d_val = nullptr;
+    int r = CF_OK;
+    if ((r = dalloc(&d_users, (size_t)n)) || (r = dalloc(&d_idx, (size_t)n * k)) ||
+        (val_out && (r = dalloc(&d_val, (size_t)n * k)))) {
+        dfree(d_users); dfree(d_idx); dfree(d_val);
+        return r;
+    }
+    FusedTopkArgs f{};
+    f.model = c.model;
+    f.d = c.n_factors;
+    f.Dp = (c.n_factors + 7) & ~7;
+    f.Dh = f.Dp / 2;
+    f.n_users = n;
+    f.n_items = c.n_items;
+    f.k = k;
+    f.users = d_users;
+    f.U = e->U;
+    f.V = e->V;
+    f.b = e->b;
+    f.exclude_train = exclude_train ? 1 : 0;
+    f.indptr = e->indptr;
+    f.indices = e->indices;
+    f.idx_out = d_idx;
+    f.val_out = d_val;
+    hipError_t he = hipMemcpyAsync(d_users, users, (size_t)n * 4, hipMemcpyHostToDevice, e->stream);
+    if (he == hipSuccess) {
+        ProfScope ps(e, CF_K_TOPK);
+        he = launch_fused_topk(f, e->stream);
+    }
+    if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    if (he == hipSuccess && val_out)
+        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    dfree(d_users); dfree(d_idx); dfree(d_val);
+    if (he != hipSuccess) return fail(CF_EHIP, std::string("cf_score_topk (fused): ") + hipGetErrorString(he));
+    return CF_OK;
 }
 
 }  // namespace
@@ -790,6 +837,12 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     if (n == 0) return CF_OK;
     for (int r = 0; r < n; ++r)
         if (users[r] < 0 || users[r] >= c.n_users) return fail(CF_EINVAL, "user id out of range");
+    CF_HIP(hipStreamSynchronize(e->side));
+    const bool fused_ok = k <= kFusedMaxK && c.n_factors <= kFusedMaxD;
+    if (e->topk_path == 2 && !fused_ok)
+        return fail(CF_EINVAL, "fused top-k needs k <= 32 and n_factors <= 128");
+    if (fused_ok && e->topk_path != 1)
+        return score_topk_fused(e, users, n, k, exclude_train, idx_out, val_out);
     const size_t row_bytes = (size_t)c.n_items * 4;
     const size_t budget = (size_t)512 << 20;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / row_bytes));
@@ -846,6 +899,17 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     dfree(d_users); dfree(d_idx); dfree(d_val);
     if (he != hipSuccess) return fail(CF_EHIP, std::string("cf_score_topk: ") + hipGetErrorString(he));
     return CF_OK;
+}
+
+int cf_set_option(cf_engine* e, const char* name, int64_t value) {
+    if (!e || !name) return fail(CF_EINVAL, "null argument");
+    const std::string n(name);
+    if (n == "topk_path") {
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
+        e->topk_path = (int)value;
+        return CF_OK;
+    }
+    return fail(CF_EINVAL, "unknown option " + n);
 }
 
 int cf_profile_enable(cf_engine* e, int32_t on) {

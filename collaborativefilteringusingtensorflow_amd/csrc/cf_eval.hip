@@ -216,6 +216,220 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(TopkArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused scoring GEMM + streaming top-k (no score matrix in HBM).
+//
+// One block = 64 users; it sweeps all items in steps of 64.  Per step the
+// four waves compute a 2 x 2 arrangement of 32 x 32 score tiles with
+// v_mfma_f32_32x32x2_f32 (exact f32, a k-ordered fmaf chain): lane l feeds
+// A = U[row l&31][k] and B = V[k][col l&31] where lane half h = l>>5 walks
+// the k-half [h*Dh, (h+1)*Dh) -- so each lane streams contiguous k and reads
+// its operands four MFMAs at a time with ds_read_b128 from LDS tiles whose
+// row stride (Dp+4 floats == 4*odd mod 64 banks) is conflict-free.
+// The train items of each user are excluded with a 64-bit mask per user and
+// step, built by advancing a cursor through the user's sorted CSR row as the
+// sweep moves (items are visited in increasing order).  Every surviving
+// score becomes a 64-bit key (order-preserving score bits, then ~item id: ties
+// go to the lower id, as TopKV2); keys above the user's running threshold
+// are appended to its LDS candidate list, which a wave bitonic-sorts down to
+// k entries (and raises the threshold) whenever fewer than 64 slots remain.
+// ---------------------------------------------------------------------------
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int kFS = kFusedMaxD + 4;   // LDS row stride upper bound (floats)
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+    const int lo = __shfl_xor((int)(v & 0xFFFFFFFFull), m, 64);
+    const int hi = __shfl_xor((int)(v >> 32), m, 64);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int src) {
+    const int lo = __shfl((int)(v & 0xFFFFFFFFull), src, 64);
+    const int hi = __shfl((int)(v >> 32), src, 64);
+    return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// one wave sorts a user's <=128 candidates descending, keeps the best `keep`
+// (<= 64) in place and returns how many it kept
+__device__ int wave_compact(unsigned long long* __restrict__ buf, int* cnt,
+                            unsigned long long* thr, int keep, int k) {
+    const int lane = lane_id();
+    const int n = *cnt;
+    unsigned long long x0 = lane < n ? buf[lane] : 0ull;
+    unsigned long long x1 = lane + 64 < n ? buf[lane + 64] : 0ull;
+    for (int size = 2; size <= 128; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride == 64) {  // partner is the lane's other register; size == 128
+                if (x0 < x1) { const unsigned long long t = x0; x0 = x1; x1 = t; }
+                continue;
+            }
+            const bool lower = (lane & stride) == 0;
+            {
+                const unsigned long long y = shfl_xor_u64(x0, stride);
+                const bool desc = (lane & size) == 0;
+                const unsigned long long mx = x0 > y ? x0 : y, mn = x0 > y ? y : x0;
+                x0 = (desc == lower) ? mx : mn;
+            }
+            {
+                const unsigned long long y = shfl_xor_u64(x1, stride);
+                const bool desc = ((lane + 64) & size) == 0;
+                const unsigned long long mx = x1 > y ? x1 : y, mn = x1 > y ? y : x1;
+                x1 = (desc == lower) ? mx : mn;
+            }
+        }
+    }
+    const int m = n < keep ? n : keep;
+    if (lane < m) buf[lane] = x0;            // keep <= 64
+    const unsigned long long kth = shfl_u64(x0, k - 1);
+    if (lane == 0) {
+        *cnt = m;
+        if (m >= k) *thr = kth;
+    }
+    return m;
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
+    __shared__ __attribute__((aligned(16))) float Us[kFusedUsers * kFS];
+    __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFS];
+    __shared__ unsigned long long buf[kFusedUsers * kFusedCap];
+    __shared__ unsigned long long thr[kFusedUsers];
+    __shared__ unsigned long long mask[kFusedUsers];
+    __shared__ int cnt[kFusedUsers];
+    __shared__ float unorm[kFusedUsers];
+    __shared__ float bt[kFusedItems];
+
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;     // 32-row user block, 32-col item block
+    const int h = lane >> 5, c = lane & 31;
+    const int d = a.d, Dp = a.Dp, Dh = a.Dh, S = a.Dp + 4;
+    const int u0 = blockIdx.x * kFusedUsers;
+    const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
+
+    for (int t = tid; t < kFusedUsers * Dp; t += kBlock) {
+        const int r = t / Dp, kk = t - r * Dp;
+        Us[r * S + kk] = (r < nu && kk < d) ? a.U[(int64_t)a.users[u0 + r] * d + kk] : 0.f;
+    }
+    int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
+    if (tid < kFusedUsers) {
+        thr[tid] = 0ull;
+        cnt[tid] = 0;
+        if (a.exclude_train && tid < nu) {
+            const int u = a.users[u0 + tid];
+            cur = a.indptr[u];
+            end = a.indptr[u + 1];
+        }
+    }
+    __syncthreads();
+    if (MODEL == CML && tid < kFusedUsers) {
+        float sqn = 0.f;
+        for (int kk = 0; kk < d; ++kk) sqn = fmaf(Us[tid * S + kk], Us[tid * S + kk], sqn);
+        unorm[tid] = sqn;
+    }
+
+    for (int64_t j0 = 0; j0 < a.n_items; j0 += kFusedItems) {
+        // ---- stage the item tile, its bias, the train mask ---------------------
+        if ((d & 3) == 0) {   // 16-B loads; rows are 16-B aligned when d % 4 == 0
+            const int q4 = Dp >> 2;
+            for (int t = tid; t < kFusedItems * q4; t += kBlock) {
+                const int r = t / q4, kk = (t - r * q4) * 4;
+                const int64_t j = j0 + r;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (j < a.n_items && kk < d) v = *reinterpret_cast<const float4*>(a.V + j * d + kk);
+                *reinterpret_cast<float4*>(Vs + r * S + kk) = v;
+            }
+        } else {
+            for (int t = tid; t < kFusedItems * Dp; t += kBlock) {
+                const int r = t / Dp, kk = t - r * Dp;
+                const int64_t j = j0 + r;
+                Vs[r * S + kk] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
+            }
+        }
+        if (MODEL == GBPR && tid < kFusedItems)
+            bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
+        if (tid < kFusedUsers) {
+            unsigned long long m = 0ull;
+            while (cur < end && (int64_t)a.indices[cur] < j0 + kFusedItems) {
+                m |= 1ull << (int)((int64_t)a.indices[cur] - j0);
+                ++cur;
+            }
+            mask[tid] = m;
+        }
+        __syncthreads();
+        // ---- 32 x 32 tile per wave on the matrix cores --------------------------
+        floatx16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        float vsq = 0.f;
+        const float* ap = Us + (wr * 32 + c) * S + h * Dh;
+        const float* bp = Vs + (wc * 32 + c) * S + h * Dh;
+        for (int t0 = 0; t0 < Dh; t0 += 4) {
+            const float4 a4 = *reinterpret_cast<const float4*>(ap + t0);
+            const float4 b4 = *reinterpret_cast<const float4*>(bp + t0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc, 0, 0, 0);
+            if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+        }
+        float vnorm = 0.f;
+        if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
+        // ---- candidates above each user's threshold -------------------------------
+        const int jl = wc * 32 + c;
+        const int64_t J = j0 + jl;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            if (R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
+                float s = acc[q];
+                if (MODEL == GBPR) s += bt[jl];
+                if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];   // -|u - v|^2
+                const unsigned long long key = ((unsigned long long)float_key(s) << 32) |
+                                               (0xFFFFFFFFull - (unsigned long long)J);
+                if (key > thr[R]) {
+                    const int pos = atomicAdd(&cnt[R], 1);
+                    buf[R * kFusedCap + pos] = key;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- shrink lists that could overflow at the next step ---------------------
+        for (int R = wv; R < nu; R += kWavesPerBlock)
+            if (cnt[R] > kFusedCap - kFusedItems)
+                wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        __syncthreads();
+    }
+    // ---- final sort and output -------------------------------------------------------
+    for (int R = wv; R < nu; R += kWavesPerBlock) {
+        const int n = wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        const int64_t orow = (int64_t)(u0 + R) * a.k;
+        if (lane < a.k) {
+            int id = -1;
+            float v = __int_as_float(0x7fc00000);
+            if (lane < n) {
+                const unsigned long long e = buf[R * kFusedCap + lane];
+                id = (int)(0xFFFFFFFFull - (e & 0xFFFFFFFFull));
+                v = key_float((uint32_t)(e >> 32));
+            }
+            a.idx_out[orow + lane] = id;
+            if (a.val_out) a.val_out[orow + lane] = v;
+        }
+    }
+}
+
+hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
+    if (a.n_users <= 0) return hipSuccess;
+    const dim3 grid((a.n_users + kFusedUsers - 1) / kFusedUsers), block(kBlock);
+    switch (a.model) {
+        case GBPR: hipLaunchKernelGGL(fused_topk_kernel<GBPR>, grid, block, 0, s, a); break;
+        case CML: hipLaunchKernelGGL(fused_topk_kernel<CML>, grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL(fused_topk_kernel<BPR>, grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s) {
     if (a.n_users <= 0) return hipSuccess;
     dim3 grid((unsigned)((a.n_items + kTile - 1) / kTile), (unsigned)((a.n_users + kTile - 1) / kTile));

@@ -120,6 +120,30 @@ struct ScoreArgs {
     const int32_t* __restrict__ indices;
 };
 
+// fused scoring GEMM (fp32 MFMA) + streaming per-user top-k, d <= 128, k <= 32
+constexpr int kFusedUsers = 64;
+constexpr int kFusedItems = 64;
+constexpr int kFusedMaxD = 128;
+constexpr int kFusedMaxK = 32;
+constexpr int kFusedCap = 128;   // candidate slots per user
+
+struct FusedTopkArgs {
+    int model;
+    int d, Dp, Dh;            // Dp = d rounded up to 8, Dh = Dp / 2
+    int n_users;              // users in this launch
+    int64_t n_items;
+    int k;
+    const int32_t* __restrict__ users;
+    const float* __restrict__ U;
+    const float* __restrict__ V;
+    const float* __restrict__ b;         // GBPR bias (nullable)
+    int exclude_train;
+    const int64_t* __restrict__ indptr;
+    const int32_t* __restrict__ indices;
+    int32_t* __restrict__ idx_out;       // [n_users, k]
+    float* __restrict__ val_out;         // [n_users, k] (nullable)
+};
+
 struct TopkArgs {
     int k;
     int64_t n_items;
@@ -142,6 +166,7 @@ hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int
                               int2* pairs, hipStream_t s);
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);
 hipError_t launch_topk(const TopkArgs& a, int n_users, hipStream_t s);
+hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s);
 
 // host-side mirror of the device bijection (for key generation)
 PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch);

@@ -198,6 +198,9 @@ class Engine(object):
                 "cf_score_topk")
         return (idx, val) if return_values else idx
 
+    def set_option(self, name, value):
+        N.check(self._L.cf_set_option(self._h, name.encode(), int(value)), "cf_set_option(%s)" % name)
+
     # ---- measurement -------------------------------------------------------------
     def profile(self, on=True):
         N.check(self._L.cf_profile_enable(self._h, 1 if on else 0), "cf_profile_enable")

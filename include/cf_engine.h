@@ -226,6 +226,14 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
                   int32_t k, int32_t exclude_train, int32_t* host_idx_out,
                   float* host_val_out);
 
+/*
+ * Engine options (name, value):
+ *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 32 and d <= 128, else
+ *                materialised scores + radix select), 1 = materialised,
+ *                2 = fused (CF_EINVAL when k/d exceed its limits)
+ */
+int cf_set_option(cf_engine* eng, const char* name, int64_t value);
+
 /* ---- measurement ----------------------------------------------------------- */
 /* HIP-event timing of every launch of each cf_kernel_id on the engine stream. */
 int cf_profile_enable(cf_engine* eng, int32_t on);

@@ -40,12 +40,15 @@ def check_lists(gpu_idx, scores, oracle_lists, atol):
                 assert abs(s[a] - s[b]) <= atol, (r, a, b, s[a], s[b])
 
 
-@pytest.mark.parametrize("model,d", [("bpr", 32), ("gbpr", 20), ("cml", 50), ("amf", 100)])
-def test_topk_matches_oracle(fold1, model, d):
+@pytest.mark.parametrize("path", [0, 1])          # auto (fused MFMA for k <= 32), materialised
+@pytest.mark.parametrize("model,d", [("bpr", 32), ("gbpr", 20), ("cml", 50), ("amf", 100),
+                                     ("bpr", 128), ("cml", 7)])
+def test_topk_matches_oracle(fold1, model, d, path):
     e, U, V, b = setup(model, fold1, d, 21, bias=(model == "gbpr"), truncated=(model != "cml"))
+    e.set_option("topk_path", path)
     tst_ip = fold1["test_indptr"]
     users = np.nonzero(np.diff(tst_ip))[0].astype(np.int32)
-    for k in (10, 100):
+    for k in (1, 10, 32, 100):
         idx = e.score_topk(users, k, exclude_train=True)
         S = O.predict(model, U.astype(np.float64), V.astype(np.float64),
                       None if b is None else b.astype(np.float64), users)
@@ -68,7 +71,8 @@ def test_recommend_equals_literal_overfetch(fold1):
     e.close()
 
 
-def test_ties_go_to_lower_id(fold1):
+@pytest.mark.parametrize("path", [1, 2])
+def test_ties_go_to_lower_id(fold1, path):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
     e = Engine("bpr", nu, ni, 4, seed=1)
@@ -78,16 +82,22 @@ def test_ties_go_to_lower_id(fold1):
     V[::3] = 1.0   # every third item ties at score 4, the rest tie at 0
     e.set_table("user", U)
     e.set_table("item", V)
-    idx, val = e.score_topk(np.array([5], np.int32), 50, exclude_train=False, return_values=True)
-    assert list(idx[0]) == list(range(0, 150, 3))
+    e.set_option("topk_path", path)
+    idx, val = e.score_topk(np.array([5], np.int32), 30, exclude_train=False, return_values=True)
+    assert list(idx[0]) == list(range(0, 90, 3))
     assert np.all(val[0] == 4.0)
-    idx = e.score_topk(np.array([5], np.int32), 600, exclude_train=False)
-    assert list(idx[0][:561]) == list(range(0, ni, 3))
-    assert list(idx[0][561:600]) == [x for x in range(ni) if x % 3][:39]
+    if path == 1:
+        idx = e.score_topk(np.array([5], np.int32), 600, exclude_train=False)
+        assert list(idx[0][:561]) == list(range(0, ni, 3))
+        assert list(idx[0][561:600]) == [x for x in range(ni) if x % 3][:39]
+    # many users at once (several fused blocks), all tied
+    idx = e.score_topk(np.arange(0, 943, 3, dtype=np.int32), 20, exclude_train=False)
+    assert all(list(r) == list(range(0, 60, 3)) for r in idx)
     e.close()
 
 
-def test_exclusion_and_padding(fold1):
+@pytest.mark.parametrize("path", [1, 2])
+def test_exclusion_and_padding(fold1, path):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     # tiny graph: user 0 owns items 0..7 of 10 -> only 2 items remain
     ip = np.array([0, 8, 9], np.int64)
@@ -97,6 +107,7 @@ def test_exclusion_and_padding(fold1):
     rng = np.random.RandomState(0)
     e.set_table("user", rng.randn(2, 4).astype(np.float32))
     e.set_table("item", rng.randn(10, 4).astype(np.float32))
+    e.set_option("topk_path", path)
     idx = e.score_topk(np.array([0, 1], np.int32), 5)
     assert sorted(int(x) for x in idx[0][:2]) == [8, 9]
     assert list(idx[0][2:]) == [-1, -1, -1]
