@@ -13,14 +13,18 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
-OUT = os.path.join(PKG, "build")
+# CF_BUILD_VARIANT=<name> + CF_EXTRA_FLAGS="-D..." build an experimental
+# variant into build/variants/<name>/ (load it with CF_ENGINE_LIB=<path>)
+VARIANT = os.environ.get("CF_BUILD_VARIANT", "")
+OUT = os.path.join(PKG, "build", "variants", VARIANT) if VARIANT else os.path.join(PKG, "build")
 LIB = os.path.join(OUT, "libcf_engine.so")
 SOURCES = ["cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp"]
 HEADERS = ["cf_kernels.h", "cf_device.h", os.path.join(ROOT, "include", "cf_engine.h")]
 ARCH = os.environ.get("CF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
-         "-Wall", "-Wno-unused-function", "-I" + os.path.join(ROOT, "include")]
+         "-Wall", "-Wno-unused-function", "-Wno-pass-failed", "-I" + os.path.join(ROOT, "include")]
+FLAGS += os.environ.get("CF_EXTRA_FLAGS", "").split()
 
 
 def _newer(target, deps):

@@ -12,7 +12,10 @@ constexpr int kBlock = 256;        // 4 waves per workgroup
 constexpr int kWavesPerBlock = kBlock / kWave;
 constexpr int kGL = 16;            // lanes per pair / per row ("group")
 constexpr int kGroupsPerBlock = kBlock / kGL;   // 16
-constexpr int kPairsPerGroup = 2;  // pairs one group carries through the grad kernel
+#ifndef CF_PAIRS_PER_GROUP
+#define CF_PAIRS_PER_GROUP 2
+#endif
+constexpr int kPairsPerGroup = CF_PAIRS_PER_GROUP;  // pairs one group carries through grad
 constexpr int kPairsPerBlock = kGroupsPerBlock * kPairsPerGroup;  // 32
 constexpr int kMaxNeg = 64;
 constexpr int kMaxGroup = 16;
