@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--score-pass", action="store_true",
                     help="also time one full scoring + top-10 pass over this rank's users")
+    ap.add_argument("--grad-path", type=int, default=0,
+                    help="cf_set_option grad_path: 0 auto (phased kernel), 1 generic kernel")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -160,6 +162,7 @@ def main():
             kw[k] = cfg[k]
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
                  dense_item_apply=(world > 1), seed=1000 + rank, **kw)
+    eng.set_option("grad_path", args.grad_path)
     eng.set_interactions(indptr, indices)
     eng.init_params(0.0, 0.1, truncated=cfg["truncated"], seed=1)  # same V on every rank
     if cfg["model"] == "amf":

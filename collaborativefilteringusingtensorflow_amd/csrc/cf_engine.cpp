@@ -108,6 +108,7 @@ struct cf_engine {
     size_t keys_cap = 0;
 
     int topk_path = 0;  // cf_set_option("topk_path")
+    int grad_path = 0;  // cf_set_option("grad_path")
 
     // profiling
     bool prof = false;
@@ -168,7 +169,7 @@ int ensure_batch(cf_engine* e, int B) {
         CF_TRY(dalloc(&e->occU_[k], nU));
         CF_TRY(dalloc(&e->occV_[k], nV));
     }
-    CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks(B)));
+    CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks_max(B)));
     e->Bcap = B;
     return CF_OK;
 }
@@ -182,6 +183,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.G = group_count(c);
     a.B = B;
     a.adversarial = (c.model == CF_AMF && e->phase == 1) ? 1 : 0;
+    a.grad_path = e->grad_path;
     a.reg = c.reg;
     a.rho = c.rho;
     a.margin = c.margin;
@@ -324,7 +326,7 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
     p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
     p.apply_items = c.dense_item_apply ? 0 : 1;
     p.loss_partial = e->loss_partial;
-    p.n_partial = grad_blocks(B);
+    p.n_partial = grad_blocks(a);
     p.loss_acc = loss_acc;
     {
         ProfScope ps(e, CF_K_APPLY);
@@ -907,6 +909,11 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
         e->topk_path = (int)value;
+        return CF_OK;
+    }
+    if (n == "grad_path") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "grad_path must be 0 or 1");
+        e->grad_path = (int)value;
         return CF_OK;
     }
     return fail(CF_EINVAL, "unknown option " + n);

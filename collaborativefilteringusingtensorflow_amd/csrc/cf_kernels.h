@@ -42,6 +42,7 @@ struct StepArgs {
     int G;           // group users per pair (GBPR)
     int B;           // pairs in this step
     int adversarial; // AMF phase flag
+    int grad_path;   // 0 auto, 1 generic grad_kernel, 2 phased grad_fast_kernel when eligible
     float reg, rho, margin, reg_cov, reg_adv;
     int use_rank_weight;
     float n_items_f;
@@ -158,7 +159,9 @@ struct TopkArgs {
 // ---- host launchers (cf_kernels.hip / cf_eval.hip) -------------------------
 hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + count
 hipError_t launch_grad(const StepArgs& a, hipStream_t s);   // gather, loss, grads, apply
-int grad_blocks(int B);
+// blocks (= loss partials) of the grad launch for this step shape
+int grad_blocks(const StepArgs& a);
+int grad_blocks_max(int B);  // upper bound over every grad variant
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);

@@ -487,6 +487,307 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// grad, phased fast path (compile-time W, G <= 1, d <= 128).
+//
+// CDNA retires loads, stores and atomics through ONE in-order vmcnt counter:
+// a load issued after a float atomic cannot be waited for before the atomic
+// drains (~3k cycles under load).  So a group first issues EVERY load of its
+// P pairs -- indices, then rows and occurrence counts, then the Adagrad
+// accumulator rows of the rows that occur once -- and only then computes and
+// issues the updates / atomics.  Same arithmetic as grad_kernel.
+// ---------------------------------------------------------------------------
+template <int EPL>
+__device__ __forceinline__ void gload_acc(const float* __restrict__ A, int64_t r, int d, int gl,
+                                          bool want, float (&acc)[EPL]) {
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) acc[s] = 1.f;
+    if (want) {
+        const float* row = A + r * (int64_t)d;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            const int e = s * kGL + gl;
+            if (e < d) acc[s] = row[e];
+        }
+    }
+}
+
+// SparseApplyAdagrad with the accumulator row already in registers
+template <int EPL>
+__device__ __forceinline__ void gapply_pre(float* __restrict__ X, float* __restrict__ A, int64_t r,
+                                           int d, int gl, const float (&x0)[EPL],
+                                           const float (&acc0)[EPL], const float (&g)[EPL],
+                                           float lr, bool clip, float c) {
+    float acc[EPL], x[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        acc[s] = fmaf(g[s], g[s], acc0[s]);
+        x[s] = x0[s] - (lr * g[s]) / sqrtf(acc[s]);
+    }
+    if (clip) {
+        const float n = sqrtf(gdot<EPL>(x, x));
+        const float den = fmaxf(n, c);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
+    }
+    float* xr = X + r * (int64_t)d;
+    float* ar = A + r * (int64_t)d;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = s * kGL + gl;
+        if (e < d) {
+            xr[e] = x[s];
+            ar[e] = acc[s];
+        }
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __restrict__ A,
+                                            float* __restrict__ G, int32_t* __restrict__ cnt,
+                                            int64_t r, int count, int d, int gl,
+                                            const float (&x0)[EPL], const float (&acc0)[EPL],
+                                            const float (&g)[EPL], const StepArgs& a) {
+    if (count == 1) {
+        gapply_pre<EPL>(X, A, r, d, gl, x0, acc0, g, a.lr, a.clip != 0, a.clip_norm);
+        if (gl == 0) cnt[r] = 0;
+    } else {
+        gatomic<EPL>(G, r, d, gl, g);
+    }
+}
+
+template <int MODEL, int EPL, int WT>
+struct PairRows {
+    static constexpr int NG = (MODEL == GBPR) ? 1 : 0;
+    static constexpr int NGA = NG > 0 ? NG : 1;
+    int u, i, cu, ci;
+    int j[WT], cj[WT];
+    int g[NGA], cg[NGA];
+    float uu[EPL], vi[EPL], au[EPL], ai[EPL];
+    float vj[WT][EPL], aj[WT][EPL];
+    float ug[NGA][EPL], ag[NGA][EPL];
+    float bi, bj[WT];
+
+    __device__ __forceinline__ void load_idx(const StepArgs& a, int p) {
+        u = a.occU[p];
+        i = a.occV[p];
+#pragma unroll
+        for (int w = 0; w < WT; ++w) j[w] = a.occV[a.B + p * WT + w];
+#pragma unroll
+        for (int k = 0; k < NG; ++k) g[k] = a.occU[a.B + p + k];
+    }
+    __device__ __forceinline__ void load_rows(const StepArgs& a, int gl) {
+        cu = a.count_users ? a.cntU[u] : 0;
+        ci = a.count_items ? a.cntV[i] : 0;
+#pragma unroll
+        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+#pragma unroll
+        for (int k = 0; k < NG; ++k) cg[k] = a.count_users ? a.cntU[g[k]] : 0;
+        gload<EPL>(a.U, u, a.d, gl, uu);
+        gload<EPL>(a.V, i, a.d, gl, vi);
+#pragma unroll
+        for (int w = 0; w < WT; ++w) gload<EPL>(a.V, j[w], a.d, gl, vj[w]);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) gload<EPL>(a.U, g[k], a.d, gl, ug[k]);
+        if (MODEL == GBPR) {
+            bi = a.b[i];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) bj[w] = a.b[j[w]];
+        }
+    }
+    __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
+        gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
+        gload_acc<EPL>(a.AV, i, a.d, gl, ci == 1, ai);
+#pragma unroll
+        for (int w = 0; w < WT; ++w) gload_acc<EPL>(a.AV, j[w], a.d, gl, cj[w] == 1, aj[w]);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) gload_acc<EPL>(a.AU, g[k], a.d, gl, cg[k] == 1, ag[k]);
+    }
+
+    __device__ __forceinline__ void update(const StepArgs& a, int gl, float& loss_g, float& sq) {
+        const int d = a.d;
+        if (MODEL == BPR || MODEL == AMF) {
+            const float ui = gdot<EPL>(uu, vi);
+            float gu[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
+            float sc = 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                const float x = ui - gdot<EPL>(uu, vj[w]);
+                float c = -1.f / (1.f + expf(x));
+                if (MODEL == AMF) {
+                    loss_g += softplus(-x);
+                    if (a.adversarial) {
+                        const float xc = fmaxf(fminf(x, 1e8f), -80.f);
+                        loss_g += a.reg_adv * softplus(-xc);
+                        if (x >= -80.f && x <= 1e8f) c *= (1.f + a.reg_adv);
+                    }
+                } else {
+                    loss_g += neg_log_sigmoid(x);
+                }
+                sc += c;
+                float gj[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] = fmaf(c, vi[s] - vj[w][s], gu[s]);
+                    gj[s] = -c * uu[s] + a.reg * vj[w][s];
+                    sq = fmaf(vj[w][s], vj[w][s], sq);
+                }
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+            }
+            float gi[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] += a.reg * uu[s];
+                gi[s] = sc * uu[s] + a.reg * vi[s];
+                sq = fmaf(uu[s], uu[s], sq);
+                sq = fmaf(vi[s], vi[s], sq);
+            }
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+        } else if (MODEL == GBPR) {  // G == 1
+            const float ui_u = gdot<EPL>(uu, vi);
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) sq = fmaf(ug[0][s], ug[0][s], sq);
+            const float ui = a.rho * gdot<EPL>(ug[0], vi) + (1.f - a.rho) * ui_u + bi;
+            float gu[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
+            float sc = 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                const float x = ui - (gdot<EPL>(uu, vj[w]) + bj[w]);
+                const float c = -1.f / (1.f + expf(x));
+                loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj[w] * bj[w];
+                sc += c;
+                float gj[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] = fmaf(-c, vj[w][s], gu[s]);
+                    gj[s] = -c * uu[s];
+                }
+                if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w]);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+            }
+            const float rg = a.rho;  // rho / G with G == 1
+            float gi[EPL], gg[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] += (1.f - a.rho) * sc * vi[s] + a.reg * uu[s];
+                gi[s] = sc * (rg * ug[0][s] + (1.f - a.rho) * uu[s]) + a.reg * vi[s];
+                gg[s] = rg * sc * vi[s] + a.reg * ug[0][s];
+                sq = fmaf(uu[s], uu[s], sq);
+                sq = fmaf(vi[s], vi[s], sq);
+            }
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], d, gl, ug[0], ag[0], gg, a);
+            if (gl == 0) bias_finish(a, i, ci, sc);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+        } else {  // CML
+            float du[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) du[s] = uu[s] - vi[s];
+            const float dp = gdot<EPL>(du, du);
+            float dn[WT];
+            float m = INFINITY;
+            int imp = 0;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                float t[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) t[s] = uu[s] - vj[w][s];
+                dn[w] = gdot<EPL>(t, t);
+                m = fminf(m, dn[w]);
+                imp += (dp - dn[w] + a.margin > 0.f) ? 1 : 0;
+            }
+            float cnt = 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) cnt += (dn[w] == m) ? 1.f : 0.f;
+            const float z = dp - m + a.margin;
+            const float lw =
+                a.use_rank_weight ? logf((float)imp / (float)WT * a.n_items_f + 1.f) : 1.f;
+            loss_g += fmaxf(z, 0.f) * lw;
+            const float aa = (z > 0.f) ? lw : 0.f;
+            const bool l2 = a.reg_cov > 0.f;
+            float gu[EPL], gi[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] = 2.f * aa * du[s];
+                gi[s] = -2.f * aa * du[s];
+            }
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                const float share = (dn[w] == m) ? 1.f / cnt : 0.f;
+                const float coef = 2.f * aa * share;
+                float gj[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    const float dv = uu[s] - vj[w][s];
+                    gu[s] = fmaf(-coef, dv, gu[s]);
+                    gj[s] = coef * dv;
+                    if (l2) {
+                        gj[s] += a.reg_cov * vj[w][s];
+                        sq = fmaf(vj[w][s], vj[w][s], sq);
+                    }
+                }
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+            }
+            if (l2) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] += a.reg_cov * uu[s];
+                    gi[s] += a.reg_cov * vi[s];
+                    sq = fmaf(uu[s], uu[s], sq);
+                    sq = fmaf(vi[s], vi[s], sq);
+                }
+            }
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+        }
+    }
+};
+
+template <int MODEL, int EPL, int WT, int P>
+__global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a) {
+    __shared__ double s_loss[kGroupsPerBlock];
+    const int gl = threadIdx.x & (kGL - 1);
+    const int grp = threadIdx.x >> 4;
+    float loss_g = 0.f;
+    float sq = 0.f;
+    PairRows<MODEL, EPL, WT> pr[P];
+    int pp[P];
+    bool ok[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+        pp[k] = (blockIdx.x * P + k) * kGroupsPerBlock + grp;
+        ok[k] = pp[k] < a.B;
+    }
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        if (ok[k]) pr[k].load_idx(a, pp[k]);
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        if (ok[k]) pr[k].load_rows(a, gl);
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        if (ok[k]) pr[k].load_acc(a, gl);
+#pragma unroll
+    for (int k = 0; k < P; ++k)
+        if (ok[k]) pr[k].update(a, gl, loss_g, sq);
+
+    const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
+    const float sq_g = gsum(sq);
+    if (gl == 0) s_loss[grp] = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[k];
+        a.loss_partial[blockIdx.x] = t;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // apply the summed gradient of every duplicated row (count > 1)
 // ---------------------------------------------------------------------------
 template <int EPL>
@@ -663,7 +964,29 @@ static int epl_for(int d) {
     return e <= 1 ? 1 : e <= 2 ? 2 : e <= 4 ? 4 : e <= 8 ? 8 : 16;
 }
 
-int grad_blocks(int B) { return (B + kPairsPerBlock - 1) / kPairsPerBlock; }
+#ifndef CF_FAST_PAIRS_W1
+#define CF_FAST_PAIRS_W1 2
+#endif
+#ifndef CF_FAST_PAIRS_W5
+#define CF_FAST_PAIRS_W5 1
+#endif
+
+// which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
+// fast, 0 = generic
+static int fast_w(const StepArgs& a) {
+    const bool ok = a.grad_path != 1 && epl_for(a.d) <= 8 && (a.model != GBPR || a.G == 1);
+    return ok && (a.W == 1 || a.W == 5) ? a.W : 0;
+}
+
+int grad_blocks(const StepArgs& a) {
+    const int fw = fast_w(a);
+    const int B = a.B;
+    const int ppb = fw == 1 ? CF_FAST_PAIRS_W1 * kGroupsPerBlock
+                  : fw == 5 ? CF_FAST_PAIRS_W5 * kGroupsPerBlock : kPairsPerBlock;
+    return (B + ppb - 1) / ppb;
+}
+
+int grad_blocks_max(int B) { return (B + kGroupsPerBlock - 1) / kGroupsPerBlock; }
 
 hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
@@ -677,7 +1000,7 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
 
 template <int MODEL, int WT>
 static hipError_t launch_grad_w(const StepArgs& a, hipStream_t s) {
-    const dim3 grid(grad_blocks(a.B)), block(kBlock);
+    const dim3 grid((a.B + kPairsPerBlock - 1) / kPairsPerBlock), block(kBlock);
     switch (epl_for(a.d)) {
         case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT>), grid, block, 0, s, a); break;
         case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT>), grid, block, 0, s, a); break;
@@ -688,11 +1011,28 @@ static hipError_t launch_grad_w(const StepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// W = 1 (BPRMF driver) and W = 5 (AMF / CML / GBPR drivers) get the
-// fully-prefetched specialisation; other W and d = 256 use the generic path
+template <int MODEL, int WT, int P>
+static hipError_t launch_grad_fast(const StepArgs& a, hipStream_t s) {
+    // the grid must match grad_blocks(): P * kGroupsPerBlock pairs per block
+    const int blocks = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock);
+    const dim3 grid(blocks), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P>), grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+// W = 1 (BPRMF driver) and W = 5 (AMF / CML / GBPR drivers) with G <= 1 and
+// d <= 128 take the phased fast path; anything else the generic kernel
 template <int MODEL>
 static hipError_t launch_grad_m(const StepArgs& a, hipStream_t s) {
     const int e = epl_for(a.d);
+    const int fw = fast_w(a);
+    if (fw == 1) return launch_grad_fast<MODEL, 1, CF_FAST_PAIRS_W1>(a, s);
+    if (fw == 5) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_W5>(a, s);
     if (a.W == 1) return launch_grad_w<MODEL, 1>(a, s);
     if (a.W == 5 && e <= 8) return launch_grad_w<MODEL, 5>(a, s);
     return launch_grad_w<MODEL, 0>(a, s);

@@ -231,6 +231,9 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 32 and d <= 128, else
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
+ *   "grad_path"  0 = auto (phased gradient kernel for W in {1,5}, d <= 128,
+ *                GBPR group size 1; generic kernel otherwise), 1 = generic
+ *                kernel always.  Both give the same arithmetic.
  */
 int cf_set_option(cf_engine* eng, const char* name, int64_t value);
 

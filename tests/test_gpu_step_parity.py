@@ -16,6 +16,17 @@ pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
 
+_GRAD_PATH = [0]
+
+
+@pytest.fixture(autouse=True, params=[0, 1], ids=["phased", "generic"])
+def grad_path(request):
+    """Every step test runs on both gradient kernels (cf_set_option grad_path):
+    the phased W in {1,5} kernel and the generic one."""
+    _GRAD_PATH[0] = request.param
+    yield request.param
+    _GRAD_PATH[0] = 0
+
 
 def rel(a, b):
     a = np.asarray(a, dtype=np.float64)
@@ -27,6 +38,7 @@ def make_engine(model, fold1, d, W, G=1, dense=False, **kw):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=G,
                dense_item_apply=dense, seed=7, **kw)
+    e.set_option("grad_path", _GRAD_PATH[0])
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     return e
 
