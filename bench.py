@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_degrees, synth_graph  # noqa: E402,E501
 from collaborativefilteringusingtensorflow_amd.distributed import make_gpu_sharded, shard_users  # noqa: E402,E501
+from collaborativefilteringusingtensorflow_amd._native import KERNELS  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -124,6 +125,12 @@ def main():
                     help="also time one full scoring + top-10 pass over this rank's users")
     ap.add_argument("--grad-path", type=int, default=0,
                     help="cf_set_option grad_path: 0 auto (phased kernel), 1 generic kernel")
+    ap.add_argument("--prep-stream", type=int, default=0,
+                    help="cf_set_option prep_stream: 0 in-order (default), 1 side stream")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="cf_set_option pipeline: 1 apply(s)+draw(s+1) in one launch (default)")
+    ap.add_argument("--slot-max", type=int, default=0,
+                    help="cf_set_option slot_max (0 = engine default)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -163,6 +170,10 @@ def main():
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
                  dense_item_apply=(world > 1), seed=1000 + rank, **kw)
     eng.set_option("grad_path", args.grad_path)
+    eng.set_option("prep_stream", args.prep_stream)
+    eng.set_option("pipeline", args.pipeline)
+    if args.slot_max:
+        eng.set_option("slot_max", args.slot_max)
     eng.set_interactions(indptr, indices)
     eng.init_params(0.0, 0.1, truncated=cfg["truncated"], seed=1)  # same V on every rank
     if cfg["model"] == "amf":
@@ -188,7 +199,10 @@ def main():
 
     run(args.warmup)
     sync()
+    # timed region: HIP events around the dominant kernel only (an event pair
+    # around every launch would add ~20 us per step to the loop)
     eng.profile_reset()
+    eng.set_option("profile_mask", 1 << KERNELS["step"])
     eng.profile(not args.no_profile)
     sync()
     t0 = time.perf_counter()
@@ -200,18 +214,30 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local_rank)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    loss = eng.take_loss()
-    log("rank %d: loss accumulated %.4e over %d steps" % (rank, loss, args.warmup + args.steps))
+    step_ms, step_n = eng.profile_read("step")
 
+    # per-kernel breakdown: a separate, untimed pass with every launch timed
     kernels = {}
-    for kname in ("sample", "step", "apply", "apply_dense", "clip"):
-        ms, n = eng.profile_read(kname)
-        if n:
-            kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}
+    if not args.no_profile:
+        nb = min(args.steps, 50)
+        eng.profile_reset()
+        eng.set_option("profile_mask", 0xFFFFFFFF)
+        eng.profile(True)
+        run(nb)
+        sync()
+        eng.profile(False)
+        for kname in ("sample", "slot", "step", "apply", "apply_prep", "apply_dense", "clip"):
+            ms, n = eng.profile_read(kname)
+            if n:
+                kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}
+        kernels["note"] = "separate %d-step pass with every launch timed (not the timed region)" % nb
+    loss = eng.take_loss()
+    log("rank %d: loss accumulated %.4e" % (rank, loss))
+
     trip_per_step = B * W
     total_trip = trip_per_step * args.steps * world
     value = total_trip / elapsed
-    step_avg_s = kernels.get("step", {}).get("avg_us", float("nan")) * 1e-6
+    step_avg_s = (1e-3 * step_ms / step_n) if step_n else float("nan")
     gb = gather_bytes_per_pair(d, W, cfg["G"] if cfg["model"] == "gbpr" else 0,
                                bias=cfg["model"] == "gbpr") * B
     achieved = gb / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
@@ -222,7 +248,9 @@ def main():
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                 "traffic": traffic,
                 "bytes_per_launch": gb,
-                "bytes_def": "SURVEY 8(d) gather bytes: B*((2+W)*4d + 4(2+W))"}
+                "bytes_def": "SURVEY 8(d) gather bytes: B*((2+W)*4d + 4(2+W))",
+                "avg_launch_us": step_avg_s * 1e6 if step_n else None,
+                "timed_launches": step_n}
     full_b = full_step_bytes_per_pair(d, W) * B * args.steps * world
     out = {
         "metric": "BPR triplets/sec/GPU (d=64) + achieved HBM GB/s; NDCG@10 vs ref",

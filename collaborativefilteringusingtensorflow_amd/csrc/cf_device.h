@@ -61,6 +61,23 @@ __device__ __forceinline__ float wave_min(float v) {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// inclusive prefix sum over the 64 lanes of a wave
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
 // Order-preserving map float -> uint32 (larger float => larger key).  Key 0
 // is reserved for "excluded" (train items under exclude_train).
 __device__ __forceinline__ uint32_t float_key(float f) {

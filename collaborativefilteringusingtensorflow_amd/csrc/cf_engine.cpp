@@ -78,12 +78,26 @@ struct cf_engine {
     float *GV_own = nullptr, *Gb_own = nullptr;
     int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
     int32_t* cntV_[2] = {nullptr, nullptr};
+    // store-and-sum of duplicated rows (slot_kernel): slot base per row, the
+    // duplicate list (global row ids), [slots used, |dup|], and the slot
+    // kernel's per-block status words [2 steps][kSlotMaxBlocks]
+    int32_t *offU = nullptr, *offV = nullptr;
+    int32_t* dup = nullptr;
+    int32_t* ctl = nullptr;
+    uint64_t* status = nullptr;
+    int status_par = 0;
+    float* slotG = nullptr;   // [slot_cap, d]
+    size_t slot_cap = 0;
+    int slot_max = 32;        // cf_set_option("slot_max")
+    int pipeline = 1;         // cf_set_option("pipeline"): cf_train_steps fuses apply(s) + prep(s+1)
 
     // batch: two buffer sets, so that the sampler of step s+1 runs on the side
     // stream while step s's gradient and apply kernels run on the main stream
     int Bcap = 0;
     int32_t* occU_[2] = {nullptr, nullptr};
     int32_t* occV_[2] = {nullptr, nullptr};
+    int32_t* rankU_[2] = {nullptr, nullptr};  // occurrence rank inside its row
+    int32_t* rankV_[2] = {nullptr, nullptr};
     int set = 0;
     hipStream_t side = nullptr;
     hipEvent_t prep_done[2] = {nullptr, nullptr};
@@ -109,9 +123,11 @@ struct cf_engine {
 
     int topk_path = 0;  // cf_set_option("topk_path")
     int grad_path = 0;  // cf_set_option("grad_path")
+    int prep_side = 0;  // cf_set_option("prep_stream"): 1 = side stream (overlap), 0 = main
 
     // profiling
     bool prof = false;
+    uint32_t prof_mask = 0xFFFFFFFFu;  // cf_set_option("profile_mask"): kernel ids timed
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CF_K_COUNT];
     std::vector<hipEvent_t> ev_pool;
 };
@@ -139,7 +155,7 @@ struct ProfScope {
         return x;
     }
     ProfScope(cf_engine* e_, int k_, hipStream_t s_ = nullptr) : e(e_), k(k_), s(s_) {
-        if (!e->prof) return;
+        if (!e->prof || !((e->prof_mask >> k) & 1)) return;
         if (!s) s = e->stream;
         a = get(e);
         z = get(e);
@@ -166,9 +182,17 @@ int ensure_batch(cf_engine* e, int B) {
     for (int k = 0; k < 2; ++k) {
         dfree(e->occU_[k]);
         dfree(e->occV_[k]);
+        dfree(e->rankU_[k]);
+        dfree(e->rankV_[k]);
         CF_TRY(dalloc(&e->occU_[k], nU));
         CF_TRY(dalloc(&e->occV_[k], nV));
+        CF_TRY(dalloc(&e->rankU_[k], nU));
+        CF_TRY(dalloc(&e->rankV_[k], nV));
     }
+    // every occurrence of a duplicated row may need a slot row
+    dfree(e->slotG);
+    e->slot_cap = nU + nV;
+    CF_TRY(dalloc(&e->slotG, e->slot_cap * (size_t)e->cfg.n_factors));
     CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks_max(B)));
     e->Bcap = B;
     return CF_OK;
@@ -207,6 +231,12 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.occV = e->occV_[k];
     a.cntU = e->cntU_[k];
     a.cntV = e->cntV_[k];
+    a.rankU = e->rankU_[k];
+    a.rankV = e->rankV_[k];
+    a.offU = e->offU;
+    a.offV = e->offV;
+    a.slotG = e->slotG;
+    a.slot_max = e->slot_max;
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
     a.count_items = c.dense_item_apply ? 0 : 1;
@@ -239,7 +269,7 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
 }
 
 int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
-                     const int32_t* groups, int B, int k) {
+                     const int32_t* groups, int B, int k, hipStream_t st) {
     const cf_config& c = e->cfg;
     const int W = c.n_neg, G = group_count(c);
     if (!pairs || !negs) return fail(CF_EINVAL, "pairs and negs are required");
@@ -277,36 +307,54 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
             su[B + (size_t)p * G + k] = g;
         }
     }
-    CF_HIP(hipMemcpyAsync(e->occU_[k], su, nU * sizeof(int32_t), hipMemcpyHostToDevice, e->side));
-    CF_HIP(hipMemcpyAsync(e->occV_[k], sv, nV * sizeof(int32_t), hipMemcpyHostToDevice, e->side));
-    CF_HIP(hipEventRecord(e->stage_ev, e->side));
+    CF_HIP(hipMemcpyAsync(e->occU_[k], su, nU * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    CF_HIP(hipMemcpyAsync(e->occV_[k], sv, nV * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    CF_HIP(hipEventRecord(e->stage_ev, st));
     return CF_OK;
 }
 
-// One step: [side] sample/load + count into buffer set k; [main] gradient +
-// singleton apply, duplicate apply (+ CML clip).  The side stream runs one
-// step ahead: prep(s+1) overlaps grad/apply(s).  Loss added to *loss_acc.
-int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
-             const int32_t* groups, double* loss_acc) {
-    const cf_config& c = e->cfg;
-    CF_TRY(ensure_batch(e, B));
-    const int k = e->set;
-    e->set ^= 1;
-    StepArgs a = base_step_args(e, B, k);
-    // set k was last used by step s-2: its apply must be done before reuse
-    CF_HIP(hipStreamWaitEvent(e->side, e->apply_done[k], 0));
+// Stage / position the batch of one step in buffer set k and launch its draw
+// + count (prep) on stream ps.  Returns the step's arguments in *a.
+int begin_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
+               const int32_t* groups, int k, hipStream_t ps, StepArgs* a) {
+    *a = base_step_args(e, B, k);
     if (pairs) {
-        CF_TRY(stage_host_batch(e, pairs, negs, groups, B, k));
-        a.sample = 0;
+        CF_TRY(stage_host_batch(e, pairs, negs, groups, B, k, ps));
+        a->sample = 0;
     } else {
-        CF_TRY(sampler_args(e, B, &a));
+        CF_TRY(sampler_args(e, B, a));
     }
+    ProfScope pr(e, CF_K_SAMPLE, ps);
+    CF_HIP(launch_prep(*a, ps));
+    return CF_OK;
+}
+
+// The rest of a step on the engine stream: slots, gradient (+ singleton
+// Adagrad), duplicate apply (+ CML clip).  With `next`, the apply launch also
+// draws and counts the next step's batch (launch_apply_prep).  Loss added to
+// *loss_acc.
+int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
+                const StepArgs* next) {
+    const cf_config& c = e->cfg;
     {
-        ProfScope ps(e, CF_K_SAMPLE, e->side);
-        CF_HIP(launch_prep(a, e->side));
+        SlotArgs sa{};
+        sa.n_users = c.n_users;
+        sa.n_items = c.n_items;
+        sa.count_users = a.count_users;
+        sa.count_items = a.count_items;
+        sa.slot_max = e->slot_max;
+        sa.cntU = a.cntU;
+        sa.cntV = a.cntV;
+        sa.offU = e->offU;
+        sa.offV = e->offV;
+        sa.dup = e->dup;
+        sa.status = e->status + (size_t)kSlotMaxBlocks * e->status_par;
+        sa.status_next = e->status + (size_t)kSlotMaxBlocks * (e->status_par ^ 1);
+        sa.ctl = e->ctl;
+        e->status_par ^= 1;
+        ProfScope pr(e, CF_K_SLOT);
+        CF_HIP(launch_slots(sa, e->stream));
     }
-    CF_HIP(hipEventRecord(e->prep_done[k], e->side));
-    CF_HIP(hipStreamWaitEvent(e->stream, e->prep_done[k], 0));
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
@@ -316,23 +364,35 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
     p.clip = c.model == CF_CML ? 1 : 0;
+    p.slot_max = e->slot_max;
+    p.ctl = e->ctl;
+    p.dup = e->dup;
     p.n_users = c.n_users;
-    p.n_items = c.n_items;
-    p.blocksU = (int)((c.n_users + kApplyRowsPerBlockU - 1) / kApplyRowsPerBlockU);
+    p.offU = e->offU;
+    p.offV = e->offV;
+    p.slotG = e->slotG;
     p.cntU = e->cntU_[k];
     p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
     p.V = e->V; p.AV = e->AV; p.GV = e->GV;
     p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
-    p.apply_items = c.dense_item_apply ? 0 : 1;
+    {
+        const int64_t occU = (int64_t)B * users_per_pair(c), occV = (int64_t)B * items_per_pair(c);
+        const int64_t mu = std::min<int64_t>(c.n_users, occU / 2);
+        const int64_t mv = a.count_items ? std::min<int64_t>(c.n_items, occV / 2) : 0;
+        p.max_groups = (int)(mu + mv);
+    }
     p.loss_partial = e->loss_partial;
     p.n_partial = grad_blocks(a);
     p.loss_acc = loss_acc;
-    {
+    if (next) {
+        ProfScope ps(e, CF_K_APPLY_PREP);
+        CF_HIP(launch_apply_prep(p, *next, e->stream));
+    } else {
         ProfScope ps(e, CF_K_APPLY);
         CF_HIP(launch_apply(p, e->stream));
     }
-    CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
+    if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
     if (e->need_clip_U) {
         ProfScope ps(e, CF_K_CLIP);
         CF_HIP(launch_clip_full(e->U, c.n_users, c.n_factors, c.clip_norm, e->stream));
@@ -343,6 +403,50 @@ int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
         CF_HIP(launch_clip_full(e->V, c.n_items, c.n_factors, c.clip_norm, e->stream));
         e->need_clip_V = false;
     }
+    return CF_OK;
+}
+
+// One step, host-fed (pairs != null) or from the device sampler.  With
+// prep_stream=1 the draw / staging runs on the side stream, so that it can
+// overlap the previous step's kernels.
+int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
+             const int32_t* groups, double* loss_acc) {
+    CF_TRY(ensure_batch(e, B));
+    const int k = e->set;
+    e->set ^= 1;
+    hipStream_t ps = e->prep_side ? e->side : e->stream;
+    // set k was last used by step s-2: its apply must be done before reuse
+    if (e->prep_side) CF_HIP(hipStreamWaitEvent(ps, e->apply_done[k], 0));
+    StepArgs a;
+    CF_TRY(begin_step(e, B, pairs, negs, groups, k, ps, &a));
+    if (e->prep_side) {
+        CF_HIP(hipEventRecord(e->prep_done[k], ps));
+        CF_HIP(hipStreamWaitEvent(e->stream, e->prep_done[k], 0));
+    }
+    return finish_step(e, a, B, k, loss_acc, nullptr);
+}
+
+// n steps from the device sampler, pipelined on the engine stream: the apply
+// launch of step s also draws and counts step s+1 (3 launches per step).
+int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
+    if (n <= 0) return CF_OK;
+    CF_TRY(ensure_batch(e, B));
+    int k = e->set;
+    if (e->prep_side) CF_HIP(hipStreamWaitEvent(e->stream, e->apply_done[k], 0));
+    StepArgs a;
+    CF_TRY(begin_step(e, B, nullptr, nullptr, nullptr, k, e->stream, &a));
+    for (int s = 0; s < n; ++s) {
+        StepArgs nx{};
+        const bool more = s + 1 < n;
+        if (more) {
+            nx = base_step_args(e, B, k ^ 1);
+            CF_TRY(sampler_args(e, B, &nx));
+        }
+        CF_TRY(finish_step(e, a, B, k, loss_acc, more ? &nx : nullptr));
+        a = nx;
+        k ^= 1;
+    }
+    e->set = k;
     return CF_OK;
 }
 
@@ -485,6 +589,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     if (c.n_factors < 1 || c.n_factors > kMaxFactors) return fail(CF_EINVAL, "n_factors must be 1..256");
     if (c.n_users < 1 || c.n_users > INT32_MAX) return fail(CF_EINVAL, "n_users out of range");
     if (c.n_items < 2 || c.n_items > INT32_MAX) return fail(CF_EINVAL, "n_items out of range");
+    if (c.n_users + c.n_items > INT32_MAX) return fail(CF_EINVAL, "n_users + n_items must fit int32 (row ids)");
     if (c.n_neg < 1 || c.n_neg > kMaxNeg) return fail(CF_EINVAL, "n_neg must be 1..64");
     if (c.model == CF_GBPR && (c.gsize < 1 || c.gsize > kMaxGroup))
         return fail(CF_EINVAL, "gsize must be 1..16");
@@ -522,7 +627,10 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
         (r = dalloc(&e->cntU_[0], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[0], (size_t)c.n_items)) ||
         (r = dalloc(&e->cntU_[1], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[1], (size_t)c.n_items)) ||
-        (r = dalloc(&e->loss, 2)))
+        (r = dalloc(&e->offU, (size_t)c.n_users)) || (r = dalloc(&e->offV, (size_t)c.n_items)) ||
+        (r = dalloc(&e->dup, (size_t)(c.n_users + c.n_items))) ||
+        (r = dalloc(&e->status, 2 * (size_t)kSlotMaxBlocks)) ||
+        (r = dalloc(&e->ctl, 4)) || (r = dalloc(&e->loss, 2)))
         return bail(r);
     if (c.model == CF_GBPR) {
         if ((r = dalloc(&e->b, (size_t)c.n_items)) || (r = dalloc(&e->Ab, (size_t)c.n_items)) ||
@@ -542,6 +650,10 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         hipMemsetAsync(e->cntV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->ctl, 0, 4 * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->status, 0, 2 * kSlotMaxBlocks * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
         return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
     if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
@@ -575,10 +687,12 @@ int cf_destroy(cf_engine* e) {
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
     for (int k = 0; k < 2; ++k) {
         dfree(e->cntU_[k]); dfree(e->cntV_[k]); dfree(e->occU_[k]); dfree(e->occV_[k]);
+        dfree(e->rankU_[k]); dfree(e->rankV_[k]);
         if (e->prep_done[k]) (void)hipEventDestroy(e->prep_done[k]);
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
+    dfree(e->offU); dfree(e->offV); dfree(e->dup); dfree(e->status); dfree(e->ctl); dfree(e->slotG);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
@@ -722,9 +836,15 @@ int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_ou
     if (e->cfg.dense_item_apply && e->GV != e->GV_own)
         return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
     double* acc = loss_sum_out ? e->loss + 1 : e->loss;
-    for (int s = 0; s < n_steps; ++s) {
-        CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc));
-        if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
+    if (e->cfg.dense_item_apply) {
+        for (int s = 0; s < n_steps; ++s) {
+            CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc));
+            CF_TRY(run_items_dense(e));
+        }
+    } else if (e->pipeline) {
+        CF_TRY(run_steps_device(e, B, n_steps, acc));
+    } else {
+        for (int s = 0; s < n_steps; ++s) CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc));
     }
     if (loss_sum_out) CF_TRY(read_loss(e, 1, loss_sum_out));
     return CF_OK;
@@ -743,11 +863,12 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
     CF_TRY(sampler_args(e, B, &a));
     a.count_users = 0;
     a.count_items = 0;
-    CF_HIP(hipStreamWaitEvent(e->side, e->apply_done[k], 0));
-    CF_HIP(launch_prep(a, e->side));
+    hipStream_t ps = e->prep_side ? e->side : e->stream;
+    if (e->prep_side) CF_HIP(hipStreamWaitEvent(ps, e->apply_done[k], 0));
+    CF_HIP(launch_prep(a, ps));
     const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
     std::vector<int32_t> hu(nU), hv(nV);
-    CF_HIP(hipStreamSynchronize(e->side));
+    CF_HIP(hipStreamSynchronize(ps));
     CF_HIP(hipMemcpy(hu.data(), e->occU_[k], nU * 4, hipMemcpyDeviceToHost));
     CF_HIP(hipMemcpy(hv.data(), e->occV_[k], nV * 4, hipMemcpyDeviceToHost));
     for (int p = 0; p < B; ++p) {
@@ -909,6 +1030,28 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
         e->topk_path = (int)value;
+        return CF_OK;
+    }
+    if (n == "prep_stream") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "prep_stream must be 0 or 1");
+        CF_HIP(hipStreamSynchronize(e->stream));
+        CF_HIP(hipStreamSynchronize(e->side));
+        e->prep_side = (int)value;
+        return CF_OK;
+    }
+    if (n == "profile_mask") {
+        e->prof_mask = (uint32_t)value;
+        return CF_OK;
+    }
+    if (n == "pipeline") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "pipeline must be 0 or 1");
+        e->pipeline = (int)value;
+        return CF_OK;
+    }
+    if (n == "slot_max") {
+        if (value < 1 || value > (1 << 20)) return fail(CF_EINVAL, "slot_max must be in [1, 2^20]");
+        CF_HIP(hipStreamSynchronize(e->stream));
+        e->slot_max = (int)value;
         return CF_OK;
     }
     if (n == "grad_path") {

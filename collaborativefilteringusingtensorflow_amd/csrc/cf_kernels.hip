@@ -1,6 +1,6 @@
 // cf_kernels.hip -- the training hot path for gfx950 (MI355X / CDNA4).
 //
-// One optimizer step of BPRMF / GBPRMF / CML / AMF is three launches; the
+// One optimizer step of BPRMF / GBPRMF / CML / AMF is four launches; the
 // unit of parallelism is a 16-lane group per (u,i) pair / per row, four per
 // wave, so a wave keeps four pairs' gathers in flight.
 //
@@ -10,21 +10,27 @@
 //                (one coalesced pass, group-OR of hit masks, redraw only the
 //                rejected ones), G group users from the item's CSC column --
 //                or take a host-fed batch; then count every touched row's
-//                occurrences in the batch (one no-return atomicAdd each).
+//                occurrences (returning atomicAdd: the old value is the
+//                occurrence's rank inside its row).
+//  slot_kernel   lists the rows that occur more than once and hands each row
+//                with 2..slot_max occurrences a contiguous range of slot rows
+//                (one atomic per block).
 //  grad_kernel   gather U[u], V[i], V[j] (+U[g], b) rows, group-reduce the
 //                dots / distances, evaluate the loss and dL/dx, form every
 //                per-occurrence gradient row.  A row that occurs ONCE in the
 //                batch is updated right here with SparseApplyAdagrad
 //                (acc += g^2; w -= lr*g/sqrt(acc); CML: clip) -- its
-//                pre-update value is already in registers.  A row that
-//                occurs several times scatter-adds into a dense fp32
-//                accumulator (float atomics, 64-B segments), so duplicates
-//                SUM before the update: TF1's _deduplicate_indexed_slices
-//                (SURVEY 0.4).
-//  apply_kernel  scans the count arrays (int4 per lane) and applies the
-//                summed gradient of every duplicated row (count > 1), then
-//                zeroes its accumulator row and count.
+//                pre-update value is already in registers.  A duplicated
+//                row's gradient is a plain store into its slot row (hot rows,
+//                > slot_max occurrences, scatter-add into a dense fp32
+//                accumulator with float atomics), so duplicates SUM before
+//                the update: TF1's _deduplicate_indexed_slices.
+//  apply_kernel  walks the duplicate list: sums each row's slot rows in rank
+//                order (or takes its atomic sum), applies Adagrad and resets
+//                the row's count.
 //
+// Float atomics run at the memory side at ~1.3 TB/s chip-wide, plain stores
+// at ~6 TB/s: the store-and-sum form moves the duplicate gradients ~4x faster.
 // Reference semantics: src/models/pl/models/bprmf.py:52-88,
 // gbprmf.py:58-106, cml.py:55-129, src/models/others/models/amf.py:66-162;
 // samplers src/samplers/sampler_ranking.py:22-37, sampler_gbpr.py:23-43.
@@ -118,16 +124,37 @@ __device__ __forceinline__ void gapply(float* __restrict__ X, float* __restrict_
     }
 }
 
-// row r of X: singleton -> apply now; duplicated -> accumulate
+template <int EPL>
+__device__ __forceinline__ void gstore(float* __restrict__ S, int64_t r, int d, int gl,
+                                       const float (&g)[EPL]) {
+    float* row = S + r * (int64_t)d;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = s * kGL + gl;
+        if (e < d) row[e] = g[s];
+    }
+}
+
+// slot row of one occurrence of a duplicated row: rows with 2..slot_max
+// occurrences own the contiguous slots [off, off+count), in rank order; -1 =
+// hot row (more occurrences) or uncounted table -> float atomics into G
+__device__ __forceinline__ int64_t slot_of(int count, int off, int rank, int slot_max) {
+    return (count >= 2 && count <= slot_max) ? (int64_t)off + rank : -1;
+}
+
+// row r of X: singleton -> apply now; duplicated -> its slot row (summed by
+// apply_kernel in rank order) or, for hot rows, float atomics into G
 template <int EPL>
 __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict__ A,
                                         float* __restrict__ G, int32_t* __restrict__ cnt,
-                                        int64_t r, int count, int d, int gl,
+                                        int64_t r, int count, int64_t slot, int d, int gl,
                                         const float (&x0)[EPL], const float (&g)[EPL],
                                         const StepArgs& a) {
     if (count == 1) {
         gapply<EPL>(X, A, r, d, gl, x0, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) cnt[r] = 0;
+    } else if (slot >= 0) {
+        gstore<EPL>(a.slotG, slot, d, gl, g);
     } else {
         gatomic<EPL>(G, r, d, gl, g);
     }
@@ -162,9 +189,9 @@ __device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t
 // prep: sample (or load) the batch and count row occurrences
 // ---------------------------------------------------------------------------
 template <int MODEL>
-__global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
+__device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
     const int gl = threadIdx.x & (kGL - 1);
-    const int p = blockIdx.x * kGroupsPerBlock + (threadIdx.x >> 4);
+    const int p = block * kGroupsPerBlock + (threadIdx.x >> 4);
     if (p >= a.B) return;  // whole group leaves; no block barrier below
     const int W = a.W;
     const int G = (MODEL == GBPR) ? a.G : 0;
@@ -215,7 +242,7 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
         } else if (gl < nw) {
             j = a.occV[B + p * W + w];
         }
-        if (a.count_items && gl < nw) atomicAdd(&a.cntV[j], 1);
+        if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
     }
     if (MODEL == GBPR && gl < G) {
         int32_t g;
@@ -229,16 +256,21 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
         } else {
             g = a.occU[B + p * G + gl];
         }
-        if (a.count_users) atomicAdd(&a.cntU[g], 1);
+        if (a.count_users) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
     }
     if (gl == 0) {
         if (a.sample) {
             a.occU[p] = u;
             a.occV[p] = i;
         }
-        if (a.count_users) atomicAdd(&a.cntU[u], 1);
-        if (a.count_items) atomicAdd(&a.cntV[i], 1);
+        if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
+        if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
     }
+}
+
+template <int MODEL>
+__global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
+    prep_body<MODEL>(a, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -252,14 +284,21 @@ struct NegRows {
     static constexpr int N = WT > 0 ? WT : 1;
     int j[N];
     int c[N];
+    int64_t sl[N];  // slot row (or -1)
     float v[N][EPL];
     __device__ __forceinline__ void prefetch(const StepArgs& a, int p, int gl) {
         if constexpr (WT > 0) {
+            int rk[N];
 #pragma unroll
-            for (int w = 0; w < WT; ++w) j[w] = a.occV[a.B + p * WT + w];
+            for (int w = 0; w < WT; ++w) {
+                j[w] = a.occV[a.B + p * WT + w];
+                rk[w] = a.count_items ? a.rankV[a.B + p * WT + w] : 0;
+            }
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 c[w] = a.count_items ? a.cntV[j[w]] : 0;
+                const int o = a.count_items ? a.offV[j[w]] : 0;
+                sl[w] = slot_of(c[w], o, rk[w], a.slot_max);
                 gload<EPL>(a.V, j[w], a.d, gl, v[w]);
             }
         }
@@ -270,7 +309,10 @@ struct NegRows {
             return w;
         } else {
             j[0] = a.occV[a.B + p * a.W + w];
+            const int rk = a.count_items ? a.rankV[a.B + p * a.W + w] : 0;
             c[0] = a.count_items ? a.cntV[j[0]] : 0;
+            const int o = a.count_items ? a.offV[j[0]] : 0;
+            sl[0] = slot_of(c[0], o, rk, a.slot_max);
             gload<EPL>(a.V, j[0], a.d, gl, v[0]);
             return 0;
         }
@@ -294,10 +336,14 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
         if (p >= B) break;  // group-uniform
         const int u = a.occU[p];
         const int i = a.occV[p];
+        const int ru = a.count_users ? a.rankU[p] : 0;
+        const int ri = a.count_items ? a.rankV[p] : 0;
         NegRows<EPL, WT> J;
         J.prefetch(a, p, gl);
         const int cu = a.count_users ? a.cntU[u] : 0;
         const int ci = a.count_items ? a.cntV[i] : 0;
+        const int64_t su = slot_of(cu, a.count_users ? a.offU[u] : 0, ru, a.slot_max);
+        const int64_t si = slot_of(ci, a.count_items ? a.offV[i] : 0, ri, a.slot_max);
         float uu[EPL], vi[EPL];
         gload<EPL>(a.U, u, d, gl, uu);
         gload<EPL>(a.V, i, d, gl, vi);
@@ -333,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                     gj[s] = -c * uu[s] + a.reg * J.v[sl][s];
                     sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
                 }
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -343,8 +389,8 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else if (MODEL == GBPR) {
             // ui = rho*mean_k<g_k,i> + (1-rho)<u,i> + b_i ; uj = <u,j> + b_j   (A.2)
             const float bi = a.b[i];
@@ -383,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
                 if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj);
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, J.c[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             const float rg = a.rho / Gf;
             float gi[EPL];
@@ -394,18 +440,19 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
             for (int k2 = 0; k2 < G; ++k2) {
                 const int g = a.occU[B + p * G + k2];
                 const int cg = a.cntU[g];
+                const int64_t sg_ = slot_of(cg, a.offU[g], a.rankU[B + p * G + k2], a.slot_max);
                 float gk[EPL], gg[EPL];
                 gload<EPL>(a.U, g, d, gl, gk);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) gg[s] = rg * sc * vi[s] + a.reg * gk[s];
-                gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, g, cg, d, gl, gk, gg, a);
+                gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
             if (gl == 0) bias_finish(a, i, ci, sc);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
 #pragma unroll
@@ -457,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                     }
                 }
                 // a touched row with a zero gradient is still clipped (cml.py:128-129)
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -468,8 +515,8 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
                     sq = fmaf(vi[s], vi[s], sq);
                 }
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, gi, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         }
     }
 
@@ -501,6 +548,9 @@ __device__ __forceinline__ void gload_acc(const float* __restrict__ A, int64_t r
                                           bool want, float (&acc)[EPL]) {
 #pragma unroll
     for (int s = 0; s < EPL; ++s) acc[s] = 1.f;
+#ifdef CF_EXP_NO_ACC
+    want = false;
+#endif
     if (want) {
         const float* row = A + r * (int64_t)d;
 #pragma unroll
@@ -544,14 +594,21 @@ __device__ __forceinline__ void gapply_pre(float* __restrict__ X, float* __restr
 template <int EPL>
 __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __restrict__ A,
                                             float* __restrict__ G, int32_t* __restrict__ cnt,
-                                            int64_t r, int count, int d, int gl,
+                                            int64_t r, int count, int64_t slot, int d, int gl,
                                             const float (&x0)[EPL], const float (&acc0)[EPL],
                                             const float (&g)[EPL], const StepArgs& a) {
+    // CF_EXP_* are bench-only attribution builds (wrong results by design)
     if (count == 1) {
+#ifndef CF_EXP_NO_SINGLE
         gapply_pre<EPL>(X, A, r, d, gl, x0, acc0, g, a.lr, a.clip != 0, a.clip_norm);
+#endif
         if (gl == 0) cnt[r] = 0;
+    } else if (slot >= 0) {
+        gstore<EPL>(a.slotG, slot, d, gl, g);
     } else {
+#ifndef CF_EXP_NO_ATOMIC
         gatomic<EPL>(G, r, d, gl, g);
+#endif
     }
 }
 
@@ -559,9 +616,11 @@ template <int MODEL, int EPL, int WT>
 struct PairRows {
     static constexpr int NG = (MODEL == GBPR) ? 1 : 0;
     static constexpr int NGA = NG > 0 ? NG : 1;
-    int u, i, cu, ci;
-    int j[WT], cj[WT];
-    int g[NGA], cg[NGA];
+    int u, i, cu, ci, ru, ri;
+    int j[WT], cj[WT], rj[WT];
+    int g[NGA], cg[NGA], rg[NGA];
+    int ou_, oi_;                      // slot bases, until load_acc
+    int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
     float uu[EPL], vi[EPL], au[EPL], ai[EPL];
     float vj[WT][EPL], aj[WT][EPL];
     float ug[NGA][EPL], ag[NGA][EPL];
@@ -570,18 +629,34 @@ struct PairRows {
     __device__ __forceinline__ void load_idx(const StepArgs& a, int p) {
         u = a.occU[p];
         i = a.occV[p];
+        ru = a.count_users ? a.rankU[p] : 0;
+        ri = a.count_items ? a.rankV[p] : 0;
 #pragma unroll
-        for (int w = 0; w < WT; ++w) j[w] = a.occV[a.B + p * WT + w];
+        for (int w = 0; w < WT; ++w) {
+            j[w] = a.occV[a.B + p * WT + w];
+            rj[w] = a.count_items ? a.rankV[a.B + p * WT + w] : 0;
+        }
 #pragma unroll
-        for (int k = 0; k < NG; ++k) g[k] = a.occU[a.B + p + k];
+        for (int k = 0; k < NG; ++k) {
+            g[k] = a.occU[a.B + p + k];
+            rg[k] = a.count_users ? a.rankU[a.B + p + k] : 0;
+        }
     }
     __device__ __forceinline__ void load_rows(const StepArgs& a, int gl) {
         cu = a.count_users ? a.cntU[u] : 0;
         ci = a.count_items ? a.cntV[i] : 0;
+        ou_ = a.count_users ? a.offU[u] : 0;
+        oi_ = a.count_items ? a.offV[i] : 0;
 #pragma unroll
-        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+        for (int w = 0; w < WT; ++w) {
+            cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+            sj[w] = a.count_items ? a.offV[j[w]] : 0;
+        }
 #pragma unroll
-        for (int k = 0; k < NG; ++k) cg[k] = a.count_users ? a.cntU[g[k]] : 0;
+        for (int k = 0; k < NG; ++k) {
+            cg[k] = a.count_users ? a.cntU[g[k]] : 0;
+            sg[k] = a.count_users ? a.offU[g[k]] : 0;
+        }
         gload<EPL>(a.U, u, a.d, gl, uu);
         gload<EPL>(a.V, i, a.d, gl, vi);
 #pragma unroll
@@ -595,6 +670,12 @@ struct PairRows {
         }
     }
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
+        su = slot_of(cu, ou_, ru, a.slot_max);
+        si = slot_of(ci, oi_, ri, a.slot_max);
+#pragma unroll
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], (int)sj[w], rj[w], a.slot_max);
+#pragma unroll
+        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], (int)sg[k], rg[k], a.slot_max);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
         gload_acc<EPL>(a.AV, i, a.d, gl, ci == 1, ai);
 #pragma unroll
@@ -633,7 +714,7 @@ struct PairRows {
                     gj[s] = -c * uu[s] + a.reg * vj[w][s];
                     sq = fmaf(vj[w][s], vj[w][s], sq);
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -643,8 +724,8 @@ struct PairRows {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else if (MODEL == GBPR) {  // G == 1
             const float ui_u = gdot<EPL>(uu, vi);
 #pragma unroll
@@ -667,7 +748,7 @@ struct PairRows {
                     gj[s] = -c * uu[s];
                 }
                 if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w]);
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             const float rg = a.rho;  // rho / G with G == 1
             float gi[EPL], gg[EPL];
@@ -679,10 +760,10 @@ struct PairRows {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], d, gl, ug[0], ag[0], gg, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
             if (gl == 0) bias_finish(a, i, ci, sc);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else {  // CML
             float du[EPL];
 #pragma unroll
@@ -730,7 +811,7 @@ struct PairRows {
                         sq = fmaf(vj[w][s], vj[w][s], sq);
                     }
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -741,8 +822,8 @@ struct PairRows {
                     sq = fmaf(vi[s], vi[s], sq);
                 }
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         }
     }
 };
@@ -788,16 +869,147 @@ __global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// apply the summed gradient of every duplicated row (count > 1)
+// slots: after prep's counts are final, list every duplicated row (count >= 2)
+// and give each row with 2..slot_max occurrences a contiguous range of slot
+// rows.  Ranges are allocated per block with ONE atomic per block (their
+// order does not matter, only that each row's slots are contiguous).
+// ---------------------------------------------------------------------------
+constexpr int kSlotRPT = 8;  // rows per thread per chunk
+
+__device__ __forceinline__ void slot_counts(const SlotArgs& a, const int32_t* cnt, int64_t n,
+                                            bool counted, int64_t r0, int (&c)[kSlotRPT]) {
+#pragma unroll
+    for (int q = 0; q < kSlotRPT; q += 4) {
+        const int64_t r = r0 + q;
+        if (counted && r + 3 < n) {
+            const int4 v = *reinterpret_cast<const int4*>(cnt + r);
+            c[q] = v.x; c[q + 1] = v.y; c[q + 2] = v.z; c[q + 3] = v.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) c[q + t] = (counted && r + t < n) ? cnt[r + t] : 0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
+    __shared__ int s_wd[kWavesPerBlock], s_ws[kWavesPerBlock];
+    __shared__ int s_base[2];
+    if (blockIdx.x == 0)
+        for (int k = threadIdx.x; k < kSlotMaxBlocks; k += kBlock)
+            __hip_atomic_store(a.status_next + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int blk = blockIdx.x;
+    const bool isU = blk < a.blocksU;
+    const int64_t n = isU ? a.n_users : a.n_items;
+    const bool counted = isU ? a.count_users != 0 : a.count_items != 0;
+    const int32_t* cnt = isU ? a.cntU : a.cntV;
+    const int64_t rb = (int64_t)(isU ? blk : blk - a.blocksU) * a.rows_per_block;
+    const int chunks = a.rows_per_block / (kBlock * kSlotRPT);
+    // pass 1: this thread's duplicated rows and slot rows (any order is valid:
+    // only per-row contiguity of the slot ranges matters)
+    int nd = 0, ns = 0;
+    for (int ch = 0; ch < chunks; ++ch) {
+        int c[kSlotRPT];
+        slot_counts(a, cnt, n, counted, rb + (int64_t)ch * kBlock * kSlotRPT + threadIdx.x * kSlotRPT, c);
+#pragma unroll
+        for (int q = 0; q < kSlotRPT; ++q) {
+            nd += (c[q] >= 2) ? 1 : 0;
+            ns += (c[q] >= 2 && c[q] <= a.slot_max) ? c[q] : 0;
+        }
+    }
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const int id = wave_incl_scan(nd), is = wave_incl_scan(ns);
+    if (lane == 63) {
+        s_wd[wv] = id;
+        s_ws[wv] = is;
+    }
+    __syncthreads();
+    int pd = id - nd, ps = is - ns, td = 0, ts = 0;
+#pragma unroll
+    for (int k = 0; k < kWavesPerBlock; ++k) {
+        if (k < wv) {
+            pd += s_wd[k];
+            ps += s_ws[k];
+        }
+        td += s_wd[k];
+        ts += s_ws[k];
+    }
+    // publish this block's totals (flag bit 63 | dups << 32 | slots) in ONE
+    // 8-B agent-scope store, then sum every lower block's word (relaxed agent
+    // loads, L1 bypassed).  Each block publishes before it waits and waits only
+    // on lower ids, and the grid is <= kSlotMaxBlocks, so it always drains.
+    if (threadIdx.x == 0)
+        __hip_atomic_store(a.status + blk,
+                           (1ull << 63) | ((uint64_t)(uint32_t)td << 32) | (uint64_t)(uint32_t)ts,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int bd = 0, bs = 0;
+    for (int k = threadIdx.x; k < blk; k += kBlock) {
+        uint64_t w;
+        do {
+            w = __hip_atomic_load(a.status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while ((w >> 63) == 0ull);
+        bd += (int)((w >> 32) & 0x7FFFFFFFull);
+        bs += (int)(uint32_t)w;
+    }
+    bd = wave_sum_i(bd);
+    bs = wave_sum_i(bs);
+    __syncthreads();  // s_wd / s_ws are reused
+    if (lane == 0) {
+        s_wd[wv] = bd;
+        s_ws[wv] = bs;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int x = 0, y = 0;
+#pragma unroll
+        for (int k = 0; k < kWavesPerBlock; ++k) {
+            x += s_wd[k];
+            y += s_ws[k];
+        }
+        s_base[0] = x;
+        s_base[1] = y;
+        if (blk == (int)gridDim.x - 1) {
+            a.ctl[0] = y + ts;
+            a.ctl[1] = x + td;
+        }
+    }
+    __syncthreads();
+    if (td == 0) return;  // block-uniform
+    pd += s_base[0];
+    ps += s_base[1];
+    // pass 2: write the list entries and slot bases (counts re-read, L2-warm)
+    int32_t* off = isU ? a.offU : a.offV;
+    const int64_t gbase = isU ? 0 : a.n_users;
+    for (int ch = 0; ch < chunks && nd > 0; ++ch) {
+        const int64_t r0 = rb + (int64_t)ch * kBlock * kSlotRPT + threadIdx.x * kSlotRPT;
+        int c[kSlotRPT];
+        slot_counts(a, cnt, n, counted, r0, c);
+#pragma unroll
+        for (int q = 0; q < kSlotRPT; ++q) {
+            if (c[q] >= 2) {
+                a.dup[pd++] = (int32_t)(gbase + r0 + q);
+                if (c[q] <= a.slot_max) {
+                    off[r0 + q] = ps;
+                    ps += c[q];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// apply the summed gradient of every duplicated row: the TF1 IndexedSlices
+// dedup-sum + SparseApplyAdagrad (bprmf.py:74-75 and siblings).  One group
+// per listed row: the slot rows [off, off+count) summed in rank order, or the
+// atomic sum in G for a hot row (G re-zeroed); then the row's count is reset.
+// Block 0 also folds the grad kernel's loss partials.
 // ---------------------------------------------------------------------------
 template <int EPL>
-__global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
+__device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     __shared__ double s_red[kWavesPerBlock];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
-    const int gw = lane >> 4;       // group inside the wave
     const int gl = lane & (kGL - 1);
-    if (blockIdx.x == 0 && a.loss_acc != nullptr) {
+    if (block == 0 && a.loss_acc != nullptr) {
         double t = 0.0;
         for (int k = threadIdx.x; k < a.n_partial; k += kBlock) t += a.loss_partial[k];
         t = wave_sum_d(t);
@@ -805,60 +1017,73 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
         __syncthreads();
         if (threadIdx.x == 0) a.loss_acc[0] += (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
-    const bool isU = (int)blockIdx.x < a.blocksU;
-    const int64_t blk = isU ? (int64_t)blockIdx.x : (int64_t)blockIdx.x - a.blocksU;
-    const int64_t n = isU ? a.n_users : a.n_items;
-    int32_t* cnt = isU ? a.cntU : a.cntV;
-    float* X = isU ? a.U : a.V;
-    float* A = isU ? a.AU : a.AV;
-    float* G = isU ? a.GU : a.GV;
-    const bool bias = !isU && a.b != nullptr;
-
-    const int rpt = isU ? 4 : 1;                   // rows per thread
-    const int64_t base_row = blk * (isU ? kApplyRowsPerBlockU : kApplyRowsPerBlockV);
-    const int64_t r0 = base_row + (int64_t)threadIdx.x * rpt;
-    int c4[4] = {0, 0, 0, 0};
-    if (rpt == 4 && r0 + 3 < n) {
-        const int4 v = *reinterpret_cast<const int4*>(cnt + r0);
-        c4[0] = v.x; c4[1] = v.y; c4[2] = v.z; c4[3] = v.w;
-    } else {
-        for (int q = 0; q < rpt; ++q) c4[q] = (r0 + q < n) ? cnt[r0 + q] : 0;
-    }
+    const int64_t total = a.ctl[1];
+    const int64_t ngrp = ((int64_t)nblocks * kBlock) >> 4;
+    for (int64_t t = ((int64_t)block * kBlock + threadIdx.x) >> 4; t < total; t += ngrp) {
+        const int64_t id = a.dup[t];
+        const bool isU = id < a.n_users;  // group-uniform
+        const int64_t r = isU ? id : id - a.n_users;
+        int32_t* cnt = isU ? a.cntU : a.cntV;
+        float* X = isU ? a.U : a.V;
+        float* A = isU ? a.AU : a.AV;
+        float* G = isU ? a.GU : a.GV;
+        const int c = cnt[r];
+        const int64_t s0 = (c <= a.slot_max) ? (isU ? a.offU[r] : a.offV[r]) : -1;
+        float x[EPL], acc[EPL], g[EPL];
+        gload<EPL>(X, r, a.d, gl, x);
+        gload_acc<EPL>(A, r, a.d, gl, true, acc);
+        if (s0 >= 0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (q >= rpt) break;  // block-uniform
-        const bool win = c4[q] > 1;
-        const int64_t r_l = r0 + q;
-        if (bias && win) {
-            const float g = a.Gb[r_l];
-            const float acc = fmaf(g, g, a.Ab[r_l]);
-            a.Ab[r_l] = acc;
-            a.b[r_l] -= (a.lr * g) / sqrtf(acc);
-            a.Gb[r_l] = 0.f;
-        }
-        const unsigned long long m = __ballot(win);
-        const int nwin = __popcll(m);
-        for (int base = 0; base < nwin; base += 4) {  // wave-uniform
-            const int my = base + gw;
-            unsigned long long mm = m;
-            for (int t = 0; t < my && mm; ++t) mm &= mm - 1ull;
-            const int pos = (my < nwin) ? __ffsll((long long)mm) - 1 : 0;
-            const int64_t r = base_row + __shfl((int)threadIdx.x * rpt + q, pos, 64);
-            if (my < nwin) {  // group-uniform
-                float g[EPL], x[EPL];
-                gload<EPL>(G, r, a.d, gl, g);
-                gload<EPL>(X, r, a.d, gl, x);
-                float* gr = G + r * a.d;
+            for (int s = 0; s < EPL; ++s) g[s] = 0.f;
+            for (int t0 = 0; t0 < c; t0 += 4) {  // 4 slot rows in flight, summed in rank order
+                float h[4][EPL];
 #pragma unroll
-                for (int s = 0; s < EPL; ++s) {
-                    const int e = s * kGL + gl;
-                    if (e < a.d) gr[e] = 0.f;
-                }
-                gapply<EPL>(X, A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
+                for (int q = 0; q < 4; ++q)
+                    if (t0 + q < c) gload<EPL>(a.slotG, s0 + t0 + q, a.d, gl, h[q]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (t0 + q < c) {
+#pragma unroll
+                        for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+                    }
+            }
+        } else {
+            gload<EPL>(G, r, a.d, gl, g);
+            float* gr = G + r * a.d;
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                const int e = s * kGL + gl;
+                if (e < a.d) gr[e] = 0.f;
             }
         }
-        if (win) cnt[r_l] = 0;
+        gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
+        if (gl == 0) {
+            cnt[r] = 0;
+            if (!isU && a.b != nullptr) {
+                const float gb = a.Gb[r];
+                const float ab = fmaf(gb, gb, a.Ab[r]);
+                a.Ab[r] = ab;
+                a.b[r] -= (a.lr * gb) / sqrtf(ab);
+                a.Gb[r] = 0.f;
+            }
+        }
     }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
+    apply_body<EPL>(a, blockIdx.x, gridDim.x);
+}
+
+// horizontal fusion on the device-sampler path: apply of step s (blocks
+// [0, napply)) beside the draw + count of step s+1 (the rest) -- independent
+// work (other buffer set), one launch instead of two
+template <int EPL, int MODEL>
+__global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArgs a, int napply) {
+    if ((int)blockIdx.x < napply)
+        apply_body<EPL>(p, blockIdx.x, napply);
+    else
+        prep_body<MODEL>(a, blockIdx.x - napply);
 }
 
 // ---------------------------------------------------------------------------
@@ -1048,11 +1273,30 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
     }
 }
 
+hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid) {
+    // rows per block: the smallest multiple of one chunk (kBlock * kSlotRPT)
+    // that keeps the grid within kSlotMaxBlocks
+    const int64_t chunk = (int64_t)kBlock * kSlotRPT;
+    int64_t rpb = chunk;
+    while ((a.n_users + rpb - 1) / rpb + (a.n_items + rpb - 1) / rpb > kSlotMaxBlocks) rpb += chunk;
+    if (rpb > (int64_t)1 << 30) return hipErrorInvalidValue;
+    a.rows_per_block = (int)rpb;
+    a.blocksU = (int)((a.n_users + rpb - 1) / rpb);
+    const int blocks = a.blocksU + (int)((a.n_items + rpb - 1) / rpb);
+    if (grid) *grid = blocks;
+    hipLaunchKernelGGL(slot_kernel, dim3(blocks), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+static int apply_grid(const ApplyArgs& a) {
+    int64_t blocks = ((int64_t)a.max_groups + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    if (blocks > 2048) blocks = 2048;  // grid-stride over the list
+    if (blocks < 1) blocks = 1;        // block 0 still reduces the loss
+    return (int)blocks;
+}
+
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
-    const int bV = a.apply_items ? (int)((a.n_items + kApplyRowsPerBlockV - 1) / kApplyRowsPerBlockV) : 0;
-    int blocks = a.blocksU + bV;
-    if (blocks == 0) blocks = 1;  // block 0 still reduces the loss
-    const dim3 grid(blocks), block(kBlock);
+    const dim3 grid(apply_grid(a)), block(kBlock);
     switch (epl_for(a.d)) {
         case 1: hipLaunchKernelGGL(apply_kernel<1>, grid, block, 0, s, a); break;
         case 2: hipLaunchKernelGGL(apply_kernel<2>, grid, block, 0, s, a); break;
@@ -1061,6 +1305,26 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
         default: hipLaunchKernelGGL(apply_kernel<16>, grid, block, 0, s, a); break;
     }
     return hipGetLastError();
+}
+
+template <int MODEL>
+static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
+    const int na = apply_grid(p);
+    const int np = (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    const dim3 grid(na + np), block(kBlock);
+    switch (epl_for(p.d)) {
+        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL>), grid, block, 0, s, p, a, na); break;
+        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL>), grid, block, 0, s, p, a, na); break;
+        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL>), grid, block, 0, s, p, a, na); break;
+        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL>), grid, block, 0, s, p, a, na); break;
+        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL>), grid, block, 0, s, p, a, na); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
+    if (a.B <= 0) return launch_apply(p, s);
+    return a.model == GBPR ? launch_apply_prep_m<GBPR>(p, a, s) : launch_apply_prep_m<BPR>(p, a, s);
 }
 
 static int row_grid(int64_t n_rows) {

@@ -69,7 +69,9 @@ enum cf_kernel_id {
     CF_K_CLIP = 4,       /* CML full-table clip_by_norm                       */
     CF_K_SCORE = 5,      /* user x item scoring tile kernel                   */
     CF_K_TOPK = 6,       /* masked per-user top-k                             */
-    CF_K_COUNT = 7
+    CF_K_SLOT = 7,       /* duplicate-row list + slot ranges (store-and-sum)   */
+    CF_K_APPLY_PREP = 8, /* apply of step s fused with the draw of step s+1    */
+    CF_K_COUNT = 9
 };
 
 /*
@@ -234,6 +236,20 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "grad_path"  0 = auto (phased gradient kernel for W in {1,5}, d <= 128,
  *                GBPR group size 1; generic kernel otherwise), 1 = generic
  *                kernel always.  Both give the same arithmetic.
+ *   "prep_stream" 0 = everything in order on the engine stream (default);
+ *                1 = sample/count on a side stream, overlapping the previous
+ *                step's gradient.  Same results.
+ *   "slot_max"   rows occurring 2..slot_max times in a batch sum their
+ *                per-occurrence gradient rows from plain-stored slots; rows
+ *                occurring more often use float atomics (default 32; 1 = atomics
+ *                for every duplicated row).  Same arithmetic up to fp32
+ *                summation order.
+ *   "pipeline"   1 = cf_train_steps launches the duplicate apply of step s and
+ *                the draw + count of step s+1 as one kernel (default); 0 = one
+ *                step at a time.  Same results.
+ *   "profile_mask" bit k set = cf_profile_enable times kernel id k (default
+ *                all): timing only the kernel of interest keeps the event
+ *                pairs of the others out of a timed loop.
  */
 int cf_set_option(cf_engine* eng, const char* name, int64_t value);
 

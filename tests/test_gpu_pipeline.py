@@ -1,0 +1,76 @@
+"""The device-sampler training loop (cf_train_steps) against the same batches
+fed one step at a time.  train_steps pipelines the steps -- the duplicate
+apply of step s and the draw + count of step s+1 share one launch
+(cf_set_option "pipeline"), or the draw runs on a side stream ("prep_stream")
+-- and must train exactly what cf_sample + cf_step train on the identical
+sampler stream (same seed => same (epoch, batch) => same batch).
+
+Tolerance: 1e-5 relative (fp32 summation order of duplicated rows may differ).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def make(model, fold1, d, W, G, **opts):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    kw = dict(reg=0.05)
+    if model == "gbpr":
+        kw["rho"] = 0.4
+    e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=G,
+               seed=31, **kw)
+    for k, v in opts.items():
+        e.set_option(k, v)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=5)
+    if model == "amf":
+        e.begin_phase(1)
+    return e
+
+
+TABLES = {"bpr": ("user", "item", "acc_user", "acc_item"),
+          "amf": ("user", "item", "acc_user", "acc_item"),
+          "cml": ("user", "item", "acc_user", "acc_item"),
+          "gbpr": ("user", "item", "bias", "acc_user", "acc_item", "acc_bias")}
+
+
+@pytest.mark.parametrize("opts", [{}, {"pipeline": 0}, {"prep_stream": 1, "pipeline": 0},
+                                  {"slot_max": 2}],
+                         ids=["pipelined", "stepwise", "side-stream", "slot2"])
+@pytest.mark.parametrize("model,d,W,G,B", [("bpr", 32, 1, 1, 100), ("bpr", 24, 5, 1, 250),
+                                           ("gbpr", 16, 5, 1, 100), ("gbpr", 16, 2, 3, 100),
+                                           ("cml", 20, 5, 1, 100), ("amf", 40, 5, 1, 100)])
+def test_train_steps_equals_host_fed_stream(fold1, model, d, W, G, B, opts):
+    K = 23
+    host = make(model, fold1, d, W, G)
+    dev = make(model, fold1, d, W, G, **opts)
+    loss_h = 0.0
+    for _ in range(K):
+        pairs, negs, groups = host.sample(B)
+        loss_h += host.step(pairs, negs, groups)
+    loss_d = dev.train_steps(B, K)
+    assert abs(loss_d - loss_h) <= RTOL * abs(loss_h), (loss_d, loss_h)
+    assert host.sampler_state() == dev.sampler_state()
+    for t in TABLES[model]:
+        assert rel(dev.get_table(t), host.get_table(t)) <= RTOL, (t, rel(dev.get_table(t), host.get_table(t)))
+    # the pipelined engine continues correctly after a host-fed step
+    pairs, negs, groups = host.sample(B)
+    p2, n2, g2 = dev.sample(B)
+    assert np.array_equal(pairs, p2) and np.array_equal(negs, n2)
+    host.step(pairs, negs, groups)
+    dev.step(p2, n2, g2)
+    host.train_steps(B, 3)
+    dev.train_steps(B, 3)
+    for t in TABLES[model]:
+        assert rel(dev.get_table(t), host.get_table(t)) <= RTOL, t
+    host.close()
+    dev.close()

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 _GRAD_PATH = [0]
+_OPTS = {}   # extra cf_set_option values for make_engine
 
 
 @pytest.fixture(autouse=True, params=[0, 1], ids=["phased", "generic"])
@@ -39,6 +40,8 @@ def make_engine(model, fold1, d, W, G=1, dense=False, **kw):
     e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=G,
                dense_item_apply=dense, seed=7, **kw)
     e.set_option("grad_path", _GRAD_PATH[0])
+    for k, v in _OPTS.items():
+        e.set_option(k, v)
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     return e
 
@@ -153,9 +156,29 @@ def test_cml_steps_match_oracle(fold1, streams, reg_cov, use_rw, dense):
     e.close()
 
 
-def test_duplicate_rows_sum_before_adagrad(fold1):
+@pytest.fixture
+def opts():
+    yield _OPTS
+    _OPTS.clear()
+
+
+@pytest.mark.parametrize("slot_max", [1, 2, 3, 1 << 20])
+@pytest.mark.parametrize("model,name,d", [("bpr", "rank_b50_w5", 24), ("amf", "rank_b100_w5", 40)])
+def test_slot_regimes_match_oracle(fold1, streams, opts, slot_max, model, name, d):
+    """Duplicated rows: every split between slot store-and-sum (2..slot_max
+    occurrences) and float atomics (more) gives the TF1 dedup-sum."""
+    opts["slot_max"] = slot_max
+    out = run_bpr_like(model, fold1, get_stream(streams, name), d, 0.05, K=40)
+    for t, (g, o) in out.items():
+        assert rel(g, o) <= RTOL, (t, rel(g, o))
+
+
+@pytest.mark.parametrize("slot_max", [32, 64])
+def test_duplicate_rows_sum_before_adagrad(fold1, opts, slot_max):
     """TF1 dedups IndexedSlices before SparseApplyAdagrad: a batch
-    that repeats the same (u,i,j) must differ from per-occurrence updates."""
+    that repeats the same (u,i,j) must differ from per-occurrence updates.
+    37 repeats: float atomics at slot_max 32, 37 summed slot rows at 64."""
+    opts["slot_max"] = slot_max
     d = 8
     U, V, _ = init_tables(fold1, d, 11)
     e = make_engine("bpr", fold1, d, 1, reg=0.0)
@@ -194,3 +217,12 @@ def test_untouched_rows_unchanged(fold1, streams):
     assert np.array_equal(V2[mv], V[mv])
     assert not np.array_equal(U2[touched_u], U[touched_u])
     e.close()
+
+
+def test_side_stream_prep_matches_oracle(fold1, streams, opts):
+    """prep_stream=1: the next batch is staged and counted on a side stream
+    while the current step runs; results are those of the in-order engine."""
+    opts["prep_stream"] = 1
+    out = run_bpr_like("bpr", fold1, get_stream(streams, "rank_b100_w5"), 32, 0.05, K=40)
+    for t, (g, o) in out.items():
+        assert rel(g, o) <= RTOL, (t, rel(g, o))

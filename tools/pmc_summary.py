@@ -19,9 +19,10 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHORT = {"grad_kernel": "step", "prep_kernel": "sample", "apply_kernel": "apply",
+SHORT = {"grad_fast_kernel": "step", "grad_kernel": "step", "apply_prep_kernel": "apply_prep",
+         "prep_kernel": "sample", "slot_kernel": "slot", "apply_kernel": "apply",
          "apply_dense_kernel": "apply_dense", "clip_full_kernel": "clip",
-         "score_kernel": "score", "topk_kernel": "topk"}
+         "fused_topk_kernel": "fused_topk", "score_kernel": "score", "topk_kernel": "topk"}
 
 
 def short(name):
