@@ -56,6 +56,20 @@ def durations(d):
     return out
 
 
+def kernel_csv(d, counter, out):
+    """Per-kernel mean of one counter (KiB) -> profiles/<round>/<tag>_pmc_*.csv"""
+    acc = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] == counter:
+                    acc[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    with open(out, "w") as f:
+        f.write("kernel,counter,dispatches,mean_value_KiB\n")
+        for k in sorted(acc):
+            f.write('"%s",%s,%d,%.3f\n' % (k, counter, len(acc[k]), sum(acc[k]) / len(acc[k])))
+
+
 def main():
     tag, fdir, wdir = sys.argv[1:4]
     tdir = sys.argv[4] if len(sys.argv) > 4 else None
@@ -83,6 +97,10 @@ def main():
                            "KiB -> bytes, FETCH x2 gfx950 correction"}
     with open(path, "w") as f:
         json.dump(data, f, indent=1)
+    rnd = os.environ.get("CF_ROUND", "r01")
+    os.makedirs(os.path.join(ROOT, "profiles", rnd), exist_ok=True)
+    kernel_csv(fdir, "FETCH_SIZE", os.path.join(ROOT, "profiles", rnd, tag + "_pmc_fetch.csv"))
+    kernel_csv(wdir, "WRITE_SIZE", os.path.join(ROOT, "profiles", rnd, tag + "_pmc_write.csv"))
     print(json.dumps(data[tag], indent=1))
 
 
