@@ -73,6 +73,17 @@ def full_step_bytes_per_pair(d, W, G=0):
     return rows * 16 * d + 4 * rows
 
 
+def draw_bytes_per_pair(W, G, mean_row):
+    """Algorithmic bytes of the device draw + count of one pair (prep_body):
+    the pair record (8 B), its user's CSR extent (2 x 8 B) and row scan
+    (4 B x row length, mean over pairs = sum(deg^2)/sum(deg)), the occurrence
+    ids and ranks written (2 x 4 B per occurrence) and one count atomic per
+    occurrence (4 B); GBPR adds the item's CSC extent + one user id per group
+    member."""
+    occ = 2 + W + G
+    return 8 + 16 + 4 * mean_row + 12 * occ + ((16 + 4 * G) if G else 0)
+
+
 def load_pmc(workload, n_gpus):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -128,7 +139,8 @@ def main():
     ap.add_argument("--prep-stream", type=int, default=0,
                     help="cf_set_option prep_stream: 0 in-order (default), 1 side stream")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="cf_set_option pipeline: 1 apply(s)+draw(s+1) in one launch (default)")
+                    help="cf_set_option pipeline: 2 grad(s)+draw(s+1), apply(s)+slots(s+1) (default); "
+                         "1 apply(s)+draw(s+1); 0 stepwise")
     ap.add_argument("--slot-max", type=int, default=0,
                     help="cf_set_option slot_max (0 = engine default)")
     args = ap.parse_args()
@@ -202,7 +214,10 @@ def main():
     # timed region: HIP events around the dominant kernel only (an event pair
     # around every launch would add ~20 us per step to the loop)
     eng.profile_reset()
-    eng.set_option("profile_mask", 1 << KERNELS["step"])
+    # pipeline 2 (default): the dominant launch is the gradient of step s fused
+    # with the draw + count of step s+1 ("grad_prep"); otherwise "step"
+    dom = "grad_prep" if (world == 1 and args.pipeline == 2) else "step"
+    eng.set_option("profile_mask", 1 << KERNELS[dom])
     eng.profile(not args.no_profile)
     sync()
     t0 = time.perf_counter()
@@ -214,7 +229,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local_rank)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    step_ms, step_n = eng.profile_read("step")
+    step_ms, step_n = eng.profile_read(dom)
 
     # per-kernel breakdown: a separate, untimed pass with every launch timed
     kernels = {}
@@ -226,7 +241,8 @@ def main():
         run(nb)
         sync()
         eng.profile(False)
-        for kname in ("sample", "slot", "step", "apply", "apply_prep", "apply_dense", "clip"):
+        for kname in ("sample", "slot", "step", "grad_prep", "apply", "apply_prep", "apply_slot",
+                      "apply_dense", "clip"):
             ms, n = eng.profile_read(kname)
             if n:
                 kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}
@@ -238,17 +254,30 @@ def main():
     total_trip = trip_per_step * args.steps * world
     value = total_trip / elapsed
     step_avg_s = (1e-3 * step_ms / step_n) if step_n else float("nan")
-    gb = gather_bytes_per_pair(d, W, cfg["G"] if cfg["model"] == "gbpr" else 0,
-                               bias=cfg["model"] == "gbpr") * B
-    achieved = gb / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
+    Gm = cfg["G"] if cfg["model"] == "gbpr" else 0
+    gb = gather_bytes_per_pair(d, W, Gm, bias=cfg["model"] == "gbpr") * B
+    deg = np.diff(np.asarray(indptr, dtype=np.int64)).astype(np.float64)
+    mean_row = float((deg * deg).sum() / max(deg.sum(), 1.0))
+    db = draw_bytes_per_pair(W, Gm, mean_row) * B if dom == "grad_prep" else 0.0
+    achieved = (gb + db) / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
     traffic = load_pmc(args.config, world)
-    roofline = {"kernel": "grad_kernel (gather + loss + grads + singleton-row Adagrad)",
+    if dom == "grad_prep":
+        kdesc = ("grad_fast_kernel: gather + loss + grads + singleton-row Adagrad of step s, "
+                 "fused with the device draw + count of step s+1")
+        bdef = ("SURVEY 8(d) gather bytes B*((2+W)*4d + 4(2+W)) of step s + draw bytes of step s+1 "
+                "B*(8 + 16 + 4*E[row] + 12(2+W)), E[row] = sum(deg^2)/nnz = %.1f" % mean_row)
+    else:
+        kdesc = "grad_kernel (gather + loss + grads + singleton-row Adagrad)"
+        bdef = "SURVEY 8(d) gather bytes: B*((2+W)*4d + 4(2+W))"
+    roofline = {"kernel": kdesc,
                 "bound": "hbm",
                 "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                 "traffic": traffic,
-                "bytes_per_launch": gb,
-                "bytes_def": "SURVEY 8(d) gather bytes: B*((2+W)*4d + 4(2+W))",
+                "bytes_per_launch": gb + db,
+                "gather_bytes_per_launch": gb,
+                "gather_only_GBps": gb / step_avg_s / 1e9 if achieved else None,
+                "bytes_def": bdef,
                 "avg_launch_us": step_avg_s * 1e6 if step_n else None,
                 "timed_launches": step_n}
     full_b = full_step_bytes_per_pair(d, W) * B * args.steps * world

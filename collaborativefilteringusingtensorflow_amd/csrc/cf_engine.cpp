@@ -66,7 +66,7 @@ struct cf_engine {
     int64_t nnz = 0;
     int64_t* indptr = nullptr;
     int32_t* indices = nullptr;
-    int2* pairs = nullptr;
+    int4* pairs = nullptr;   // (u, i, row start, row length) per interaction
     int64_t* indptr_t = nullptr;
     int32_t* indices_t = nullptr;
     std::vector<int64_t> h_indptr;
@@ -79,17 +79,23 @@ struct cf_engine {
     int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
     int32_t* cntV_[2] = {nullptr, nullptr};
     // store-and-sum of duplicated rows (slot_kernel): slot base per row, the
-    // duplicate list (global row ids), [slots used, |dup|], and the slot
-    // kernel's per-block status words [2 steps][kSlotMaxBlocks]
-    int32_t *offU = nullptr, *offV = nullptr;
-    int32_t* dup = nullptr;
-    int32_t* ctl = nullptr;
+    // duplicate list (global row ids), [slots used, |dup|] -- one set per batch
+    // buffer set, so that the slot pass of step s+1 can run beside the apply
+    // of step s -- and the slot kernel's per-block status words
+    // [2 launches][kSlotMaxBlocks]
+    int32_t* offU_[2] = {nullptr, nullptr};
+    int32_t* offV_[2] = {nullptr, nullptr};
+    int32_t* dup_[2] = {nullptr, nullptr};
+    int32_t* ctl_[2] = {nullptr, nullptr};
     uint64_t* status = nullptr;
     int status_par = 0;
     float* slotG = nullptr;   // [slot_cap, d]
     size_t slot_cap = 0;
     int slot_max = 32;        // cf_set_option("slot_max")
-    int pipeline = 1;         // cf_set_option("pipeline"): cf_train_steps fuses apply(s) + prep(s+1)
+    // cf_set_option("pipeline") for cf_train_steps: 0 = four launches per
+    // step (prep, slot, grad, apply); 1 = apply(s) + prep(s+1) fused;
+    // 2 = grad(s) + prep(s+1) and apply(s) + slot(s+1) fused (two launches)
+    int pipeline = 1;
 
     // batch: two buffer sets, so that the sampler of step s+1 runs on the side
     // stream while step s's gradient and apply kernels run on the main stream
@@ -233,8 +239,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.cntV = e->cntV_[k];
     a.rankU = e->rankU_[k];
     a.rankV = e->rankV_[k];
-    a.offU = e->offU;
-    a.offV = e->offV;
+    a.offU = e->offU_[k];
+    a.offV = e->offV_[k];
     a.slotG = e->slotG;
     a.slot_max = e->slot_max;
     a.loss_partial = e->loss_partial;
@@ -333,43 +339,40 @@ int begin_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
 // Adagrad), duplicate apply (+ CML clip).  With `next`, the apply launch also
 // draws and counts the next step's batch (launch_apply_prep).  Loss added to
 // *loss_acc.
-int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
-                const StepArgs* next) {
+// slot pass arguments of the step in buffer set k (counts complete)
+SlotArgs slot_args(cf_engine* e, const StepArgs& a, int k) {
     const cf_config& c = e->cfg;
-    {
-        SlotArgs sa{};
-        sa.n_users = c.n_users;
-        sa.n_items = c.n_items;
-        sa.count_users = a.count_users;
-        sa.count_items = a.count_items;
-        sa.slot_max = e->slot_max;
-        sa.cntU = a.cntU;
-        sa.cntV = a.cntV;
-        sa.offU = e->offU;
-        sa.offV = e->offV;
-        sa.dup = e->dup;
-        sa.status = e->status + (size_t)kSlotMaxBlocks * e->status_par;
-        sa.status_next = e->status + (size_t)kSlotMaxBlocks * (e->status_par ^ 1);
-        sa.ctl = e->ctl;
-        e->status_par ^= 1;
-        ProfScope pr(e, CF_K_SLOT);
-        CF_HIP(launch_slots(sa, e->stream));
-    }
-    {
-        ProfScope ps(e, CF_K_STEP);
-        CF_HIP(launch_grad(a, e->stream));
-    }
+    SlotArgs sa{};
+    sa.n_users = c.n_users;
+    sa.n_items = c.n_items;
+    sa.count_users = a.count_users;
+    sa.count_items = a.count_items;
+    sa.slot_max = e->slot_max;
+    sa.cntU = a.cntU;
+    sa.cntV = a.cntV;
+    sa.offU = e->offU_[k];
+    sa.offV = e->offV_[k];
+    sa.dup = e->dup_[k];
+    sa.status = e->status + (size_t)kSlotMaxBlocks * e->status_par;
+    sa.status_next = e->status + (size_t)kSlotMaxBlocks * (e->status_par ^ 1);
+    sa.ctl = e->ctl_[k];
+    e->status_par ^= 1;
+    return sa;
+}
+
+ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc) {
+    const cf_config& c = e->cfg;
     ApplyArgs p{};
     p.d = c.n_factors;
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
     p.clip = c.model == CF_CML ? 1 : 0;
     p.slot_max = e->slot_max;
-    p.ctl = e->ctl;
-    p.dup = e->dup;
+    p.ctl = e->ctl_[k];
+    p.dup = e->dup_[k];
     p.n_users = c.n_users;
-    p.offU = e->offU;
-    p.offV = e->offV;
+    p.offU = e->offU_[k];
+    p.offV = e->offV_[k];
     p.slotG = e->slotG;
     p.cntU = e->cntU_[k];
     p.cntV = e->cntV_[k];
@@ -385,14 +388,12 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
     p.loss_partial = e->loss_partial;
     p.n_partial = grad_blocks(a);
     p.loss_acc = loss_acc;
-    if (next) {
-        ProfScope ps(e, CF_K_APPLY_PREP);
-        CF_HIP(launch_apply_prep(p, *next, e->stream));
-    } else {
-        ProfScope ps(e, CF_K_APPLY);
-        CF_HIP(launch_apply(p, e->stream));
-    }
-    if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
+    return p;
+}
+
+// CML: the full-table clip pending after step 1 / a table upload
+int pending_clips(cf_engine* e) {
+    const cf_config& c = e->cfg;
     if (e->need_clip_U) {
         ProfScope ps(e, CF_K_CLIP);
         CF_HIP(launch_clip_full(e->U, c.n_users, c.n_factors, c.clip_norm, e->stream));
@@ -404,6 +405,29 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
         e->need_clip_V = false;
     }
     return CF_OK;
+}
+
+int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
+                const StepArgs* next) {
+    {
+        SlotArgs sa = slot_args(e, a, k);
+        ProfScope pr(e, CF_K_SLOT);
+        CF_HIP(launch_slots(sa, e->stream));
+    }
+    {
+        ProfScope ps(e, CF_K_STEP);
+        CF_HIP(launch_grad(a, e->stream));
+    }
+    ApplyArgs p = apply_args(e, a, B, k, loss_acc);
+    if (next) {
+        ProfScope ps(e, CF_K_APPLY_PREP);
+        CF_HIP(launch_apply_prep(p, *next, e->stream));
+    } else {
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
+    return pending_clips(e);
 }
 
 // One step, host-fed (pairs != null) or from the device sampler.  With
@@ -435,6 +459,42 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
     if (e->prep_side) CF_HIP(hipStreamWaitEvent(e->stream, e->apply_done[k], 0));
     StepArgs a;
     CF_TRY(begin_step(e, B, nullptr, nullptr, nullptr, k, e->stream, &a));
+    if (e->pipeline == 2) {
+        // two launches per step: grad(s) | draw(s+1), then apply(s) | slots(s+1)
+        {
+            SlotArgs sa = slot_args(e, a, k);
+            ProfScope pr(e, CF_K_SLOT);
+            CF_HIP(launch_slots(sa, e->stream));
+        }
+        for (int s = 0; s < n; ++s) {
+            StepArgs nx{};
+            const bool more = s + 1 < n;
+            if (more) {
+                nx = base_step_args(e, B, k ^ 1);
+                CF_TRY(sampler_args(e, B, &nx));
+            }
+            {
+                ProfScope ps(e, more ? CF_K_GRAD_PREP : CF_K_STEP);
+                CF_HIP(launch_grad(a, e->stream, more ? &nx : nullptr));
+            }
+            ApplyArgs p = apply_args(e, a, B, k, loss_acc);
+            if (more) {
+                SlotArgs sa = slot_args(e, nx, k ^ 1);
+                ProfScope ps(e, CF_K_APPLY_SLOT);
+                CF_HIP(launch_apply_slots(p, sa, e->stream));
+            } else {
+                ProfScope ps(e, CF_K_APPLY);
+                CF_HIP(launch_apply(p, e->stream));
+            }
+            CF_TRY(pending_clips(e));
+            a = nx;
+            k ^= 1;
+        }
+        if (e->prep_side)
+            for (int q = 0; q < 2; ++q) CF_HIP(hipEventRecord(e->apply_done[q], e->stream));
+        e->set = k;
+        return CF_OK;
+    }
     for (int s = 0; s < n; ++s) {
         StepArgs nx{};
         const bool more = s + 1 < n;
@@ -627,10 +687,12 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
         (r = dalloc(&e->cntU_[0], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[0], (size_t)c.n_items)) ||
         (r = dalloc(&e->cntU_[1], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[1], (size_t)c.n_items)) ||
-        (r = dalloc(&e->offU, (size_t)c.n_users)) || (r = dalloc(&e->offV, (size_t)c.n_items)) ||
-        (r = dalloc(&e->dup, (size_t)(c.n_users + c.n_items))) ||
+        (r = dalloc(&e->offU_[0], (size_t)c.n_users)) || (r = dalloc(&e->offV_[0], (size_t)c.n_items)) ||
+        (r = dalloc(&e->offU_[1], (size_t)c.n_users)) || (r = dalloc(&e->offV_[1], (size_t)c.n_items)) ||
+        (r = dalloc(&e->dup_[0], (size_t)(c.n_users + c.n_items))) ||
+        (r = dalloc(&e->dup_[1], (size_t)(c.n_users + c.n_items))) ||
         (r = dalloc(&e->status, 2 * (size_t)kSlotMaxBlocks)) ||
-        (r = dalloc(&e->ctl, 4)) || (r = dalloc(&e->loss, 2)))
+        (r = dalloc(&e->ctl_[0], 4)) || (r = dalloc(&e->ctl_[1], 4)) || (r = dalloc(&e->loss, 2)))
         return bail(r);
     if (c.model == CF_GBPR) {
         if ((r = dalloc(&e->b, (size_t)c.n_items)) || (r = dalloc(&e->Ab, (size_t)c.n_items)) ||
@@ -650,9 +712,12 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         hipMemsetAsync(e->cntV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offU, 0, (size_t)c.n_users * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offV, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->ctl, 0, 4 * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offU_[0], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->offV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->ctl_[0], 0, 4 * 4, s) != hipSuccess ||
+        hipMemsetAsync(e->ctl_[1], 0, 4 * 4, s) != hipSuccess ||
         hipMemsetAsync(e->status, 0, 2 * kSlotMaxBlocks * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
         return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
@@ -688,11 +753,12 @@ int cf_destroy(cf_engine* e) {
     for (int k = 0; k < 2; ++k) {
         dfree(e->cntU_[k]); dfree(e->cntV_[k]); dfree(e->occU_[k]); dfree(e->occV_[k]);
         dfree(e->rankU_[k]); dfree(e->rankV_[k]);
+        dfree(e->offU_[k]); dfree(e->offV_[k]); dfree(e->dup_[k]); dfree(e->ctl_[k]);
         if (e->prep_done[k]) (void)hipEventDestroy(e->prep_done[k]);
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
-    dfree(e->offU); dfree(e->offV); dfree(e->dup); dfree(e->status); dfree(e->ctl); dfree(e->slotG);
+    dfree(e->status); dfree(e->slotG);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
@@ -728,6 +794,7 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     const cf_config& c = e->cfg;
     if (!indptr || (nnz > 0 && !indices)) return fail(CF_EINVAL, "null CSR");
     if (nnz < 1) return fail(CF_EINVAL, "no interactions");
+    if (nnz > INT32_MAX) return fail(CF_EINVAL, "nnz must be < 2^31 (int32 row offsets in the pair records)");
     if (indptr[0] != 0 || indptr[c.n_users] != nnz) return fail(CF_EINVAL, "indptr does not span nnz");
     for (int64_t u = 0; u < c.n_users; ++u) {
         const int64_t rb = indptr[u], re = indptr[u + 1];
@@ -1044,7 +1111,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "pipeline") {
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "pipeline must be 0 or 1");
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "pipeline must be 0, 1 or 2");
         e->pipeline = (int)value;
         return CF_OK;
     }

@@ -57,7 +57,7 @@ struct StepArgs {
     uint64_t rng_key;    // per-epoch draw key
     PermKey perm;
     // graph
-    const int2* __restrict__ pairs;         // [nnz] (u,i), CSR order
+    const int4* __restrict__ pairs;         // [nnz] (u, i, row start, row length), CSR order
     const int64_t* __restrict__ indptr;     // [n_users+1]
     const int32_t* __restrict__ indices;    // [nnz] sorted per user
     const int64_t* __restrict__ indptr_t;   // [n_items+1] (GBPR)
@@ -189,7 +189,9 @@ struct TopkArgs {
 
 // ---- host launchers (cf_kernels.hip / cf_eval.hip) -------------------------
 hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + count
-hipError_t launch_grad(const StepArgs& a, hipStream_t s);   // gather, loss, grads, apply
+// gather, loss, grads, singleton apply; with `next`, the same launch also
+// draws and counts the next step's batch (other buffer set)
+hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
 // blocks (= loss partials) of the grad launch for this step shape
 int grad_blocks(const StepArgs& a);
 int grad_blocks_max(int B);  // upper bound over every grad variant
@@ -198,13 +200,15 @@ hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid = nullptr);
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 // apply of step s and prep of step s+1 in one launch (device-sampler pipeline)
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& next, hipStream_t s);
+// apply of step s and the slot pass of step s+1 in one launch
+hipError_t launch_apply_slots(const ApplyArgs& p, SlotArgs next, hipStream_t s);
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);
 hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int truncated,
                               uint64_t seed, hipStream_t s);
 hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
-                              int2* pairs, hipStream_t s);
+                              int4* pairs, hipStream_t s);
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);
 hipError_t launch_topk(const TopkArgs& a, int n_users, hipStream_t s);
 hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s);

@@ -40,9 +40,93 @@
 namespace cfk {
 
 // ---------------------------------------------------------------------------
-// 16-lane group helpers: element e of a row lives in lane (e % 16), slot
-// e / 16, so one load instruction reads 64 contiguous bytes of four rows.
+// 16-lane group helpers.  A row of d floats is held as EPL slots per lane.
+// Rows that fill every slot (d == 16*EPL: d = 16, 32, 64, 128, 256) use the
+// vector layout: lane gl holds VW = min(EPL, 4) contiguous floats of each
+// 64*VW-byte stripe, so one dwordx{VW} instruction moves a whole stripe of
+// four rows (one per group of the wave) -- a 256-B row (d = 64) is one
+// 16-B-per-lane access.  Other d use the scalar layout: element s*16 + gl,
+// masked by e < d.  Arithmetic is layout-blind (slot-wise, with group
+// reductions); memory stays row-major either way.
 // ---------------------------------------------------------------------------
+// The vector layout measured no faster on the gather (46.0 vs 44.9 us, cfg2
+// grad without atomics) and its float atomics touch four 64-B segments per
+// row-stripe instead of one (grad 105 vs 50 us), so the scalar layout is the
+// default; -DCF_VEC_ROWS=1 builds the vector layout for experiments.
+#ifndef CF_VEC_ROWS
+#define CF_VEC_ROWS 0
+#endif
+template <int EPL>
+struct Lay {
+    static constexpr int VW = CF_VEC_ROWS ? (EPL >= 4 ? 4 : EPL) : 1;
+    static constexpr int NQ = EPL / VW;  // stripes per row
+};
+
+// element index of slot s in lane gl (full rows: vector layout)
+template <int EPL>
+__device__ __forceinline__ int elem_of(int s, int gl, bool full) {
+    constexpr int VW = Lay<EPL>::VW;
+    return full ? (s / VW) * (kGL * VW) + gl * VW + (s % VW) : s * kGL + gl;
+}
+
+template <int EPL>
+__device__ __forceinline__ void row_ld(const float* __restrict__ row, int d, int gl, float fill,
+                                       float (&x)[EPL]) {
+    constexpr int VW = Lay<EPL>::VW;
+    if (CF_VEC_ROWS && d == kGL * EPL) {
+#pragma unroll
+        for (int q = 0; q < Lay<EPL>::NQ; ++q) {
+            const float* p = row + q * (kGL * VW) + gl * VW;
+            if constexpr (VW == 4) {
+                const float4 v = *reinterpret_cast<const float4*>(p);
+                x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+            } else if constexpr (VW == 2) {
+                const float2 v = *reinterpret_cast<const float2*>(p);
+                x[2 * q] = v.x; x[2 * q + 1] = v.y;
+            } else {
+                x[q] = p[0];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            const int e = s * kGL + gl;
+            x[s] = (e < d) ? row[e] : fill;
+        }
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void row_st(float* __restrict__ row, int d, int gl, const float (&x)[EPL]) {
+    constexpr int VW = Lay<EPL>::VW;
+    if (CF_VEC_ROWS && d == kGL * EPL) {
+#pragma unroll
+        for (int q = 0; q < Lay<EPL>::NQ; ++q) {
+            float* p = row + q * (kGL * VW) + gl * VW;
+            if constexpr (VW == 4) {
+                *reinterpret_cast<float4*>(p) = make_float4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+            } else if constexpr (VW == 2) {
+                *reinterpret_cast<float2*>(p) = make_float2(x[2 * q], x[2 * q + 1]);
+            } else {
+                p[0] = x[q];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            const int e = s * kGL + gl;
+            if (e < d) row[e] = x[s];
+        }
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void row_zero(float* __restrict__ row, int d, int gl) {
+    float z[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) z[s] = 0.f;
+    row_st<EPL>(row, d, gl, z);
+}
 __device__ __forceinline__ float gsum(float v) {
     v += __shfl_xor(v, 8, 64);
     v += __shfl_xor(v, 4, 64);
@@ -62,21 +146,17 @@ __device__ __forceinline__ uint32_t gor(uint32_t v) {
 template <int EPL>
 __device__ __forceinline__ void gload(const float* __restrict__ X, int64_t r, int d, int gl,
                                       float (&x)[EPL]) {
-    const float* row = X + r * (int64_t)d;
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
-        x[s] = (e < d) ? row[e] : 0.f;
-    }
+    row_ld<EPL>(X + r * (int64_t)d, d, gl, 0.f, x);
 }
 
 template <int EPL>
 __device__ __forceinline__ void gatomic(float* __restrict__ G, int64_t r, int d, int gl,
                                         const float (&g)[EPL]) {
     float* row = G + r * (int64_t)d;
+    const bool full = CF_VEC_ROWS && d == kGL * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
+        const int e = elem_of<EPL>(s, gl, full);
         if (e < d) unsafeAtomicAdd(row + e, g[s]);
     }
 }
@@ -98,11 +178,7 @@ __device__ __forceinline__ void gapply(float* __restrict__ X, float* __restrict_
     float* xr = X + r * (int64_t)d;
     float* ar = A + r * (int64_t)d;
     float acc[EPL], x[EPL];
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
-        acc[s] = (e < d) ? ar[e] : 1.f;
-    }
+    row_ld<EPL>(ar, d, gl, 1.f, acc);
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         acc[s] = fmaf(g[s], g[s], acc[s]);
@@ -114,25 +190,14 @@ __device__ __forceinline__ void gapply(float* __restrict__ X, float* __restrict_
 #pragma unroll
         for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
     }
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
-        if (e < d) {
-            xr[e] = x[s];
-            ar[e] = acc[s];
-        }
-    }
+    row_st<EPL>(xr, d, gl, x);
+    row_st<EPL>(ar, d, gl, acc);
 }
 
 template <int EPL>
 __device__ __forceinline__ void gstore(float* __restrict__ S, int64_t r, int d, int gl,
                                        const float (&g)[EPL]) {
-    float* row = S + r * (int64_t)d;
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
-        if (e < d) row[e] = g[s];
-    }
+    row_st<EPL>(S + r * (int64_t)d, d, gl, g);
 }
 
 // slot row of one occurrence of a duplicated row: rows with 2..slot_max
@@ -202,12 +267,14 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
     if (a.sample) {
         const uint64_t slot = a.slot_base + (uint64_t)p;
         const uint64_t idx = permute(slot, a.perm);   // shuffled pair order (sampler_ranking.py:24)
-        const int2 pr = a.pairs[idx];
+        // one 16-B record per pair carries the user's CSR extent, so the row
+        // scan does not wait on a dependent indptr load
+        const int4 pr = a.pairs[idx];
         u = pr.x;
         i = pr.y;
         key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
-        rb = a.indptr[u];
-        re = a.indptr[u + 1];
+        rb = (int64_t)(uint32_t)pr.z;
+        re = rb + pr.w;
     } else {
         u = a.occU[p];
         i = a.occV[p];
@@ -264,7 +331,13 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             a.occV[p] = i;
         }
         if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
+#if defined(CF_EXP_NORET)
+        if (a.count_items) { atomicAdd(&a.cntV[i], 1); a.rankV[p] = 0; }
+#elif defined(CF_EXP_NO_ICOUNT)
+        if (a.count_items) a.rankV[p] = 0;
+#else
         if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
+#endif
     }
 }
 
@@ -320,7 +393,7 @@ struct NegRows {
 };
 
 template <int MODEL, int EPL, int WT>
-__global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
+__device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
     __shared__ double s_loss[kGroupsPerBlock];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
@@ -332,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
     float sq = 0.f;      // lane-partial sum of squares for the L2 term
 
     for (int k = 0; k < kPairsPerGroup; ++k) {
-        const int p = (blockIdx.x * kPairsPerGroup + k) * kGroupsPerBlock + grp;
+        const int p = (block * kPairsPerGroup + k) * kGroupsPerBlock + grp;
         if (p >= B) break;  // group-uniform
         const int u = a.occU[p];
         const int i = a.occV[p];
@@ -529,8 +602,30 @@ __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a) {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[k];
-        a.loss_partial[blockIdx.x] = t;
+        a.loss_partial[block] = t;
     }
+}
+
+// Horizontal fusion on the device-sampler pipeline: the grid carries the ng
+// gradient blocks of step s and the np draw + count blocks of step s+1
+// (independent work: the other buffer set), spread evenly over the block ids
+// so that the latency-bound draw fills the gaps of the gather.  np == 0 is the
+// plain gradient launch.
+__device__ __forceinline__ bool minor_block(int b, int nmajor, int nminor, int& idx) {
+    const int64_t tot = (int64_t)nmajor + nminor;
+    const int lo = (int)(((int64_t)b * nminor) / tot);
+    const int hi = (int)(((int64_t)(b + 1) * nminor) / tot);
+    idx = (hi > lo) ? lo : b - lo;
+    return hi > lo;
+}
+
+template <int MODEL, int EPL, int WT>
+__global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a, StepArgs nx, int ng, int np) {
+    int idx;
+    if (minor_block(blockIdx.x, ng, np, idx))
+        prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
+    else
+        grad_body<MODEL, EPL, WT>(a, idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -551,14 +646,7 @@ __device__ __forceinline__ void gload_acc(const float* __restrict__ A, int64_t r
 #ifdef CF_EXP_NO_ACC
     want = false;
 #endif
-    if (want) {
-        const float* row = A + r * (int64_t)d;
-#pragma unroll
-        for (int s = 0; s < EPL; ++s) {
-            const int e = s * kGL + gl;
-            if (e < d) acc[s] = row[e];
-        }
-    }
+    if (want) row_ld<EPL>(A + r * (int64_t)d, d, gl, 1.f, acc);
 }
 
 // SparseApplyAdagrad with the accumulator row already in registers
@@ -579,16 +667,8 @@ __device__ __forceinline__ void gapply_pre(float* __restrict__ X, float* __restr
 #pragma unroll
         for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
     }
-    float* xr = X + r * (int64_t)d;
-    float* ar = A + r * (int64_t)d;
-#pragma unroll
-    for (int s = 0; s < EPL; ++s) {
-        const int e = s * kGL + gl;
-        if (e < d) {
-            xr[e] = x[s];
-            ar[e] = acc[s];
-        }
-    }
+    row_st<EPL>(X + r * (int64_t)d, d, gl, x);
+    row_st<EPL>(A + r * (int64_t)d, d, gl, acc);
 }
 
 template <int EPL>
@@ -829,7 +909,7 @@ struct PairRows {
 };
 
 template <int MODEL, int EPL, int WT, int P>
-__global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a) {
+__device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     __shared__ double s_loss[kGroupsPerBlock];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
@@ -840,7 +920,7 @@ __global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a) {
     bool ok[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        pp[k] = (blockIdx.x * P + k) * kGroupsPerBlock + grp;
+        pp[k] = (block * P + k) * kGroupsPerBlock + grp;
         ok[k] = pp[k] < a.B;
     }
 #pragma unroll
@@ -864,8 +944,17 @@ __global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a) {
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[k];
-        a.loss_partial[blockIdx.x] = t;
+        a.loss_partial[block] = t;
     }
+}
+
+template <int MODEL, int EPL, int WT, int P>
+__global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
+    int idx;
+    if (minor_block(blockIdx.x, ng, np, idx))
+        prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
+    else
+        grad_fast_body<MODEL, EPL, WT, P>(a, idx);
 }
 
 // ---------------------------------------------------------------------------
@@ -891,13 +980,12 @@ __device__ __forceinline__ void slot_counts(const SlotArgs& a, const int32_t* cn
     }
 }
 
-__global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
+__device__ __forceinline__ void slot_body(const SlotArgs& a, int blk, int nblocks) {
     __shared__ int s_wd[kWavesPerBlock], s_ws[kWavesPerBlock];
     __shared__ int s_base[2];
-    if (blockIdx.x == 0)
+    if (blk == 0)
         for (int k = threadIdx.x; k < kSlotMaxBlocks; k += kBlock)
             __hip_atomic_store(a.status_next + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int blk = blockIdx.x;
     const bool isU = blk < a.blocksU;
     const int64_t n = isU ? a.n_users : a.n_items;
     const bool counted = isU ? a.count_users != 0 : a.count_items != 0;
@@ -967,7 +1055,7 @@ __global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
         }
         s_base[0] = x;
         s_base[1] = y;
-        if (blk == (int)gridDim.x - 1) {
+        if (blk == nblocks - 1) {
             a.ctl[0] = y + ts;
             a.ctl[1] = x + td;
         }
@@ -994,6 +1082,10 @@ __global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
             }
         }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
+    slot_body(a, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1035,13 +1127,14 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         if (s0 >= 0) {
 #pragma unroll
             for (int s = 0; s < EPL; ++s) g[s] = 0.f;
-            for (int t0 = 0; t0 < c; t0 += 4) {  // 4 slot rows in flight, summed in rank order
-                float h[4][EPL];
+            constexpr int NF = 4;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
+            for (int t0 = 0; t0 < c; t0 += NF) {
+                float h[NF][EPL];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < NF; ++q)
                     if (t0 + q < c) gload<EPL>(a.slotG, s0 + t0 + q, a.d, gl, h[q]);
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < NF; ++q)
                     if (t0 + q < c) {
 #pragma unroll
                         for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
@@ -1049,12 +1142,7 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
             }
         } else {
             gload<EPL>(G, r, a.d, gl, g);
-            float* gr = G + r * a.d;
-#pragma unroll
-            for (int s = 0; s < EPL; ++s) {
-                const int e = s * kGL + gl;
-                if (e < a.d) gr[e] = 0.f;
-            }
+            row_zero<EPL>(G + r * a.d, a.d, gl);
         }
         gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) {
@@ -1086,6 +1174,18 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
         prep_body<MODEL>(a, blockIdx.x - napply);
 }
 
+// the slot pass of step s+1 (blocks [0, nslot): its look-back only waits on
+// lower slot blocks, all dispatched earlier) beside the apply of step s (the
+// rest).  Needs step s+1's counts complete, i.e. its draw ran in the gradient
+// launch of step s; the slot ranges / duplicate list are double-buffered.
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void apply_slot_kernel(ApplyArgs p, SlotArgs sa, int nslot) {
+    if ((int)blockIdx.x < nslot)
+        slot_body(sa, blockIdx.x, nslot);
+    else
+        apply_body<EPL>(p, blockIdx.x - nslot, gridDim.x - nslot);
+}
+
 // ---------------------------------------------------------------------------
 // dense item apply (multi-rank: after the all-reduce every replica applies the
 // identical update; a row whose summed gradient is all-zero is an exact no-op
@@ -1105,12 +1205,7 @@ __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
         if (gor(nz) == 0u) continue;  // group-uniform
         float x[EPL];
         gload<EPL>(a.X, r, a.d, gl, x);
-        float* gr = a.G + r * (int64_t)a.d;
-#pragma unroll
-        for (int s = 0; s < EPL; ++s) {
-            const int e = s * kGL + gl;
-            if (e < a.d) gr[e] = 0.f;
-        }
+        row_zero<EPL>(a.G + r * (int64_t)a.d, a.d, gl);
         gapply<EPL>(a.X, a.A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
     }
     if (a.b != nullptr) {
@@ -1139,12 +1234,9 @@ __global__ __launch_bounds__(kBlock) void clip_full_kernel(float* __restrict__ X
         gload<EPL>(X, r, d, gl, x);
         const float n = sqrtf(gdot<EPL>(x, x));
         const float den = fmaxf(n, c);
-        float* xr = X + r * (int64_t)d;
 #pragma unroll
-        for (int s = 0; s < EPL; ++s) {
-            const int e = s * kGL + gl;
-            if (e < d) xr[e] = (x[s] * c) / den;
-        }
+        for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
+        row_st<EPL>(X + r * (int64_t)d, d, gl, x);
     }
 }
 
@@ -1173,12 +1265,13 @@ __global__ void fill_kernel(float* __restrict__ X, int64_t n, float v) {
 
 __global__ void build_pairs_kernel(const int64_t* __restrict__ indptr,
                                    const int32_t* __restrict__ indices, int64_t n_users,
-                                   int2* __restrict__ pairs) {
+                                   int4* __restrict__ pairs) {
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nt = (int64_t)gridDim.x * blockDim.x;
     for (int64_t u = t0; u < n_users; u += nt)
         for (int64_t k = indptr[u]; k < indptr[u + 1]; ++k)
-            pairs[k] = make_int2((int)u, indices[k]);
+            pairs[k] = make_int4((int)u, indices[k], (int)(uint32_t)indptr[u],
+                                 (int)(indptr[u + 1] - indptr[u]));
 }
 
 // ---------------------------------------------------------------------------
@@ -1223,29 +1316,36 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+static int prep_blocks(const StepArgs* nx) {
+    return (nx && nx->B > 0) ? (nx->B + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
+}
+
 template <int MODEL, int WT>
-static hipError_t launch_grad_w(const StepArgs& a, hipStream_t s) {
-    const dim3 grid((a.B + kPairsPerBlock - 1) / kPairsPerBlock), block(kBlock);
+static hipError_t launch_grad_w(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
+    const int ng = (a.B + kPairsPerBlock - 1) / kPairsPerBlock, np = prep_blocks(nx);
+    const StepArgs n = nx ? *nx : a;
+    const dim3 grid(ng + np), block(kBlock);
     switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4, WT>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8, WT>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16, WT>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT>), grid, block, 0, s, a, n, ng, np); break;
+        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT>), grid, block, 0, s, a, n, ng, np); break;
+        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4, WT>), grid, block, 0, s, a, n, ng, np); break;
+        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8, WT>), grid, block, 0, s, a, n, ng, np); break;
+        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16, WT>), grid, block, 0, s, a, n, ng, np); break;
     }
     return hipGetLastError();
 }
 
 template <int MODEL, int WT, int P>
-static hipError_t launch_grad_fast(const StepArgs& a, hipStream_t s) {
+static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     // the grid must match grad_blocks(): P * kGroupsPerBlock pairs per block
-    const int blocks = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock);
-    const dim3 grid(blocks), block(kBlock);
+    const int ng = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock), np = prep_blocks(nx);
+    const StepArgs n = nx ? *nx : a;
+    const dim3 grid(ng + np), block(kBlock);
     switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P>), grid, block, 0, s, a, n, ng, np); break;
+        case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P>), grid, block, 0, s, a, n, ng, np); break;
+        case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P>), grid, block, 0, s, a, n, ng, np); break;
+        default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P>), grid, block, 0, s, a, n, ng, np); break;
     }
     return hipGetLastError();
 }
@@ -1253,36 +1353,42 @@ static hipError_t launch_grad_fast(const StepArgs& a, hipStream_t s) {
 // W = 1 (BPRMF driver) and W = 5 (AMF / CML / GBPR drivers) with G <= 1 and
 // d <= 128 take the phased fast path; anything else the generic kernel
 template <int MODEL>
-static hipError_t launch_grad_m(const StepArgs& a, hipStream_t s) {
+static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     const int e = epl_for(a.d);
     const int fw = fast_w(a);
-    if (fw == 1) return launch_grad_fast<MODEL, 1, CF_FAST_PAIRS_W1>(a, s);
-    if (fw == 5) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_W5>(a, s);
-    if (a.W == 1) return launch_grad_w<MODEL, 1>(a, s);
-    if (a.W == 5 && e <= 8) return launch_grad_w<MODEL, 5>(a, s);
-    return launch_grad_w<MODEL, 0>(a, s);
+    if (fw == 1) return launch_grad_fast<MODEL, 1, CF_FAST_PAIRS_W1>(a, nx, s);
+    if (fw == 5) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_W5>(a, nx, s);
+    if (a.W == 1) return launch_grad_w<MODEL, 1>(a, nx, s);
+    if (a.W == 5 && e <= 8) return launch_grad_w<MODEL, 5>(a, nx, s);
+    return launch_grad_w<MODEL, 0>(a, nx, s);
 }
 
-hipError_t launch_grad(const StepArgs& a, hipStream_t s) {
-    if (a.B <= 0) return hipSuccess;
+hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
+    if (a.B <= 0) return next ? launch_prep(*next, s) : hipSuccess;
+    if (next && next->model != a.model) return hipErrorInvalidValue;
     switch (a.model) {
-        case BPR: return launch_grad_m<BPR>(a, s);
-        case GBPR: return launch_grad_m<GBPR>(a, s);
-        case CML: return launch_grad_m<CML>(a, s);
-        default: return launch_grad_m<AMF>(a, s);
+        case BPR: return launch_grad_m<BPR>(a, next, s);
+        case GBPR: return launch_grad_m<GBPR>(a, next, s);
+        case CML: return launch_grad_m<CML>(a, next, s);
+        default: return launch_grad_m<AMF>(a, next, s);
     }
 }
 
-hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid) {
-    // rows per block: the smallest multiple of one chunk (kBlock * kSlotRPT)
-    // that keeps the grid within kSlotMaxBlocks
+// rows per block: the smallest multiple of one chunk (kBlock * kSlotRPT) that
+// keeps the grid within kSlotMaxBlocks; returns the grid (0 on overflow)
+static int slot_shape(SlotArgs& a) {
     const int64_t chunk = (int64_t)kBlock * kSlotRPT;
     int64_t rpb = chunk;
     while ((a.n_users + rpb - 1) / rpb + (a.n_items + rpb - 1) / rpb > kSlotMaxBlocks) rpb += chunk;
-    if (rpb > (int64_t)1 << 30) return hipErrorInvalidValue;
+    if (rpb > (int64_t)1 << 30) return 0;
     a.rows_per_block = (int)rpb;
     a.blocksU = (int)((a.n_users + rpb - 1) / rpb);
-    const int blocks = a.blocksU + (int)((a.n_items + rpb - 1) / rpb);
+    return a.blocksU + (int)((a.n_items + rpb - 1) / rpb);
+}
+
+hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid) {
+    const int blocks = slot_shape(a);
+    if (blocks == 0) return hipErrorInvalidValue;
     if (grid) *grid = blocks;
     hipLaunchKernelGGL(slot_kernel, dim3(blocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
@@ -1325,6 +1431,20 @@ static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hip
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return launch_apply(p, s);
     return a.model == GBPR ? launch_apply_prep_m<GBPR>(p, a, s) : launch_apply_prep_m<BPR>(p, a, s);
+}
+
+hipError_t launch_apply_slots(const ApplyArgs& p, SlotArgs sa, hipStream_t s) {
+    const int ns = slot_shape(sa);
+    if (ns == 0) return hipErrorInvalidValue;
+    const dim3 grid(ns + apply_grid(p)), block(kBlock);
+    switch (epl_for(p.d)) {
+        case 1: hipLaunchKernelGGL(apply_slot_kernel<1>, grid, block, 0, s, p, sa, ns); break;
+        case 2: hipLaunchKernelGGL(apply_slot_kernel<2>, grid, block, 0, s, p, sa, ns); break;
+        case 4: hipLaunchKernelGGL(apply_slot_kernel<4>, grid, block, 0, s, p, sa, ns); break;
+        case 8: hipLaunchKernelGGL(apply_slot_kernel<8>, grid, block, 0, s, p, sa, ns); break;
+        default: hipLaunchKernelGGL(apply_slot_kernel<16>, grid, block, 0, s, p, sa, ns); break;
+    }
+    return hipGetLastError();
 }
 
 static int row_grid(int64_t n_rows) {
@@ -1380,7 +1500,7 @@ hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s) {
 }
 
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
-                              int2* pairs, hipStream_t s) {
+                              int4* pairs, hipStream_t s) {
     if (n_users <= 0) return hipSuccess;
     hipLaunchKernelGGL(build_pairs_kernel, dim3(grid_for(n_users)), dim3(kBlock), 0, s, indptr,
                        indices, n_users, pairs);

@@ -71,7 +71,9 @@ enum cf_kernel_id {
     CF_K_TOPK = 6,       /* masked per-user top-k                             */
     CF_K_SLOT = 7,       /* duplicate-row list + slot ranges (store-and-sum)   */
     CF_K_APPLY_PREP = 8, /* apply of step s fused with the draw of step s+1    */
-    CF_K_COUNT = 9
+    CF_K_GRAD_PREP = 9,  /* gradient of step s fused with the draw of step s+1 */
+    CF_K_APPLY_SLOT = 10,/* apply of step s fused with the slot pass of s+1    */
+    CF_K_COUNT = 11
 };
 
 /*
@@ -244,9 +246,12 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                occurring more often use float atomics (default 32; 1 = atomics
  *                for every duplicated row).  Same arithmetic up to fp32
  *                summation order.
- *   "pipeline"   1 = cf_train_steps launches the duplicate apply of step s and
- *                the draw + count of step s+1 as one kernel (default); 0 = one
- *                step at a time.  Same results.
+ *   "pipeline"   how cf_train_steps overlaps consecutive steps (same results):
+ *                1 = the duplicate apply of step s with the draw + count of
+ *                step s+1, three launches per step (default); 2 = two
+ *                launches, the gradient of step s with the draw + count of
+ *                step s+1, then the duplicate apply of step s with the slot
+ *                pass of step s+1; 0 = one step at a time, four launches.
  *   "profile_mask" bit k set = cf_profile_enable times kernel id k (default
  *                all): timing only the kernel of interest keeps the event
  *                pairs of the others out of a timed loop.
