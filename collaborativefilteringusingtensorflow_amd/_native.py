@@ -83,6 +83,13 @@ SIGNATURES = {
     "cf_step_local": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_items": (ctypes.c_int, [_P]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
+    "cf_set_shard": (ctypes.c_int, [_P, _I32, _I32, _PI64]),
+    "cf_set_group_source": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
+    "cf_bind_exchange": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P, _I64]),
+    "cf_xchg_begin": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32, _PI32]),
+    "cf_xchg_serve": (ctypes.c_int, [_P, _I64]),
+    "cf_xchg_grad": (ctypes.c_int, [_P]),
+    "cf_xchg_finish": (ctypes.c_int, [_P, _I64]),
     "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
     "cf_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, _I64]),
     "cf_profile_enable": (ctypes.c_int, [_P, _I32]),

@@ -119,6 +119,25 @@ struct cf_engine {
     int64_t epoch = 0, batch = 0;
     int sampler_B = 0;
 
+    // user sharding + GBPR group exchange (cf_set_shard / cf_bind_exchange /
+    // cf_xchg_*): this rank owns global users [shard_u0, shard_u1)
+    int world = 1, rank = 0;
+    int64_t shard_u0 = 0, shard_u1 = 0;
+    std::vector<int64_t> h_bounds;
+    int64_t* bounds = nullptr;       // [world + 1] device
+    bool group_source_global = false;
+    int32_t* xhist = nullptr;        // pack histogram [blocks][world]
+    size_t xhist_cap = 0;
+    int32_t* xcounts = nullptr;      // [world + 1] device
+    int32_t* h_xcounts = nullptr;    // pinned mirror
+    int32_t *x_send_ids = nullptr, *x_recv_ids = nullptr;             // bound (caller) buffers
+    float *x_rows = nullptr, *x_grads = nullptr, *x_serve_rows = nullptr, *x_serve_grads = nullptr;
+    int64_t x_send_cap = 0, x_recv_cap = 0;
+    int x_stage = 0;                 // 0 idle, 1 begun, 2 served, 3 grads done
+    StepArgs x_args{};
+    int x_set = 0;
+    int x_B = 0;
+
     // model state
     int phase = 0;
     bool need_clip_U = false, need_clip_V = false;
@@ -246,6 +265,10 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
     a.count_items = c.dense_item_apply ? 0 : 1;
+    a.shard_u0 = e->shard_u0;
+    a.shard_u1 = e->shard_u1;
+    a.xrows = e->x_rows;
+    a.xgrads = e->x_grads;
     return a;
 }
 
@@ -308,7 +331,15 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
             sv[B + (size_t)p * W + w] = j;
         }
         for (int k = 0; k < G; ++k) {
+            // group members are global user ids on a sharded engine; one
+            // owned by another rank is coded -1 - id (cf_xchg_begin)
             const int32_t g = groups[(size_t)p * G + k];
+            if (e->world > 1) {
+                if (g < 0 || g >= e->h_bounds[e->world]) return fail(CF_EINVAL, "group user out of range");
+                su[B + (size_t)p * G + k] =
+                    (g >= e->shard_u0 && g < e->shard_u1) ? (int32_t)(g - e->shard_u0) : -1 - g;
+                continue;
+            }
             if (g < 0 || g >= nu) return fail(CF_EINVAL, "group user out of range");
             su[B + (size_t)p * G + k] = g;
         }
@@ -541,6 +572,13 @@ int read_loss(cf_engine* e, int slot, double* out) {
     return CF_OK;
 }
 
+// a user-sharded GBPR engine steps only through the group exchange
+int check_not_xchg(cf_engine* e) {
+    if (e->cfg.model == CF_GBPR && e->world > 1)
+        return fail(CF_ESTATE, "user-sharded GBPR steps through cf_xchg_begin/serve/grad/finish");
+    return CF_OK;
+}
+
 int check_engine(cf_engine* e) {
     if (!e) return fail(CF_EINVAL, "null engine");
     return set_dev(e);
@@ -701,6 +739,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     }
     e->GV = e->GV_own;
     e->Gb = e->Gb_own;
+    e->shard_u1 = c.n_users;
     if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
     hipStream_t s = e->stream;
@@ -759,6 +798,8 @@ int cf_destroy(cf_engine* e) {
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
     dfree(e->status); dfree(e->slotG);
+    dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
+    if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
@@ -815,7 +856,7 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     CF_HIP(hipMemcpyAsync(e->indptr, indptr, ((size_t)c.n_users + 1) * 8, hipMemcpyHostToDevice, e->stream));
     CF_HIP(hipMemcpyAsync(e->indices, indices, (size_t)nnz * 4, hipMemcpyHostToDevice, e->stream));
     CF_HIP(launch_build_pairs(e->indptr, e->indices, c.n_users, e->pairs, e->stream));
-    if (c.model == CF_GBPR) {
+    if (c.model == CF_GBPR && !e->group_source_global) {
         // item -> users transpose (item_posUserList, sampler_gbpr.py:15)
         std::vector<int64_t> tp((size_t)c.n_items + 1, 0);
         for (int64_t k = 0; k < nnz; ++k) tp[(size_t)indices[k] + 1]++;
@@ -886,6 +927,7 @@ int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
 int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32_t* groups,
             int32_t B, double* loss_out) {
     CF_TRY(check_engine(e));
+    CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
     if (!pairs) return fail(CF_EINVAL, "host batch required (use cf_train_steps for the device sampler)");
     if (e->cfg.dense_item_apply && e->GV != e->GV_own)
@@ -899,6 +941,7 @@ int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32
 
 int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_out) {
     CF_TRY(check_engine(e));
+    CF_TRY(check_not_xchg(e));
     if (B < 1 || n_steps < 0) return fail(CF_EINVAL, "bad B / n_steps");
     if (e->cfg.dense_item_apply && e->GV != e->GV_own)
         return fail(CF_ESTATE, "item gradient is bound to an external buffer: use cf_step_local/cf_step_items");
@@ -942,7 +985,11 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
         pairs[2 * p] = hu[p];
         pairs[2 * p + 1] = hv[p];
         for (int w = 0; w < W; ++w) negs[(size_t)p * W + w] = hv[B + (size_t)p * W + w];
-        for (int k = 0; k < G; ++k) groups[(size_t)p * G + k] = hu[B + (size_t)p * G + k];
+        for (int k = 0; k < G; ++k) {
+            const int32_t g = hu[B + (size_t)p * G + k];
+            // sharded engine: group members as GLOBAL user ids
+            groups[(size_t)p * G + k] = e->world > 1 ? (g >= 0 ? (int32_t)(g + e->shard_u0) : -1 - g) : g;
+        }
     }
     return CF_OK;
 }
@@ -1001,6 +1048,7 @@ int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
                   const int32_t* groups) {
     CF_TRY(check_engine(e));
     if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_local needs dense_item_apply=1");
+    CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
     return run_step(e, B, pairs, negs, groups, e->loss);
 }
@@ -1009,6 +1057,178 @@ int cf_step_items(cf_engine* e) {
     CF_TRY(check_engine(e));
     if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_items needs dense_item_apply=1");
     return run_items_dense(e);
+}
+
+// ---- user sharding + GBPR group exchange ------------------------------------
+int cf_set_shard(cf_engine* e, int32_t world, int32_t rank, const int64_t* bounds) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (world < 1 || world > 64 || rank < 0 || rank >= world || !bounds)
+        return fail(CF_EINVAL, "bad world / rank / bounds");
+    if (bounds[0] != 0) return fail(CF_EINVAL, "bounds[0] must be 0");
+    for (int r = 0; r < world; ++r)
+        if (bounds[r + 1] < bounds[r]) return fail(CF_EINVAL, "bounds must be non-decreasing");
+    if (bounds[world] > INT32_MAX) return fail(CF_EINVAL, "global user ids must fit int32");
+    if (bounds[rank + 1] - bounds[rank] != c.n_users)
+        return fail(CF_EINVAL, "this rank's user range must hold exactly n_users users");
+    CF_HIP(hipStreamSynchronize(e->stream));
+    e->world = world;
+    e->rank = rank;
+    e->shard_u0 = bounds[rank];
+    e->shard_u1 = bounds[rank + 1];
+    e->h_bounds.assign(bounds, bounds + world + 1);
+    dfree(e->bounds);
+    dfree(e->xcounts);
+    CF_TRY(dalloc(&e->bounds, (size_t)world + 1));
+    CF_TRY(dalloc(&e->xcounts, (size_t)world + 1));
+    if (!e->h_xcounts)
+        CF_HIP(hipHostMalloc((void**)&e->h_xcounts, 65 * sizeof(int32_t), hipHostMallocDefault));
+    CF_HIP(hipMemcpy(e->bounds, bounds, ((size_t)world + 1) * 8, hipMemcpyHostToDevice));
+    return CF_OK;
+}
+
+int cf_set_group_source(cf_engine* e, const int64_t* indptr_t, const int32_t* indices_t, int64_t nnz) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (c.model != CF_GBPR) return fail(CF_EINVAL, "group sources exist only for GBPR");
+    if (e->world < 2) return fail(CF_ESTATE, "call cf_set_shard first (world > 1)");
+    if (!indptr_t || !indices_t || nnz < 1) return fail(CF_EINVAL, "null / empty item->user CSR");
+    if (indptr_t[0] != 0 || indptr_t[c.n_items] != nnz) return fail(CF_EINVAL, "indptr_t does not span nnz");
+    const int64_t nu = e->h_bounds[e->world];
+    for (int64_t i = 0; i < c.n_items; ++i)
+        if (indptr_t[i + 1] < indptr_t[i]) return fail(CF_EINVAL, "indptr_t not monotone");
+    for (int64_t k = 0; k < nnz; ++k)
+        if (indices_t[k] < 0 || indices_t[k] >= nu) return fail(CF_EINVAL, "user id out of range");
+    CF_HIP(hipStreamSynchronize(e->stream));
+    dfree(e->indptr_t);
+    dfree(e->indices_t);
+    CF_TRY(dalloc(&e->indptr_t, (size_t)c.n_items + 1));
+    CF_TRY(dalloc(&e->indices_t, (size_t)nnz));
+    CF_HIP(hipMemcpy(e->indptr_t, indptr_t, ((size_t)c.n_items + 1) * 8, hipMemcpyHostToDevice));
+    CF_HIP(hipMemcpy(e->indices_t, indices_t, (size_t)nnz * 4, hipMemcpyHostToDevice));
+    e->group_source_global = true;
+    return CF_OK;
+}
+
+static int check_device_ptr(const void* p, const char* what) {
+    hipPointerAttribute_t attr;
+    if (!p || hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeDevice)
+        return fail(CF_EINVAL, std::string(what) + " is not device memory");
+    return CF_OK;
+}
+
+int cf_bind_exchange(cf_engine* e, void* send_ids, void* rows, void* grads, int64_t send_cap,
+                     void* recv_ids, void* serve_rows, void* serve_grads, int64_t recv_cap) {
+    CF_TRY(check_engine(e));
+    if (e->x_stage != 0) return fail(CF_ESTATE, "an exchange step is in progress");
+    if (send_cap < 0 || recv_cap < 0) return fail(CF_EINVAL, "negative capacity");
+    if (send_cap > 0) {
+        CF_TRY(check_device_ptr(send_ids, "send_ids"));
+        CF_TRY(check_device_ptr(rows, "rows"));
+        CF_TRY(check_device_ptr(grads, "grads"));
+    }
+    if (recv_cap > 0) {
+        CF_TRY(check_device_ptr(recv_ids, "recv_ids"));
+        CF_TRY(check_device_ptr(serve_rows, "serve_rows"));
+        CF_TRY(check_device_ptr(serve_grads, "serve_grads"));
+    }
+    e->x_send_ids = (int32_t*)send_ids;
+    e->x_rows = (float*)rows;
+    e->x_grads = (float*)grads;
+    e->x_send_cap = send_cap;
+    e->x_recv_ids = (int32_t*)recv_ids;
+    e->x_serve_rows = (float*)serve_rows;
+    e->x_serve_grads = (float*)serve_grads;
+    e->x_recv_cap = recv_cap;
+    return CF_OK;
+}
+
+static int check_xchg(cf_engine* e, int stage) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (c.model != CF_GBPR || !c.dense_item_apply || e->world < 2)
+        return fail(CF_ESTATE, "the group exchange needs GBPR, dense_item_apply=1 and cf_set_shard(world > 1)");
+    if (!e->group_source_global) return fail(CF_ESTATE, "set the global item->user CSR first (cf_set_group_source)");
+    if (e->x_stage != stage) return fail(CF_ESTATE, "exchange calls out of order (begin, serve, grad, finish)");
+    return CF_OK;
+}
+
+int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                  const int32_t* groups, int32_t* send_counts_out) {
+    CF_TRY(check_xchg(e, 0));
+    if (B < 1 || !send_counts_out) return fail(CF_EINVAL, "bad arguments");
+    if (e->GV == e->GV_own) return fail(CF_ESTATE, "bind the item-gradient buffer first (cf_bind_item_grad)");
+    const cf_config& c = e->cfg;
+    const int n = B * group_count(c);
+    if (n > e->x_send_cap) return fail(CF_EINVAL, "exchange send capacity < B * gsize (cf_bind_exchange)");
+    CF_TRY(ensure_batch(e, B));
+    const int k = e->set;
+    e->set ^= 1;
+    StepArgs a;
+    CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
+    const size_t nblk = (size_t)(n + kBlock - 1) / kBlock;
+    if (nblk * (size_t)e->world > e->xhist_cap) {
+        dfree(e->xhist);
+        CF_TRY(dalloc(&e->xhist, nblk * (size_t)e->world));
+        e->xhist_cap = nblk * (size_t)e->world;
+    }
+    XchgArgs x{};
+    x.n = n;
+    x.world = e->world;
+    x.bounds = e->bounds;
+    x.occ = e->occU_[k] + B;
+    x.hist = e->xhist;
+    x.counts = e->xcounts;
+    x.send_ids = e->x_send_ids;
+    CF_HIP(launch_xchg_pack(x, e->stream));
+    CF_HIP(hipMemcpyAsync(e->h_xcounts, e->xcounts, ((size_t)e->world + 1) * 4, hipMemcpyDeviceToHost,
+                          e->stream));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    for (int r = 0; r < e->world; ++r) send_counts_out[r] = e->h_xcounts[r];
+    e->x_args = a;
+    e->x_set = k;
+    e->x_B = B;
+    e->x_stage = 1;
+    return CF_OK;
+}
+
+int cf_xchg_serve(cf_engine* e, int64_t n_recv) {
+    CF_TRY(check_xchg(e, 1));
+    if (n_recv < 0 || n_recv > e->x_recv_cap) return fail(CF_EINVAL, "n_recv exceeds the bound receive capacity");
+    CF_HIP(launch_xchg_serve(e->x_recv_ids, n_recv, e->shard_u0, e->cntU_[e->x_set], e->U, e->x_serve_rows,
+                             e->cfg.n_factors, e->stream));
+    e->x_stage = 2;
+    return CF_OK;
+}
+
+int cf_xchg_grad(cf_engine* e) {
+    CF_TRY(check_xchg(e, 2));
+    const StepArgs& a = e->x_args;
+    {
+        SlotArgs sa = slot_args(e, a, e->x_set);
+        ProfScope pr(e, CF_K_SLOT);
+        CF_HIP(launch_slots(sa, e->stream));
+    }
+    {
+        ProfScope ps(e, CF_K_STEP);
+        CF_HIP(launch_grad(a, e->stream));
+    }
+    e->x_stage = 3;
+    return CF_OK;
+}
+
+int cf_xchg_finish(cf_engine* e, int64_t n_recv) {
+    CF_TRY(check_xchg(e, 3));
+    if (n_recv < 0 || n_recv > e->x_recv_cap) return fail(CF_EINVAL, "n_recv exceeds the bound receive capacity");
+    CF_HIP(launch_xchg_accumulate(e->x_recv_ids, n_recv, e->shard_u0, e->x_serve_grads, e->GU,
+                                  e->cfg.n_factors, e->stream));
+    ApplyArgs p = apply_args(e, e->x_args, e->x_B, e->x_set, e->loss);
+    {
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    e->x_stage = 0;
+    return CF_OK;
 }
 
 int cf_take_loss(cf_engine* e, double* out) {

@@ -81,6 +81,26 @@ struct StepArgs {
     float* __restrict__ slotG;    // [slot capacity, d]
     int slot_max;                 // rows above this many occurrences use float atomics into G
     double* __restrict__ loss_partial;  // [grad grid]
+    // user sharding (GBPR group exchange): this rank owns global users
+    // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
+    // occU until the exchange recodes it -1 - (its row in xrows / xgrads)
+    int64_t shard_u0, shard_u1;
+    const float* __restrict__ xrows;  // [sent, d] rows of other ranks' group users
+    float* __restrict__ xgrads;       // [sent, d] their gradient rows
+};
+
+// a row of this rank's user table that other ranks' batches touch: its count
+// word carries this flag, so it takes the summed (float-atomic) path
+constexpr int32_t kRemoteFlag = 1 << 24;
+
+struct XchgArgs {
+    int n;                        // group occurrences (B * G)
+    int world;
+    const int64_t* __restrict__ bounds;   // [world + 1] global user id ranges
+    int32_t* __restrict__ occ;            // [n] group occurrences (occU + B)
+    int32_t* __restrict__ hist;           // [blocks][world] remote occurrences per block
+    int32_t* __restrict__ counts;         // [world + 1] per owner, [world] = total
+    int32_t* __restrict__ send_ids;       // [n] global ids packed by owner
 };
 
 // slot allocation (between prep and grad): every row with count >= 2 joins the
@@ -212,6 +232,13 @@ hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);
 hipError_t launch_topk(const TopkArgs& a, int n_users, hipStream_t s);
 hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s);
+// group exchange: pack the remote group members of a batch by owner
+hipError_t launch_xchg_pack(const XchgArgs& a, hipStream_t s);
+// owner side: flag + gather the requested rows; scatter-add their gradients
+hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU,
+                             const float* U, float* rows, int d, hipStream_t s);
+hipError_t launch_xchg_accumulate(const int32_t* ids, int64_t n, int64_t u0, const float* grads,
+                                  float* GU, int d, hipStream_t s);
 
 // host-side mirror of the device bijection (for key generation)
 PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch);

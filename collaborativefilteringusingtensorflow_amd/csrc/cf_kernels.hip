@@ -319,11 +319,14 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             const int64_t cb = a.indptr_t[i], ce = a.indptr_t[i + 1];
             const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + gl) << 32));
             g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
+            // user-sharded engine: the item's users are global ids; one owned
+            // by another rank is coded -1 - id (fetched by the group exchange)
+            g = (g >= a.shard_u0 && g < a.shard_u1) ? g - a.shard_u0 : -1 - g;
             a.occU[B + p * G + gl] = g;
         } else {
             g = a.occU[B + p * G + gl];
         }
-        if (a.count_users) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
+        if (a.count_users && g >= 0) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
     }
     if (gl == 0) {
         if (a.sample) {
@@ -473,7 +476,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             for (int s = 0; s < EPL; ++s) sg[s] = 0.f;
             for (int k2 = 0; k2 < G; ++k2) {
                 float gk[EPL];
-                gload<EPL>(a.U, a.occU[B + p * G + k2], d, gl, gk);
+                const int g = a.occU[B + p * G + k2];
+                gload<EPL>(g >= 0 ? a.U : a.xrows, g >= 0 ? g : -1 - g, d, gl, gk);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
                     sg[s] += gk[s];
@@ -516,12 +520,16 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
             for (int k2 = 0; k2 < G; ++k2) {
                 const int g = a.occU[B + p * G + k2];
-                const int cg = a.cntU[g];
-                const int64_t sg_ = slot_of(cg, a.offU[g], a.rankU[B + p * G + k2], a.slot_max);
                 float gk[EPL], gg[EPL];
-                gload<EPL>(a.U, g, d, gl, gk);
+                gload<EPL>(g >= 0 ? a.U : a.xrows, g >= 0 ? g : -1 - g, d, gl, gk);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) gg[s] = rg * sc * vi[s] + a.reg * gk[s];
+                if (g < 0) {  // another rank's user: its gradient row goes back to the owner
+                    gstore<EPL>(a.xgrads, -1 - g, d, gl, gg);
+                    continue;
+                }
+                const int cg = a.cntU[g];
+                const int64_t sg_ = slot_of(cg, a.offU[g], a.rankU[B + p * G + k2], a.slot_max);
                 gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
             if (gl == 0) bias_finish(a, i, ci, sc);
@@ -734,15 +742,16 @@ struct PairRows {
         }
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
-            cg[k] = a.count_users ? a.cntU[g[k]] : 0;
-            sg[k] = a.count_users ? a.offU[g[k]] : 0;
+            cg[k] = (a.count_users && g[k] >= 0) ? a.cntU[g[k]] : 0;
+            sg[k] = (a.count_users && g[k] >= 0) ? a.offU[g[k]] : 0;
         }
         gload<EPL>(a.U, u, a.d, gl, uu);
         gload<EPL>(a.V, i, a.d, gl, vi);
 #pragma unroll
         for (int w = 0; w < WT; ++w) gload<EPL>(a.V, j[w], a.d, gl, vj[w]);
 #pragma unroll
-        for (int k = 0; k < NG; ++k) gload<EPL>(a.U, g[k], a.d, gl, ug[k]);
+        for (int k = 0; k < NG; ++k)
+            gload<EPL>(g[k] >= 0 ? a.U : a.xrows, g[k] >= 0 ? g[k] : -1 - g[k], a.d, gl, ug[k]);
         if (MODEL == GBPR) {
             bi = a.b[i];
 #pragma unroll
@@ -841,7 +850,10 @@ struct PairRows {
                 sq = fmaf(vi[s], vi[s], sq);
             }
             gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
+            if (g[0] >= 0)
+                gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
+            else  // another rank's user: its gradient row goes back to the owner
+                gstore<EPL>(a.xgrads, -1 - g[0], d, gl, gg);
             if (gl == 0) bias_finish(a, i, ci, sc);
             gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else {  // CML
@@ -1275,6 +1287,116 @@ __global__ void build_pairs_kernel(const int64_t* __restrict__ indptr,
 }
 
 // ---------------------------------------------------------------------------
+// GBPR group exchange (user-sharded engine).  Group members are drawn from
+// the item's users over ALL ranks (sampler_gbpr.py:41); a member owned by
+// another rank is fetched from its owner and its gradient row sent back
+// (DESIGN 5).  Pack: histogram the remote members per (block, owner), scan
+// owner-major, scatter each id to its packed position (deterministic: ballot
+// ranks inside the block) and recode the occurrence as -1 - position.
+// ---------------------------------------------------------------------------
+constexpr int kMaxWorld = 64;
+
+__device__ __forceinline__ int owner_of(const int64_t* __restrict__ bounds, int world, int64_t g) {
+    int o = 0;
+    for (int k = 1; k < world; ++k) o += (g >= bounds[k]) ? 1 : 0;
+    return o;
+}
+
+__global__ __launch_bounds__(kBlock) void xchg_hist_kernel(XchgArgs a) {
+    __shared__ int s_h[kMaxWorld];
+    for (int k = threadIdx.x; k < a.world; k += kBlock) s_h[k] = 0;
+    __syncthreads();
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    if (q < a.n) {
+        const int v = a.occ[q];
+        if (v < 0) atomicAdd(&s_h[owner_of(a.bounds, a.world, (int64_t)(-1 - v))], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < a.world; k += kBlock) a.hist[blockIdx.x * a.world + k] = s_h[k];
+}
+
+// one block: exclusive scan of hist in owner-major order (owner o's ids are
+// contiguous, blocks in order inside it); per-owner totals into counts
+__global__ __launch_bounds__(kBlock) void xchg_scan_kernel(XchgArgs a, int nblk) {
+    __shared__ int s_w[kWavesPerBlock];
+    __shared__ int s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    for (int o = 0; o < a.world; ++o) {
+        const int start = s_carry;
+        for (int b0 = 0; b0 < nblk; b0 += kBlock) {
+            const int b = b0 + threadIdx.x;
+            const int v = (b < nblk) ? a.hist[b * a.world + o] : 0;
+            const int inc = wave_incl_scan(v);
+            if (lane == 63) s_w[wv] = inc;
+            __syncthreads();
+            int base = s_carry;
+            for (int k = 0; k < wv; ++k) base += s_w[k];
+            if (b < nblk) a.hist[b * a.world + o] = base + inc - v;
+            __syncthreads();
+            if (threadIdx.x == 0) s_carry += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) a.counts[o] = s_carry - start;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) a.counts[a.world] = s_carry;
+}
+
+__global__ __launch_bounds__(kBlock) void xchg_scatter_kernel(XchgArgs a) {
+    __shared__ int s_cnt[kWavesPerBlock][kMaxWorld];
+    const int q = blockIdx.x * kBlock + threadIdx.x;
+    const int v = (q < a.n) ? a.occ[q] : 0;
+    const int o = (v < 0) ? owner_of(a.bounds, a.world, (int64_t)(-1 - v)) : -1;
+    const int lane = lane_id(), wv = threadIdx.x >> 6;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int my_rank = 0;
+    for (int k = 0; k < a.world; ++k) {
+        const unsigned long long m = __ballot(o == k);
+        if (o == k) my_rank = __popcll(m & lt);
+        if (lane == 0) s_cnt[wv][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (o >= 0) {
+        int pos = a.hist[blockIdx.x * a.world + o] + my_rank;
+        for (int k = 0; k < wv; ++k) pos += s_cnt[k][o];
+        a.send_ids[pos] = -1 - v;
+        a.occ[q] = -1 - pos;
+    }
+}
+
+// owner side, per requested row: flag its count word (it takes the summed
+// path, see kRemoteFlag) and copy its pre-update value out
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void xchg_serve_kernel(const int32_t* __restrict__ ids, int64_t n,
+                                                            int64_t u0, int32_t* __restrict__ cntU,
+                                                            const float* __restrict__ U,
+                                                            float* __restrict__ rows, int d) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
+    if (j >= n) return;
+    const int64_t r = (int64_t)ids[j] - u0;
+    if (gl == 0) atomicOr(&cntU[r], kRemoteFlag);
+    float x[EPL];
+    gload<EPL>(U, r, d, gl, x);
+    gstore<EPL>(rows, j, d, gl, x);
+}
+
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void xchg_accumulate_kernel(const int32_t* __restrict__ ids,
+                                                                 int64_t n, int64_t u0,
+                                                                 const float* __restrict__ grads,
+                                                                 float* __restrict__ GU, int d) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
+    if (j >= n) return;
+    float g[EPL];
+    gload<EPL>(grads, j, d, gl, g);
+    gatomic<EPL>(GU, (int64_t)ids[j] - u0, d, gl, g);
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
 static int epl_for(int d) {
@@ -1504,6 +1626,43 @@ hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int
     if (n_users <= 0) return hipSuccess;
     hipLaunchKernelGGL(build_pairs_kernel, dim3(grid_for(n_users)), dim3(kBlock), 0, s, indptr,
                        indices, n_users, pairs);
+    return hipGetLastError();
+}
+
+hipError_t launch_xchg_pack(const XchgArgs& a, hipStream_t s) {
+    if (a.world < 1 || a.world > kMaxWorld) return hipErrorInvalidValue;
+    const int nblk = a.n > 0 ? (a.n + kBlock - 1) / kBlock : 0;
+    if (nblk > 0) hipLaunchKernelGGL(xchg_hist_kernel, dim3(nblk), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(xchg_scan_kernel, dim3(1), dim3(kBlock), 0, s, a, nblk);
+    if (nblk > 0) hipLaunchKernelGGL(xchg_scatter_kernel, dim3(nblk), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU,
+                             const float* U, float* rows, int d, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + kGroupsPerBlock - 1) / kGroupsPerBlock)), block(kBlock);
+    switch (epl_for(d)) {
+        case 1: hipLaunchKernelGGL(xchg_serve_kernel<1>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+        case 2: hipLaunchKernelGGL(xchg_serve_kernel<2>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+        case 4: hipLaunchKernelGGL(xchg_serve_kernel<4>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+        case 8: hipLaunchKernelGGL(xchg_serve_kernel<8>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+        default: hipLaunchKernelGGL(xchg_serve_kernel<16>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_xchg_accumulate(const int32_t* ids, int64_t n, int64_t u0, const float* grads,
+                                  float* GU, int d, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((n + kGroupsPerBlock - 1) / kGroupsPerBlock)), block(kBlock);
+    switch (epl_for(d)) {
+        case 1: hipLaunchKernelGGL(xchg_accumulate_kernel<1>, grid, block, 0, s, ids, n, u0, grads, GU, d); break;
+        case 2: hipLaunchKernelGGL(xchg_accumulate_kernel<2>, grid, block, 0, s, ids, n, u0, grads, GU, d); break;
+        case 4: hipLaunchKernelGGL(xchg_accumulate_kernel<4>, grid, block, 0, s, ids, n, u0, grads, GU, d); break;
+        case 8: hipLaunchKernelGGL(xchg_accumulate_kernel<8>, grid, block, 0, s, ids, n, u0, grads, GU, d); break;
+        default: hipLaunchKernelGGL(xchg_accumulate_kernel<16>, grid, block, 0, s, ids, n, u0, grads, GU, d); break;
+    }
     return hipGetLastError();
 }
 

@@ -181,6 +181,49 @@ class Engine(object):
     def step_items(self):
         N.check(self._L.cf_step_items(self._h), "cf_step_items")
 
+    # ---- user sharding + GBPR group exchange (include/cf_engine.h) --------------
+    def set_shard(self, world, rank, bounds):
+        b = np.ascontiguousarray(bounds, dtype=np.int64)
+        N.check(self._L.cf_set_shard(self._h, int(world), int(rank), _ptr(b, ctypes.c_int64)),
+                "cf_set_shard")
+
+    def set_group_source(self, indptr_t, indices_t):
+        ip = np.ascontiguousarray(indptr_t, dtype=np.int64)
+        ix = np.ascontiguousarray(indices_t, dtype=np.int32)
+        N.check(self._L.cf_set_group_source(self._h, _ptr(ip, ctypes.c_int64),
+                                            _ptr(ix, ctypes.c_int32), int(ix.shape[0])),
+                "cf_set_group_source")
+
+    def bind_exchange(self, send_ids, rows, grads, send_cap, recv_ids, serve_rows, serve_grads,
+                      recv_cap):
+        v = ctypes.c_void_p
+        N.check(self._L.cf_bind_exchange(self._h, v(send_ids), v(rows), v(grads), int(send_cap),
+                                         v(recv_ids), v(serve_rows), v(serve_grads), int(recv_cap)),
+                "cf_bind_exchange")
+
+    def xchg_begin(self, world, batch_size=None, pairs=None, negs=None, groups=None):
+        """Draw (or take) the batch, pack remote group members by owner;
+        returns the number of ids sent to each rank (groups: GLOBAL ids)."""
+        counts = np.zeros(int(world), dtype=np.int32)
+        cp = _ptr(counts, ctypes.c_int32)
+        if pairs is None:
+            N.check(self._L.cf_xchg_begin(self._h, int(batch_size), None, None, None, cp),
+                    "cf_xchg_begin")
+        else:
+            B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
+            N.check(self._L.cf_xchg_begin(self._h, B, _ptr(pairs, ctypes.c_int32),
+                                          _ptr(negs, ctypes.c_int32), gp, cp), "cf_xchg_begin")
+        return counts
+
+    def xchg_serve(self, n_recv):
+        N.check(self._L.cf_xchg_serve(self._h, int(n_recv)), "cf_xchg_serve")
+
+    def xchg_grad(self):
+        N.check(self._L.cf_xchg_grad(self._h), "cf_xchg_grad")
+
+    def xchg_finish(self, n_recv):
+        N.check(self._L.cf_xchg_finish(self._h, int(n_recv)), "cf_xchg_finish")
+
     def take_loss(self):
         v = ctypes.c_double(0.0)
         N.check(self._L.cf_take_loss(self._h, ctypes.byref(v)), "cf_take_loss")

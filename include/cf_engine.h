@@ -214,6 +214,36 @@ int cf_step_local(cf_engine* eng, int32_t B, const int32_t* host_pairs,
  * (and CML clip of updated rows); zeroes the buffer. */
 int cf_step_items(cf_engine* eng);
 /* Pre-update loss accumulated since the last call (syncs), then reset. */
+/* ---- user sharding + GBPR group exchange ------------------------
+ * A user-sharded GBPR engine draws each pair's group members from the item's
+ * users over ALL ranks (item_posUserList, sampler_gbpr.py:15,41); a member
+ * owned by another rank is fetched from its owner and its gradient row sent
+ * back, so each step equals one step on the concatenated global batch.
+ * Protocol per step (the caller runs the three all-to-alls, e.g. RCCL through
+ * torch.distributed.all_to_all_single, on the engine stream):
+ *   cf_xchg_begin    sample (or take the host batch; groups = GLOBAL user ids),
+ *                    count, pack the remote members' ids by owner into
+ *                    send_ids; send_counts_out[r] = ids for rank r (syncs)
+ *   all-to-all       send_ids -> recv_ids (ids this rank serves)
+ *   cf_xchg_serve    copy the served rows (pre-update) into serve_rows
+ *   all-to-all       serve_rows -> rows (in send_ids order)
+ *   cf_xchg_grad     slots + gradient; remote members' gradient rows -> grads
+ *   all-to-all       grads -> serve_grads
+ *   cf_xchg_finish   add the served rows' gradients, user Adagrad
+ * then the item all-reduce + cf_step_items as for cf_step_local.  A served
+ * row's count word is flagged, so all its contributions are summed before
+ * the update (TF1 dedup semantics).  Requires GBPR, dense_item_apply=1. */
+int cf_set_shard(cf_engine* eng, int32_t world, int32_t rank, const int64_t* user_bounds /*[world+1]*/);
+/* global item -> user CSR (sampler_gbpr.py:15), user ids global */
+int cf_set_group_source(cf_engine* eng, const int64_t* indptr_t, const int32_t* indices_t, int64_t nnz);
+int cf_bind_exchange(cf_engine* eng, void* send_ids, void* rows, void* grads, int64_t send_cap,
+                     void* recv_ids, void* serve_rows, void* serve_grads, int64_t recv_cap);
+int cf_xchg_begin(cf_engine* eng, int32_t B, const int32_t* host_pairs, const int32_t* host_negs,
+                  const int32_t* host_groups, int32_t* send_counts_out);
+int cf_xchg_serve(cf_engine* eng, int64_t n_recv);
+int cf_xchg_grad(cf_engine* eng);
+int cf_xchg_finish(cf_engine* eng, int64_t n_recv);
+
 int cf_take_loss(cf_engine* eng, double* loss_sum_out);
 
 /* ---- evaluation ----------------------------------------------------------- */

@@ -1,0 +1,135 @@
+"""Two ranks of the user-sharded GBPR step with the cross-shard group exchange
+on the REAL engine (cf_set_shard / cf_set_group_source / cf_xchg_*).
+
+Both ranks share device 0 of the one-GPU test box and exchange through gloo
+(host-staged all-to-alls; on an 8-GPU node the same GroupExchangeStep runs on
+RCCL).  Host-fed: after K steps on the reference's captured GBPR batches
+(sampler_gbpr.py, global group members) every rank's user shard, the item
+table and the item bias must equal the float64 oracle on the concatenated
+batches (1e-5 relative).  Device-sampled: the group members drawn on device
+come from the item's users over both shards and the replicas stay identical.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_group_exchange,
+                                                                       shard_users, local_csr)
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    ip, ix = fold["train_indptr"], fold["train_indices"]
+    bounds = [shard_users(ip, world, r)[0] for r in range(world)] + [943]
+    u0, u1 = bounds[rank], bounds[rank + 1]
+    lip, lix = local_csr(ip, ix, u0, u1)
+    W, G = batches[0][1].shape[1], batches[0][2].shape[1]
+    d = U0.shape[1]
+    e = Engine("gbpr", u1 - u0, 1682, d, n_neg=W, gsize=G, rho=0.4, reg=0.01,
+               dense_item_apply=True, seed=20 + rank)
+    e.set_interactions(lip, lix)
+    e.set_table("user", U0[u0:u1])
+    e.set_table("item", V0)
+    e.set_table("bias", b0)
+    step, _grad = make_gpu_group_exchange(e, world, rank, bounds, ip, ix, 1682, d, 100,
+                                          torch.device("cuda", 0))
+    drawn = []
+    if sampled:
+        for _ in range(6):
+            pairs, negs, groups = e.sample(64)
+            pairs = pairs.copy()
+            pairs[:, 0] += u0          # sample() returns this rank's local user ids
+            drawn.append((pairs, groups))
+            step(batch_size=64)
+    else:
+        for pairs, negs, groups in batches:
+            mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
+            lp = pairs[mine].copy()
+            lp[:, 0] -= u0
+            step(pairs=lp, negs=negs[mine], groups=groups[mine])
+    torch.cuda.synchronize()
+    q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("bias"),
+           e.get_table("acc_user"), drawn))
+    e.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(fold1, batches, U0, V0, b0, sampled=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("stream", ["gbpr_b100_g1_w5", "gbpr_b100_g3_w2"])
+def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream):
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(12)
+    d = 16
+    U0 = O.init_table(rng, (943, d))
+    V0 = O.init_table(rng, (1682, d))
+    b0 = O.init_table(rng, (1682,))
+    batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
+                streams[stream + "/groups"][s]) for s in range(8)]
+    res = _run(fold1, batches, U0, V0, b0)
+    U, V, b = U0.astype(np.float64), V0.astype(np.float64), b0.astype(np.float64)
+    AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
+    for pairs, negs, groups in batches:
+        O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
+    rel = lambda a, c: np.abs(a - c).max() / np.abs(c).max()
+    for rank, u0, u1, Ul, Vr, br, AUl, _ in res:
+        assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
+        assert rel(AUl, AU[u0:u1]) <= 1e-5, (rank, rel(AUl, AU[u0:u1]))
+        assert rel(Vr, V) <= 1e-5 and rel(br, b) <= 1e-5
+    assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
+
+
+def test_two_rank_device_sampled_groups_span_shards(fold1):
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(13)
+    d = 16
+    U0 = O.init_table(rng, (943, d))
+    V0 = O.init_table(rng, (1682, d))
+    b0 = O.init_table(rng, (1682,))
+    dummy = [(np.zeros((1, 2), np.int32), np.zeros((1, 5), np.int32), np.zeros((1, 1), np.int32))]
+    res = _run(fold1, dummy, U0, V0, b0, sampled=True)
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    cross = 0
+    for rank, u0, u1, Ul, Vr, br, AUl, drawn in res:
+        assert np.all(np.isfinite(Ul)) and np.all(np.isfinite(Vr))
+        for pairs, groups in drawn:
+            for (u, i), g in zip(pairs, groups):
+                assert u0 <= u < u1
+                for gg in g:     # g in Pos^-1(i) over ALL users (sampler_gbpr.py:41)
+                    assert i in ix[ip[gg]:ip[gg + 1]]
+                    cross += int(not (u0 <= gg < u1))
+    assert cross > 0
+    assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])

@@ -1,0 +1,190 @@
+"""World-size-2 gloo test of the GBPR cross-shard group exchange
+(collaborativefilteringusingtensorflow_amd/distributed.py GroupExchangeStep) on CPU.
+
+GBPR draws group members from every user of the item (sampler_gbpr.py:15,41),
+so with users sharded a member can live on the other rank.  Each rank drives
+the product ``GroupExchangeStep`` (three all-to-alls + the item all-reduce)
+with an oracle-backed stand-in that implements the same protocol as the C ABI
+(cf_xchg_begin / serve / grad / finish, include/cf_engine.h).  After K steps
+every rank's user shard, the replicated item table and bias must equal the
+oracle run on the concatenated global batches.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class OracleGroupShard(object):
+    """numpy GBPR shard speaking the cf_xchg_* protocol (float64)."""
+
+    def __init__(self, U_local, V, b, bounds, rank, rho, reg, lr=0.1):
+        self.U, self.V, self.b = U_local.copy(), V.copy(), b.copy()
+        self.AU, self.AV, self.Ab = (np.full_like(self.U, 0.1), np.full_like(self.V, 0.1),
+                                     np.full_like(self.b, 0.1))
+        self.bounds, self.rank = np.asarray(bounds), rank
+        self.u0 = int(bounds[rank])
+        self.rho, self.reg, self.lr = rho, reg, lr
+        self.device = torch.device("cpu")
+        d = U_local.shape[1]
+        self.d = d
+        self.item_grad = torch.zeros(V.size + b.size, dtype=torch.float64)
+        self.send_ids = torch.zeros(0, dtype=torch.int32)
+        self.rows = torch.zeros((0, d), dtype=torch.float64)
+        self.grads = torch.zeros((0, d), dtype=torch.float64)
+        self.ensure_recv(1)
+
+    def ensure_recv(self, n):
+        self.recv_ids = torch.zeros(n, dtype=torch.int32)
+        self.serve_rows = torch.zeros((n, self.d), dtype=torch.float64)
+        self.serve_grads = torch.zeros((n, self.d), dtype=torch.float64)
+
+    def xchg_begin(self, world, batch_size=None, pairs=None, negs=None, groups=None):
+        self.pairs, self.negs, self.groups = pairs, negs, groups      # u local, groups global
+        owner = np.searchsorted(self.bounds, groups.reshape(-1), side="right") - 1
+        remote = owner != self.rank
+        order = np.argsort(np.where(remote, owner, -1), kind="stable")
+        order = order[remote[order]]                  # remote occurrences, packed by owner
+        self.slot = np.full(groups.size, -1)
+        self.slot[order] = np.arange(order.size)
+        counts = np.bincount(owner[order], minlength=world)
+        self.send_ids = torch.as_tensor(groups.reshape(-1)[order].astype(np.int32))
+        self.rows = torch.zeros((order.size, self.d), dtype=torch.float64)
+        self.grads = torch.zeros((order.size, self.d), dtype=torch.float64)
+        return counts
+
+    def xchg_serve(self, n):
+        ids = self.recv_ids[:n].numpy().astype(np.int64) - self.u0
+        self.serve_rows[:n] = torch.as_tensor(self.U[ids])
+
+    def xchg_grad(self):
+        rho, reg, d = self.rho, self.reg, self.d
+        pairs, negs, groups = self.pairs, self.negs, self.groups
+        Bn, G = groups.shape
+        u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+        flat = groups.reshape(-1)
+        Ug = np.where((self.slot >= 0)[:, None],
+                      self.rows.numpy()[np.maximum(self.slot, 0)],
+                      self.U[np.clip(flat - self.u0, 0, self.U.shape[0] - 1)]).reshape(Bn, G, d)
+        Uu, Vi, Vj = self.U[u_idx], self.V[i_idx], self.V[negs]
+        bi, bj = self.b[i_idx], self.b[negs]
+        ui = rho * np.sum(Ug * Vi[:, None, :], axis=(1, 2)) / G + (1 - rho) * np.sum(Uu * Vi, -1) + bi
+        x = ui[:, None] - (np.sum(Uu[:, None, :] * Vj, -1) + bj)
+        c = -1.0 / (1.0 + np.exp(x))
+        s = c.sum(axis=1)
+        gUu = (1 - rho) * s[:, None] * Vi - (c[:, :, None] * Vj).sum(axis=1) + reg * Uu
+        gUg = ((rho / G) * s[:, None, None] * Vi[:, None, :] + reg * Ug).reshape(-1, d)
+        gVi = s[:, None] * ((rho / G) * Ug.sum(axis=1) + (1 - rho) * Uu) + reg * Vi
+        gVj = -c[:, :, None] * Uu[:, None, :]
+        loc = self.slot < 0
+        self.pending = (np.concatenate([u_idx, flat[loc] - self.u0]),
+                        np.concatenate([gUu, gUg[loc]]))
+        self.grads[:] = torch.as_tensor(gUg[~loc][np.argsort(self.slot[~loc])])
+        n_items = self.V.shape[0]
+        GV = self.item_grad[:n_items * d].numpy().reshape(n_items, d)
+        Gb = self.item_grad[n_items * d:].numpy()
+        np.add.at(GV, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([gVi, gVj.reshape(-1, d)]))
+        np.add.at(Gb, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([s, (-c + reg * bj).reshape(-1)]))
+
+    def xchg_finish(self, n):
+        from oracle import cf_oracle as O
+        rows, grads = self.pending
+        ids = self.recv_ids[:n].numpy().astype(np.int64) - self.u0
+        O.dedup_adagrad(self.U, self.AU, np.concatenate([rows, ids]),
+                        np.concatenate([grads, self.serve_grads[:n].numpy()]), self.lr)
+
+    def step_items(self):
+        n_items, d = self.V.shape
+        GV = self.item_grad[:n_items * d].numpy().reshape(n_items, d)
+        Gb = self.item_grad[n_items * d:].numpy()
+        rows = np.nonzero(np.any(GV != 0, axis=1))[0]
+        self.AV[rows] += GV[rows] ** 2
+        self.V[rows] -= self.lr * GV[rows] / np.sqrt(self.AV[rows])
+        rb = np.nonzero(Gb != 0)[0]
+        self.Ab[rb] += Gb[rb] ** 2
+        self.b[rb] -= self.lr * Gb[rb] / np.sqrt(self.Ab[rb])
+        self.item_grad.zero_()
+
+
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import (GroupExchangeStep,
+                                                                       shard_users)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                            world_size=world)
+    ip = fold["train_indptr"]
+    bounds = [shard_users(ip, world, r)[0] for r in range(world)] + [U0.shape[0]]
+    u0, u1 = bounds[rank], bounds[rank + 1]
+    be = OracleGroupShard(U0[u0:u1], V0, b0, bounds, rank, rho=0.4, reg=0.01)
+    step = GroupExchangeStep(be, be.item_grad, world)
+    n_remote = 0
+    for pairs, negs, groups in batches:
+        mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
+        lp = pairs[mine].copy()
+        lp[:, 0] -= u0
+        g = groups[mine]
+        n_remote += int(np.sum((g < u0) | (g >= u1)))
+        step(pairs=lp, negs=negs[mine], groups=g)
+    q.put((rank, u0, u1, be.U, be.V, be.b, be.AU, n_remote))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_item_users_is_the_transpose(fold1):
+    from collaborativefilteringusingtensorflow_amd.distributed import item_users
+    from oracle import cf_oracle as O
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    tp, tu = item_users(ip, ix, 1682)
+    rp, ru = O.transpose_csr(ip, ix, 1682)
+    np.testing.assert_array_equal(tp, rp)
+    for i in range(0, 1682, 37):
+        assert sorted(tu[tp[i]:tp[i + 1]].tolist()) == sorted(np.asarray(ru[rp[i]:rp[i + 1]]).tolist())
+
+
+@pytest.mark.parametrize("stream,world", [("gbpr_b100_g1_w5", 2), ("gbpr_b100_g3_w2", 2)])
+def test_group_exchange_equals_global_step(fold1, streams, stream, world):
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(9)
+    U0 = O.init_table(rng, (943, 8), dtype=np.float64)
+    V0 = O.init_table(rng, (1682, 8), dtype=np.float64)
+    b0 = O.init_table(rng, (1682,), dtype=np.float64)
+    batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
+                streams[stream + "/groups"][s]) for s in range(6)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    U, V, b = U0.copy(), V0.copy(), b0.copy()
+    AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
+    for pairs, negs, groups in batches:
+        O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
+    assert sum(r[7] for r in res) > 50          # the exchange actually carried members
+    for rank, u0, u1, Ul, Vr, br, AUl, _ in res:
+        np.testing.assert_allclose(Ul, U[u0:u1], rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(AUl, AU[u0:u1], rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(Vr, V, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(br, b, rtol=1e-12, atol=1e-14)
