@@ -32,7 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_degrees, synth_graph  # noqa: E402,E501
-from collaborativefilteringusingtensorflow_amd.distributed import make_gpu_sharded, shard_users  # noqa: E402,E501
+from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_group_exchange,  # noqa: E402
+                                                                   make_gpu_sharded, shard_users)
 from collaborativefilteringusingtensorflow_amd._native import KERNELS  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -47,6 +48,11 @@ CONFIGS = {
                  graph_seed=20261015, d=128, W=5, G=1, B=65536, reg=0.0, truncated=False,
                  margin=1.0, reg_cov=1.0, clip_norm=1.0,
                  desc="CML synthetic 1M users x 100K items, d=128, W=5"),
+    # configs[3]: GBPR, 10M users x 1M items (N > 1: user-sharded with the
+    # cross-shard group exchange + RCCL item-gradient all-reduce)
+    "cfg4": dict(model="gbpr", n_users=10_000_000, n_items=1_000_000, mean_degree=20.0, zipf=0.8,
+                 graph_seed=20261015, d=64, W=5, G=1, B=65536, reg=0.01, truncated=True,
+                 rho=0.4, desc="GBPR synthetic 10M users x 1M items, d=64, W=5, G=1"),
     # configs[4] shape, AMF phase 2 (adversarial) step
     "cfg5": dict(model="amf", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
                  graph_seed=20261015, d=128, W=5, G=1, B=65536, reg=0.05, truncated=True,
@@ -143,10 +149,16 @@ def main():
                          "1 apply(s)+draw(s+1); 0 stepwise")
     ap.add_argument("--slot-max", type=int, default=0,
                     help="cf_set_option slot_max (0 = engine default)")
+    ap.add_argument("--n-users", type=int, default=0, help="override the config's users (rehearsals)")
+    ap.add_argument("--n-items", type=int, default=0, help="override the config's items (rehearsals)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["B"] = args.batch
+    if args.n_users or args.n_items:
+        cfg["n_users"] = args.n_users or cfg["n_users"]
+        cfg["n_items"] = args.n_items or cfg["n_items"]
+        cfg["desc"] += " [rehearsal: %d users x %d items]" % (cfg["n_users"], cfg["n_items"])
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -176,7 +188,7 @@ def main():
     log("rank %d: users [%d,%d) nnz %d generated in %.1fs" % (rank, u0, u1, len(indices),
                                                              time.perf_counter() - t0))
     kw = dict(reg=cfg["reg"])
-    for k in ("margin", "reg_cov", "clip_norm", "reg_adv"):
+    for k in ("margin", "reg_cov", "clip_norm", "reg_adv", "rho"):
         if k in cfg:
             kw[k] = cfg[k]
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
@@ -191,10 +203,20 @@ def main():
     if cfg["model"] == "amf":
         eng.begin_phase(1)
 
-    if world > 1:
+    if world > 1 and cfg["model"] == "gbpr":
+        # group members come from every shard: the global CSR feeds the
+        # item -> user source, the exchange fetches / returns remote rows
+        degs = synth_degrees(nu_all, cfg["mean_degree"], cfg["graph_seed"])
+        bounds = [shard_users(degs, world, r)[0] for r in range(world)] + [nu_all]
+        gip, gix = synth_graph(nu_all, ni, cfg["mean_degree"], cfg["zipf"], cfg["graph_seed"],
+                               n_threads=min(16, os.cpu_count() or 1))
+        step, _grad = make_gpu_group_exchange(eng, world, rank, bounds, gip, gix, ni, d, B,
+                                              torch.device("cuda", local_rank))
+        del gip, gix
+    elif world > 1:
         step, _grad = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
                                        torch.device("cuda", local_rank))
-
+    if world > 1:
         def run(k):
             for _ in range(k):
                 step(B)
@@ -290,7 +312,8 @@ def main():
         "config": {"workload": cfg["desc"], "model": cfg["model"], "n_users": nu_all,
                    "n_items": ni, "nnz_rank0": int(len(indices)), "d": d, "W": W,
                    "batch_pairs_per_gpu": B, "global_batch": B * world,
-                   "parallelism": "dp%d user-sharded, RCCL item-grad all-reduce" % world
+                   "parallelism": ("dp%d user-sharded, RCCL item-grad all-reduce" % world
+                                   + (" + group-member all-to-all" if cfg["model"] == "gbpr" else ""))
                    if world > 1 else "single GPU"},
         "per_gpu_value": value / world,
         "full_step_algorithmic_GBps": full_b / elapsed / 1e9,
