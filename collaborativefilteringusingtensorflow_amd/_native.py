@@ -82,6 +82,8 @@ SIGNATURES = {
     "cf_bind_item_grad": (ctypes.c_int, [_P, _P, _I64]),
     "cf_step_local": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_items": (ctypes.c_int, [_P]),
+    "cf_step_local_grad": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
+    "cf_step_local_apply": (ctypes.c_int, [_P, _I32]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
     "cf_set_shard": (ctypes.c_int, [_P, _I32, _I32, _PI64]),
     "cf_set_group_source": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),

@@ -134,6 +134,19 @@ struct cf_engine {
     float *x_rows = nullptr, *x_grads = nullptr, *x_serve_rows = nullptr, *x_serve_grads = nullptr;
     int64_t x_send_cap = 0, x_recv_cap = 0;
     int x_stage = 0;                 // 0 idle, 1 begun, 2 served, 3 grads done
+
+    // split local step (cf_step_local_grad / cf_step_local_apply): the step
+    // between its two halves, and a batch already drawn + counted by the
+    // previous apply launch (device sampler), with the sampler position it
+    // was drawn from (restored if the draw is discarded)
+    int lg_stage = 0;
+    StepArgs lg_args{};
+    int lg_set = 0, lg_B = 0;
+    bool pend = false;
+    StepArgs pend_args{};
+    int pend_set = 0, pend_B = 0;
+    int64_t pend_epoch = 0, pend_batch = 0;
+    int pend_sampler_B = 0;
     StepArgs x_args{};
     int x_set = 0;
     int x_B = 0;
@@ -572,6 +585,23 @@ int read_loss(cf_engine* e, int slot, double* out) {
     return CF_OK;
 }
 
+// drop a batch the previous apply launch drew ahead: clear its occurrence
+// counts and put the sampler back where that draw started
+int discard_pending(cf_engine* e) {
+    if (!e->pend) return CF_OK;
+    const cf_config& c = e->cfg;
+    const StepArgs& a = e->pend_args;
+    const int64_t nU = (int64_t)e->pend_B * users_per_pair(c), nV = (int64_t)e->pend_B * items_per_pair(c);
+    if (a.count_users) CF_HIP(launch_uncount(a.occU, nU, a.cntU, e->stream));
+    if (a.count_items) CF_HIP(launch_uncount(a.occV, nV, a.cntV, e->stream));
+    e->epoch = e->pend_epoch;
+    e->batch = e->pend_batch;
+    e->sampler_B = e->pend_sampler_B;
+    e->set = e->pend_set;
+    e->pend = false;
+    return CF_OK;
+}
+
 // a user-sharded GBPR engine steps only through the group exchange
 int check_not_xchg(cf_engine* e) {
     if (e->cfg.model == CF_GBPR && e->world > 1)
@@ -832,6 +862,7 @@ int cf_synchronize(cf_engine* e) {
 
 int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indices, int64_t nnz) {
     CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
     const cf_config& c = e->cfg;
     if (!indptr || (nnz > 0 && !indices)) return fail(CF_EINVAL, "null CSR");
     if (nnz < 1) return fail(CF_EINVAL, "no interactions");
@@ -927,6 +958,7 @@ int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
 int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32_t* groups,
             int32_t B, double* loss_out) {
     CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
     CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
     if (!pairs) return fail(CF_EINVAL, "host batch required (use cf_train_steps for the device sampler)");
@@ -941,6 +973,7 @@ int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32
 
 int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_out) {
     CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
     CF_TRY(check_not_xchg(e));
     if (B < 1 || n_steps < 0) return fail(CF_EINVAL, "bad B / n_steps");
     if (e->cfg.dense_item_apply && e->GV != e->GV_own)
@@ -962,6 +995,7 @@ int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_ou
 
 int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* groups) {
     CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
     const cf_config& c = e->cfg;
     if (B < 1 || !pairs || !negs) return fail(CF_EINVAL, "bad arguments");
     const int W = c.n_neg, G = group_count(c);
@@ -996,12 +1030,18 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
 
 int cf_get_sampler_state(cf_engine* e, int64_t* epoch, int64_t* batch) {
     if (!e) return fail(CF_EINVAL, "null engine");
+    if (e->pend) {  // a batch drawn ahead is not consumed yet
+        if (epoch) *epoch = e->pend_epoch;
+        if (batch) *batch = e->pend_batch;
+        return CF_OK;
+    }
     if (epoch) *epoch = e->epoch;
     if (batch) *batch = e->batch;
     return CF_OK;
 }
 
 int cf_set_sampler_state(cf_engine* e, int64_t epoch, int64_t batch) {
+    if (e && e->pend) CF_TRY(discard_pending(e));
     if (!e) return fail(CF_EINVAL, "null engine");
     if (epoch < 0 || batch < 0) return fail(CF_EINVAL, "negative sampler state");
     e->epoch = epoch;
@@ -1011,6 +1051,7 @@ int cf_set_sampler_state(cf_engine* e, int64_t epoch, int64_t batch) {
 
 int cf_begin_phase(cf_engine* e, int32_t phase) {
     CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
     const cf_config& c = e->cfg;
     if (c.model != CF_AMF) return fail(CF_EINVAL, "phases exist only for AMF");
     if (phase != 0 && phase != 1) return fail(CF_EINVAL, "phase must be 0 or 1");
@@ -1044,13 +1085,76 @@ int cf_bind_item_grad(cf_engine* e, void* ptr, int64_t n) {
     return CF_OK;
 }
 
-int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
-                  const int32_t* groups) {
+int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                       const int32_t* groups) {
     CF_TRY(check_engine(e));
-    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_local needs dense_item_apply=1");
+    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "the split step needs dense_item_apply=1");
     CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
-    return run_step(e, B, pairs, negs, groups, e->loss);
+    if (e->lg_stage != 0) return fail(CF_ESTATE, "cf_step_local_apply of the previous step is missing");
+    if (e->pend && (pairs || e->pend_B != B)) CF_TRY(discard_pending(e));
+    CF_TRY(ensure_batch(e, B));
+    StepArgs a;
+    int k;
+    if (e->pend) {  // drawn + counted by the previous apply launch
+        a = e->pend_args;
+        k = e->pend_set;
+        e->pend = false;
+    } else {
+        k = e->set;
+        e->set ^= 1;
+        CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
+    }
+    {
+        SlotArgs sa = slot_args(e, a, k);
+        ProfScope pr(e, CF_K_SLOT);
+        CF_HIP(launch_slots(sa, e->stream));
+    }
+    {
+        ProfScope ps(e, CF_K_STEP);
+        CF_HIP(launch_grad(a, e->stream));
+    }
+    e->lg_args = a;
+    e->lg_set = k;
+    e->lg_B = B;
+    e->lg_stage = 1;
+    return CF_OK;
+}
+
+int cf_step_local_apply(cf_engine* e, int32_t next_B) {
+    CF_TRY(check_engine(e));
+    if (e->lg_stage != 1) return fail(CF_ESTATE, "cf_step_local_grad must come first");
+    if (next_B < 0) return fail(CF_EINVAL, "next_B must be >= 0");
+    const int k = e->lg_set;
+    ApplyArgs p = apply_args(e, e->lg_args, e->lg_B, k, e->loss);
+    e->lg_stage = 0;
+    if (next_B > 0 && next_B <= e->Bcap && e->prep_side == 0) {
+        // draw + count the next batch in the same launch (other buffer set)
+        StepArgs nx = base_step_args(e, next_B, k ^ 1);
+        e->pend_epoch = e->epoch;
+        e->pend_batch = e->batch;
+        e->pend_sampler_B = e->sampler_B;
+        CF_TRY(sampler_args(e, next_B, &nx));
+        {
+            ProfScope ps(e, CF_K_APPLY_PREP);
+            CF_HIP(launch_apply_prep(p, nx, e->stream));
+        }
+        e->pend = true;
+        e->pend_args = nx;
+        e->pend_set = k ^ 1;
+        e->pend_B = next_B;
+        e->set = k;  // the set after the pending one
+    } else {
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    return pending_clips(e);
+}
+
+int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                  const int32_t* groups) {
+    CF_TRY(cf_step_local_grad(e, B, pairs, negs, groups));
+    return cf_step_local_apply(e, 0);
 }
 
 int cf_step_items(cf_engine* e) {

@@ -227,6 +227,8 @@ hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hi
 hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int truncated,
                               uint64_t seed, hipStream_t s);
 hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s);
+// zero the counts of a batch's occurrences (a drawn-ahead batch is dropped)
+hipError_t launch_uncount(const int32_t* occ, int64_t n, int32_t* cnt, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
                               int4* pairs, hipStream_t s);
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);

@@ -1666,6 +1666,21 @@ hipError_t launch_xchg_accumulate(const int32_t* ids, int64_t n, int64_t u0, con
     return hipGetLastError();
 }
 
+__global__ void uncount_kernel(const int32_t* __restrict__ occ, int64_t n, int32_t* __restrict__ cnt) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = t0; q < n; q += nt) {
+        const int32_t r = occ[q];
+        if (r >= 0) cnt[r] = 0;
+    }
+}
+
+hipError_t launch_uncount(const int32_t* occ, int64_t n, int32_t* cnt, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(uncount_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, occ, n, cnt);
+    return hipGetLastError();
+}
+
 uint64_t mix64_host(uint64_t z) { return mix64(z); }
 
 PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch) {

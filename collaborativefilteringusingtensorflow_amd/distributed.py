@@ -52,22 +52,39 @@ def local_csr(indptr, indices, u0, u1):
 
 
 class ShardedStep(object):
-    """One data-parallel optimizer step: local phase -> all-reduce -> items."""
+    """One data-parallel optimizer step: local phase -> all-reduce -> items.
 
-    def __init__(self, backend, item_grad, process_group=None):
+    With a backend that splits the local phase (step_local_grad /
+    step_local_apply, include/cf_engine.h) the all-reduce is issued as soon
+    as the item gradient is complete and runs beside the user update and the
+    draw of the next batch; the item update waits for it."""
+
+    def __init__(self, backend, item_grad, process_group=None, draw_ahead=True):
         import torch.distributed as dist
         self.backend = backend
         self.item_grad = item_grad
         self.group = process_group
+        self.draw_ahead = draw_ahead
         self._dist = dist
 
     def __call__(self, batch_size=None, pairs=None, negs=None, groups=None):
+        be = self.backend
+        if not hasattr(be, "step_local_grad"):
+            if pairs is None:
+                be.step_local(batch_size)
+            else:
+                be.step_local(pairs=pairs, negs=negs, groups=groups)
+            self._dist.all_reduce(self.item_grad, group=self.group)
+            be.step_items()
+            return
         if pairs is None:
-            self.backend.step_local(batch_size)
+            be.step_local_grad(batch_size)
         else:
-            self.backend.step_local(pairs=pairs, negs=negs, groups=groups)
-        self._dist.all_reduce(self.item_grad, group=self.group)
-        self.backend.step_items()
+            be.step_local_grad(pairs=pairs, negs=negs, groups=groups)
+        work = self._dist.all_reduce(self.item_grad, group=self.group, async_op=True)
+        be.step_local_apply(batch_size if (pairs is None and self.draw_ahead) else 0)
+        work.wait()
+        be.step_items()
 
 
 def share_stream(engine, device):

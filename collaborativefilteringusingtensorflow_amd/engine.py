@@ -178,6 +178,18 @@ class Engine(object):
         N.check(self._L.cf_step_local(self._h, B, _ptr(pairs, ctypes.c_int32),
                                       _ptr(negs, ctypes.c_int32), gp), "cf_step_local")
 
+    def step_local_grad(self, batch_size=None, pairs=None, negs=None, groups=None):
+        if pairs is None:
+            N.check(self._L.cf_step_local_grad(self._h, int(batch_size), None, None, None),
+                    "cf_step_local_grad")
+            return
+        B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
+        N.check(self._L.cf_step_local_grad(self._h, B, _ptr(pairs, ctypes.c_int32),
+                                           _ptr(negs, ctypes.c_int32), gp), "cf_step_local_grad")
+
+    def step_local_apply(self, next_batch_size=0):
+        N.check(self._L.cf_step_local_apply(self._h, int(next_batch_size)), "cf_step_local_apply")
+
     def step_items(self):
         N.check(self._L.cf_step_items(self._h), "cf_step_items")
 

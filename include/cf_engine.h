@@ -210,10 +210,22 @@ int cf_bind_item_grad(cf_engine* eng, void* device_ptr, int64_t n_elems);
  * item gradient is left in the bound buffer. */
 int cf_step_local(cf_engine* eng, int32_t B, const int32_t* host_pairs,
                   const int32_t* host_negs, const int32_t* host_groups);
+/* Phase 1 in two halves, so that the item all-reduce can start as soon as the
+ * item gradient is complete and overlap the rest:
+ *   cf_step_local_grad   sample / host-feed, count, slots, gradient
+ *   (start the all-reduce of the item-gradient buffer)
+ *   cf_step_local_apply  user Adagrad; next_B > 0 also draws + counts the
+ *                        next device-sampled batch of next_B pairs in the
+ *                        same launch (used by the next cf_step_local_grad
+ *                        with that B and no host batch; any other call drops
+ *                        it and rewinds the sampler).
+ * cf_step_local = cf_step_local_grad + cf_step_local_apply(0). */
+int cf_step_local_grad(cf_engine* eng, int32_t B, const int32_t* host_pairs,
+                       const int32_t* host_negs, const int32_t* host_groups);
+int cf_step_local_apply(cf_engine* eng, int32_t next_B);
 /* Phase 2, after the buffer holds the cross-rank sum: dense item Adagrad
  * (and CML clip of updated rows); zeroes the buffer. */
 int cf_step_items(cf_engine* eng);
-/* Pre-update loss accumulated since the last call (syncs), then reset. */
 /* ---- user sharding + GBPR group exchange ------------------------
  * A user-sharded GBPR engine draws each pair's group members from the item's
  * users over ALL ranks (item_posUserList, sampler_gbpr.py:15,41); a member
@@ -244,6 +256,7 @@ int cf_xchg_serve(cf_engine* eng, int64_t n_recv);
 int cf_xchg_grad(cf_engine* eng);
 int cf_xchg_finish(cf_engine* eng, int64_t n_recv);
 
+/* Pre-update loss accumulated since the last call (syncs), then reset. */
 int cf_take_loss(cf_engine* eng, double* loss_sum_out);
 
 /* ---- evaluation ----------------------------------------------------------- */

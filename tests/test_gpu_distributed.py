@@ -89,3 +89,47 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
         assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
         assert rel(Vr, V) <= 1e-5 and rel(AVr, AV) <= 1e-5
     assert np.array_equal(res[0][4], res[1][4])   # replicas bit-identical
+
+
+def _draw_ahead_worker(port, fold, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import make_gpu_sharded
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1)
+    ip, ix = fold["train_indptr"], fold["train_indices"]
+    out = []
+    for ahead in (True, False):
+        e = Engine("bpr", 943, 1682, 16, n_neg=2, reg=0.05, dense_item_apply=True, seed=77)
+        e.set_interactions(ip, ix)
+        e.init_params(0.0, 0.1, seed=5)
+        step, _ = make_gpu_sharded(e, 1682, 16, False, torch.device("cuda", 0))
+        step.draw_ahead = ahead
+        for _ in range(9):
+            step(batch_size=120)
+        torch.cuda.synchronize()
+        state = e.sampler_state()
+        nxt = e.sample(120)           # drops a drawn-ahead batch, rewinds the sampler
+        out.append((e.get_table("user"), e.get_table("item"), e.get_table("acc_user"), state,
+                    nxt[0], nxt[1], e.take_loss()))
+        e.close()
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_draw_ahead_split_step_equals_plain_split_step(fold1):
+    """cf_step_local_grad / cf_step_local_apply(next_B): the batch drawn in the
+    apply launch is the one the sampler would draw next; dropping it rewinds."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_draw_ahead_worker, args=(_free_port(), fold1, q))
+    p.start()
+    a, b = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    for x, y in zip(a[:3], b[:3]):   # float-atomic item sums: last-bit order effects only
+        assert np.abs(x - y).max() <= 1e-6 * np.abs(y).max()
+    assert a[3] == b[3]
+    assert np.array_equal(a[4], b[4]) and np.array_equal(a[5], b[5])
+    assert abs(a[6] - b[6]) <= 1e-6 * abs(b[6])
