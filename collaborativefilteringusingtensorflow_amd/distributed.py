@@ -81,9 +81,14 @@ class ShardedStep(object):
             be.step_local_grad(batch_size)
         else:
             be.step_local_grad(pairs=pairs, negs=negs, groups=groups)
-        work = self._dist.all_reduce(self.item_grad, group=self.group, async_op=True)
+        # gloo stages device tensors through the host: overlap buys nothing
+        # there (and its async device path serialises both ranks of a shared
+        # GPU), so only RCCL gets the asynchronous all-reduce
+        overlap = self.item_grad.is_cuda and self._dist.get_backend(self.group) != "gloo"
+        work = self._dist.all_reduce(self.item_grad, group=self.group, async_op=overlap)
         be.step_local_apply(batch_size if (pairs is None and self.draw_ahead) else 0)
-        work.wait()
+        if overlap:
+            work.wait()
         be.step_items()
 
 
