@@ -97,6 +97,9 @@ SIGNATURES = {
     "cf_profile_enable": (ctypes.c_int, [_P, _I32]),
     "cf_profile_read": (ctypes.c_int, [_P, _I32, _PD, _PI64]),
     "cf_profile_reset": (ctypes.c_int, [_P]),
+    "cf_ratings_load": (ctypes.c_int, [ctypes.c_char_p, _I64, _I64, _I32, ctypes.POINTER(_P), _PI64]),
+    "cf_ratings_csr": (ctypes.c_int, [_P, _I32, ctypes.c_double, _PI64, _PI32, _PD, _PI64]),
+    "cf_ratings_free": (ctypes.c_int, [_P]),
     "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
     "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),
 }

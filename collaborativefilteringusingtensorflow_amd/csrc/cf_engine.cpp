@@ -1488,3 +1488,8 @@ int cf_profile_reset(cf_engine* e) {
 }
 
 }  // extern "C"
+
+// errors of the other host translation units (cf_ingest.cpp)
+namespace cfi {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace cfi

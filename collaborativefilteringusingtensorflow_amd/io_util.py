@@ -8,12 +8,57 @@ Same names and rules:
 * ``matBinarize``: ``(R > threshold)`` as float32 (Util.py:15-16).
 
 Plus ``to_csr``: the sorted, duplicate-free CSR the engine consumes (the
-nnz order of ``trasR.nonzero()``, sampler_ranking.py:13).
+nnz order of ``trasR.nonzero()``, sampler_ranking.py:13), and ``load_csr``:
+file -> (binarised) CSR straight from the native parser (cf_ratings_load,
+include/cf_engine.h), without the lil_matrix detour.
+
+``loadSparseR`` parses with the native multi-threaded ingest
+(csrc/cf_ingest.cpp) and returns the lil_matrix the reference returns.
 """
+import ctypes
+
 import numpy as np
 import scipy.sparse as sp
 
-__all__ = ["split_row", "loadSparseR", "saveTriads", "matBinarize", "to_csr"]
+from . import _native as N
+
+__all__ = ["split_row", "loadSparseR", "saveTriads", "matBinarize", "to_csr", "load_csr"]
+
+
+def _ratings(path, n_users, n_items, n_threads=0):
+    L = N.lib()
+    h = ctypes.c_void_p()
+    nnz = ctypes.c_int64(0)
+    N.check(L.cf_ratings_load(str(path).encode(), int(n_users), int(n_items), int(n_threads),
+                              ctypes.byref(h), ctypes.byref(nnz)), "cf_ratings_load")
+    return L, h
+
+
+def _csr(L, h, n_users, binarize, threshold):
+    nnz = ctypes.c_int64(0)
+    N.check(L.cf_ratings_csr(h, 1 if binarize else 0, float(threshold), None, None, None,
+                             ctypes.byref(nnz)), "cf_ratings_csr")
+    indptr = np.zeros(int(n_users) + 1, dtype=np.int64)
+    indices = np.zeros(nnz.value, dtype=np.int32)
+    values = np.zeros(nnz.value, dtype=np.float64)
+    N.check(L.cf_ratings_csr(h, 1 if binarize else 0, float(threshold),
+                             indptr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                             indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                             values.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                             ctypes.byref(nnz)), "cf_ratings_csr")
+    return indptr, indices, values
+
+
+def load_csr(path, n_users, n_items, threshold=None, n_threads=0):
+    """Rating file -> CSR (indptr int64, indices int32 sorted per row).
+    With ``threshold``: matBinarize(loadSparseR(...), threshold)'s pattern;
+    without: (indptr, indices, ratings float64) of loadSparseR(...)."""
+    L, h = _ratings(path, n_users, n_items, n_threads)
+    try:
+        ip, ix, v = _csr(L, h, n_users, threshold is not None, threshold or 0.0)
+    finally:
+        L.cf_ratings_free(h)
+    return (ip, ix) if threshold is not None else (ip, ix, v)
 
 
 def split_row(row_content):
@@ -25,22 +70,9 @@ def split_row(row_content):
 
 
 def loadSparseR(usernum, itemnum, inFilePath):
-    entries = {}
-    with open(inFilePath, "r") as f:
-        for line in f:
-            fields = split_row(line)
-            if len(fields) == 2:
-                entries[(int(fields[0]), int(fields[1]))] = 1.0
-            elif len(fields) == 3:
-                entries[(int(fields[0]), int(fields[1]))] = float(fields[2])
-    R = sp.lil_matrix((usernum, itemnum))
-    if entries:
-        keys = np.array(list(entries.keys()), dtype=np.int64)
-        vals = np.array(list(entries.values()), dtype=np.float64)
-        coo = sp.coo_matrix((vals, (keys[:, 0], keys[:, 1])), shape=(usernum, itemnum))
-        coo.eliminate_zeros()  # assigning 0 into a lil_matrix stores nothing
-        R = sp.lil_matrix(coo)
-    return R
+    """IOUtil.py:8-16: the rating file as a (usernum x itemnum) lil_matrix."""
+    ip, ix, v = load_csr(inFilePath, usernum, itemnum)
+    return sp.lil_matrix(sp.csr_matrix((v, ix, ip), shape=(usernum, itemnum)))
 
 
 def saveTriads(triads, outFilePath, isRatingInt=False):

@@ -308,6 +308,21 @@ int cf_profile_read(cf_engine* eng, int32_t kernel_id,
                     double* total_ms_out, int64_t* launches_out);
 int cf_profile_reset(cf_engine* eng);
 
+/* ---- rating-file ingest ----------------------------------
+ * Native IOUtil.loadSparseR (src/utils/IOUtil.py:8-16) + Util.split_row /
+ * matBinarize (src/utils/Util.py:5-16), same rules: ',' else ';' else
+ * whitespace fields; 2 fields = 1, 3 fields = float(rating), others ignored;
+ * Python index wrap for negative ids; the last write of an entry wins; zeros
+ * are not stored.  cf_ratings_csr with binarize != 0 keeps entries with
+ * value > threshold as 1.0 (matBinarize); pass NULL indices/values first to
+ * size the output (nnz_out).  Host-only: needs no HIP device. */
+typedef struct cf_ratings cf_ratings;
+int cf_ratings_load(const char* path, int64_t n_users, int64_t n_items, int32_t n_threads,
+                    cf_ratings** out, int64_t* nnz_out);
+int cf_ratings_csr(const cf_ratings* r, int32_t binarize, double threshold, int64_t* indptr,
+                   int32_t* indices, double* values, int64_t* nnz_out);
+int cf_ratings_free(cf_ratings* r);
+
 /* ---- synthetic implicit-feedback graphs (bench configs) --------- */
 /*
  * Users [u_begin, u_end) of a graph with per-user degree 1 + Poisson(mean-1)
