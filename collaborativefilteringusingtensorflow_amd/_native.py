@@ -100,6 +100,11 @@ SIGNATURES = {
     "cf_ratings_load": (ctypes.c_int, [ctypes.c_char_p, _I64, _I64, _I32, ctypes.POINTER(_P), _PI64]),
     "cf_ratings_csr": (ctypes.c_int, [_P, _I32, ctypes.c_double, _PI64, _PI32, _PD, _PI64]),
     "cf_ratings_free": (ctypes.c_int, [_P]),
+    "cf_mt_sampler_create": (ctypes.c_int, [_PI64, _PI32, _I64, _I64, _I32, _I32, _I32, _I32,
+                                            ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "cf_mt_sampler_next": (ctypes.c_int, [_P, _PI32, _PI32, _PI32]),
+    "cf_mt_sampler_state": (ctypes.c_int, [_P, _PI64, _PI64]),
+    "cf_mt_sampler_free": (ctypes.c_int, [_P]),
     "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
     "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),
 }

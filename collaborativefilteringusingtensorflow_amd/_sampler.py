@@ -13,6 +13,7 @@ batches through ``next_batch`` at all: it runs the fused on-device
 sample+step loop from the sampler's seed and position, and hands the position
 back when done, so the stream continues where training left it.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -73,3 +74,56 @@ def negatives_valid(indptr, indices, pairs, negs):
         if np.isin(js, row).any():
             return False
     return True
+
+
+class MTSampler(object):
+    """Bit-exact host mode (cf_mt_sampler): the batch
+    stream the reference sampler produces after ``np.random.seed(seed)``,
+    restated in C++ (numpy's legacy MT19937 shuffle / randint / choice).
+    Models feed it host-side (cf_step), like any ``next_batch()`` object."""
+
+    KIND = 0
+
+    def __init__(self, trasR, n_neg=5, batch_size=100, gsize=0, seed=0):
+        self.indptr, self.indices, shape = to_csr(trasR)
+        self.n_users, self.n_items = int(shape[0]), int(shape[1])
+        self.batch_size, self.n_neg, self.gsize = int(batch_size), int(n_neg), int(gsize)
+        if not 0 <= int(seed) < 2 ** 32:
+            raise ValueError("Seed must be between 0 and 2**32 - 1")  # np.random.seed's rule
+        self._L = N.lib()
+        self._h = ctypes.c_void_p()
+        ip = np.ascontiguousarray(self.indptr, dtype=np.int64)
+        ix = np.ascontiguousarray(self.indices, dtype=np.int32)
+        N.check(self._L.cf_mt_sampler_create(ip.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                             ix.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                             self.n_users, self.n_items, self.KIND, self.n_neg,
+                                             self.gsize, self.batch_size, int(seed),
+                                             ctypes.byref(self._h)), "cf_mt_sampler_create")
+
+    def _draw(self):
+        B, W, G = self.batch_size, self.n_neg, self.gsize
+        pairs = np.empty((B, 2), dtype=np.int32)
+        negs = np.empty((B, W), dtype=np.int32)
+        groups = np.empty((B, max(G, 1)), dtype=np.int32) if G else None
+        P = ctypes.POINTER(ctypes.c_int32)
+        N.check(self._L.cf_mt_sampler_next(self._h, pairs.ctypes.data_as(P), negs.ctypes.data_as(P),
+                                           groups.ctypes.data_as(P) if G else None),
+                "cf_mt_sampler_next")
+        return pairs, negs, groups
+
+    def state(self):
+        e, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._L.cf_mt_sampler_state(self._h, ctypes.byref(e), ctypes.byref(b)),
+                "cf_mt_sampler_state")
+        return int(e.value), int(b.value)
+
+    def close(self):
+        if self._h:
+            self._L.cf_mt_sampler_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,23 +1,52 @@
 """Fold loop shared by the drivers (testbprmf.py:55-125 and siblings).
 
-The reference runs folds in a ``multiprocessing.Pool`` of forked processes.
-A forked child must not inherit an initialised HIP runtime, so folds here run
-either sequentially in this process or in *spawned* processes, fold k on HIP
-device k % n_devices.
+The reference runs folds in a ``multiprocessing.Pool`` of forked processes
+(testbprmf.py:113-125).  Here the folds are independent GPU replicas (SURVEY
+8(f) row 2): with ``parallel`` each fold runs in its own *spawned* process
+(a forked child must not inherit an initialised HIP runtime) pinned to HIP
+device fold % n_devices through CF_DEVICE, so 5 folds train concurrently on a
+node's GPUs; otherwise they run one after another in this process.  The
+report is the reference's ave@N / std@N line.
 """
 import multiprocessing
+import os
 import sys
 
 import numpy as np
 
 
-def run_folds(worker, n_users, n_items, dataset_dir, folds, topN, eval_metrics, parallel=False):
+def _fold_entry(worker, fold, device, n_users, n_items, dataset_dir, q):
+    os.environ["CF_DEVICE"] = str(device)
+    try:
+        q.put((fold, list(worker(fold, n_users, n_items, dataset_dir)), None))
+    except BaseException as ex:  # reported to the parent, which raises
+        q.put((fold, None, "%s: %s" % (type(ex).__name__, ex)))
+
+
+def run_folds(worker, n_users, n_items, dataset_dir, folds, topN, eval_metrics, parallel=False,
+              n_devices=None):
     if parallel:
+        if n_devices is None:
+            from .. import _native as N
+            n_devices = max(1, N.device_count())
         ctx = multiprocessing.get_context("spawn")
-        with ctx.Pool(processes=folds) as pool:
-            results = [pool.apply_async(worker, (f, n_users, n_items, dataset_dir))
-                       for f in range(folds)]
-            scores = np.array([r.get() for r in results])
+        q = ctx.Queue()
+        procs = [ctx.Process(target=_fold_entry,
+                             args=(worker, f, f % n_devices, n_users, n_items, dataset_dir, q))
+                 for f in range(folds)]
+        for p in procs:
+            p.start()
+        got = {}
+        for _ in range(folds):
+            f, sc, err = q.get()
+            if err is not None:
+                for p in procs:
+                    p.join()
+                raise RuntimeError("fold %d failed: %s" % (f + 1, err))
+            got[f] = sc
+        for p in procs:
+            p.join()
+        scores = np.array([got[f] for f in range(folds)])
     else:
         scores = np.array([worker(f, n_users, n_items, dataset_dir) for f in range(folds)])
     aves = scores.sum(0) / len(scores)

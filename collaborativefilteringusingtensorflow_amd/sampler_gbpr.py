@@ -7,7 +7,7 @@ Drawn on the GPU.
 """
 import numpy as np
 
-from ._sampler import DeviceSampler
+from ._sampler import DeviceSampler, MTSampler
 
 
 class Sampler(DeviceSampler):
@@ -21,3 +21,19 @@ class Sampler(DeviceSampler):
     def next_batch(self):
         pairs, negs, groups = self._draw()
         return pairs.astype(np.int32), negs.astype(np.int64), groups.astype(np.int64)
+
+
+class ExactSampler(MTSampler):
+    """Bit-exact host mode: the reference's stream for ``np.random.seed(seed)``
+    (sampler_gbpr.py:23-43), same ``next_batch`` types."""
+    KIND = 2
+
+    def __init__(self, trasR, gsize=2, n_neg=5, batch_size=100, n_workers=1, seed=0):
+        if gsize < 1:
+            raise ValueError("gsize must be >= 1")
+        super(ExactSampler, self).__init__(trasR, n_neg=n_neg, batch_size=batch_size,
+                                           gsize=gsize, seed=seed)
+
+    def next_batch(self):
+        pairs, negs, groups = self._draw()
+        return pairs, negs.astype(np.int64), groups.astype(np.int64)

@@ -323,6 +323,21 @@ int cf_ratings_csr(const cf_ratings* r, int32_t binarize, double threshold, int6
                    int32_t* indices, double* values, int64_t* nnz_out);
 int cf_ratings_free(cf_ratings* r);
 
+/* ---- bit-exact host sampler ------------------------------
+ * The reference samplers' batch stream for np.random.seed(seed) set right
+ * before the sampler is built (sampler_ranking.py:22-37 kind 0,
+ * sampler_uij_ranking.py:22-38 kind 1, sampler_gbpr.py:23-43 kind 2):
+ * numpy's legacy MT19937 RandomState shuffle / randint / choice restated
+ * (csrc/cf_mt_sampler.cpp).  Host batches, fed with cf_step. */
+typedef struct cf_mt_sampler cf_mt_sampler;
+int cf_mt_sampler_create(const int64_t* indptr, const int32_t* indices, int64_t n_users,
+                         int64_t n_items, int32_t kind, int32_t n_neg, int32_t gsize,
+                         int32_t batch_size, uint32_t seed, cf_mt_sampler** out);
+int cf_mt_sampler_next(cf_mt_sampler* s, int32_t* pairs /*[B,2]*/, int32_t* negs /*[B,W]*/,
+                       int32_t* groups /*[B,G] | NULL*/);
+int cf_mt_sampler_state(const cf_mt_sampler* s, int64_t* epoch_out, int64_t* batch_out);
+int cf_mt_sampler_free(cf_mt_sampler* s);
+
 /* ---- synthetic implicit-feedback graphs (bench configs) --------- */
 /*
  * Users [u_begin, u_end) of a graph with per-user degree 1 + Poisson(mean-1)

@@ -1,8 +1,9 @@
 """End-to-end GPU tests of the drop-in model classes, and full-size parity.
 
 * cfg1 (BASELINE configs[0]): BPRMF on ml-100k fold 1, d=32, the testbprmf.py
-  hyper-parameters (reg=.1, B=100, W=1, topN=10, 50 epochs), fed the SAME
-  batch stream and initial tables as the CPU oracle (oracle/cf_oracle.c,
+  hyper-parameters (reg=.1, B=100, W=1, topN=10, 50 epochs), fed the
+  reference sampler's own stream for np.random.seed(11) (bit-exact host
+  sampler) and the same initial tables as the CPU oracle (oracle/cf_oracle.c,
   fp32): ranking metrics after training must agree within 0.2 % (north star).
 * the same drivers' device-sampled path trains (metrics far above random).
 * cfg2 at full size (1M users x 100K items, d=64, B=65,536): one step on a
@@ -54,8 +55,13 @@ def test_cfg1_bprmf_metrics_match_oracle(fold1, epochs):
     B, d, reg, topN = 100, 32, 0.1, 10
     metrics = ['pre', 'recall', 'map', 'mrr', 'ndcg']
     n_batches = len(ix) // B
-    rng = np.random.RandomState(2026)
-    batches = list(O.sample_stream(ip, ix, 1682, B, 1, n_batches * epochs, rng))
+    # the reference's own sampler stream for np.random.seed(11) (bit-exact
+    # host mode, pinned to the captured reference batches in test_exact_sampler)
+    from collaborativefilteringusingtensorflow_amd.sampler_ranking import ExactSampler
+    tra, tst = matrices(fold1)
+    es = ExactSampler(tra, n_neg=1, batch_size=B, seed=11)
+    batches = [es.next_batch() for _ in range(n_batches * epochs)]
+    es.close()
     init_rng = np.random.RandomState(11)
     U0 = O.init_table(init_rng, (943, d))
     V0 = O.init_table(init_rng, (1682, d))
@@ -66,12 +72,11 @@ def test_cfg1_bprmf_metrics_match_oracle(fold1, epochs):
         c.step(pairs, negs)
     ref = oracle_metrics(c.U, c.V, fold1, topN, metrics)
 
-    # GPU: the drop-in model class, host-fed with the same stream
-    tra, tst = matrices(fold1)
+    # GPU: the drop-in model class fed by the exact sampler itself
     model = BPRMF(943, 1682, topN, 'cv', metrics, reg, d, B, max_iter=epochs, seed=5,
                   verbose=False)
     model.set_initial_tables(user=U0, item=V0)
-    got = model.train(1, tra, tst, ListSampler(batches))
+    got = model.train(1, tra, tst, ExactSampler(tra, n_neg=1, batch_size=B, seed=11))
     drift_u = np.abs(model.engine.get_table("user") - c.U).max() / np.abs(c.U).max()
     model.close()
     print("oracle", ref, "gpu", got, "table drift", drift_u)
@@ -168,3 +173,23 @@ def test_driver_worker_end_to_end(fold1, tmp_path):
     finally:
         testbprmf.n_factors = old
     assert len(scores) == 5 and scores[4] > 0.2   # ndcg@10 after 50 epochs
+
+
+def test_fold_parallel_driver_replicas(fold1, tmp_path):
+    """run_folds(parallel=True): folds as independent spawned GPU replicas
+    (CF_DEVICE = fold % devices) with the reference's ave@N / std@N report
+    (testbprmf.py:113-125); two copies of fold 1 give identical-data replicas."""
+    from collaborativefilteringusingtensorflow_amd.drivers import testbprmf
+    from collaborativefilteringusingtensorflow_amd.drivers._common import run_folds
+    for fold in (1, 2):
+        for tag in ("train", "test"):
+            ip, ix = fold1[tag + "_indptr"], fold1[tag + "_indices"]
+            name = "ratings__%d_%s.txt" % (fold, "tra" if tag == "train" else "tst")
+            with open(tmp_path / name, "w") as f:
+                for u in range(943):
+                    for it in ix[ip[u]:ip[u + 1]]:
+                        f.write("%d\t%d\t4.0\n" % (u, it))
+    aves, stds = run_folds(testbprmf.worker, 943, 1682, str(tmp_path) + "/", 2, 10,
+                           testbprmf.eval_metrics, parallel=True)
+    assert aves.shape == (5,) and aves[4] > 0.2
+    assert np.all(stds <= 0.01)          # same data, same seeds: replicas agree
