@@ -961,7 +961,12 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
 }
 
 template <int MODEL, int EPL, int WT, int P>
-__global__ __launch_bounds__(kBlock) void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
+#ifdef CF_GRAD_WAVES_PER_EU
+#define CF_GRAD_ATTR __attribute__((amdgpu_waves_per_eu(CF_GRAD_WAVES_PER_EU, 8)))
+#else
+#define CF_GRAD_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
     int idx;
     if (minor_block(blockIdx.x, ng, np, idx))
         prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
@@ -1405,7 +1410,7 @@ static int epl_for(int d) {
 }
 
 #ifndef CF_FAST_PAIRS_W1
-#define CF_FAST_PAIRS_W1 2
+#define CF_FAST_PAIRS_W1 1  // cfg2 grad: P=1 44.2 us, P=2 49.8, P=3 55.6, P=4 61.9 (occupancy wins)
 #endif
 #ifndef CF_FAST_PAIRS_W5
 #define CF_FAST_PAIRS_W5 1
