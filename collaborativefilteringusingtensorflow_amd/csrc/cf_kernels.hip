@@ -253,10 +253,25 @@ __device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t
 // ---------------------------------------------------------------------------
 // prep: sample (or load) the batch and count row occurrences
 // ---------------------------------------------------------------------------
+// The draw runs 8 lanes per pair (32 pairs per block): one wave generation
+// covers a 65,536-pair batch at full occupancy, and a user's row (~51 ids at
+// cfg2) is tested in one batch of up to 8 independent 32-B loads.
+constexpr int kPrepGL = 8;
+constexpr int kPrepPairsPerBlock = kBlock / kPrepGL;
+constexpr int kPrepChunks = 8;   // row chunks in flight per candidate test
+
+__device__ __forceinline__ uint32_t gor8(uint32_t v) {
+    v |= (uint32_t)__shfl_xor((int)v, 4, 64);
+    v |= (uint32_t)__shfl_xor((int)v, 2, 64);
+    v |= (uint32_t)__shfl_xor((int)v, 1, 64);
+    return v;
+}
+
 template <int MODEL>
 __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
-    const int gl = threadIdx.x & (kGL - 1);
-    const int p = block * kGroupsPerBlock + (threadIdx.x >> 4);
+    constexpr int PGL = kPrepGL;
+    const int gl = threadIdx.x & (PGL - 1);
+    const int p = block * kPrepPairsPerBlock + (threadIdx.x / PGL);
     if (p >= a.B) return;  // whole group leaves; no block barrier below
     const int W = a.W;
     const int G = (MODEL == GBPR) ? a.G : 0;
@@ -279,9 +294,9 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         u = a.occU[p];
         i = a.occV[p];
     }
-    const int nchunk = (int)((re - rb + kGL - 1) / kGL);
-    for (int w0 = 0; w0 < W; w0 += kGL) {
-        const int nw = (W - w0 < kGL) ? (W - w0) : kGL;
+    const int nchunk = (int)((re - rb + PGL - 1) / PGL);
+    for (int w0 = 0; w0 < W; w0 += PGL) {
+        const int nw = (W - w0 < PGL) ? (W - w0) : PGL;
         const int w = w0 + gl;
         int32_t j = -1;
         if (a.sample) {
@@ -289,18 +304,26 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             // (sampler_ranking.py:30-36); lane w owns candidate w
             uint64_t ctr = (uint64_t)w << 32;
             if (gl < nw) j = draw_item(key, ctr++, a.n_items);
-            uint32_t pending = (nw >= 32) ? 0xFFFFFFFFu : ((1u << nw) - 1u);
+            uint32_t pending = (1u << nw) - 1u;
             for (;;) {
+                int32_t cand[PGL];
+#pragma unroll
+                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
                 uint32_t hit = 0;
-                for (int c = 0; c < nchunk; ++c) {
-                    const int64_t t = rb + (int64_t)c * kGL + gl;
-                    const int32_t el = (t < re) ? a.indices[t] : -1;
-                    for (int k = 0; k < nw; ++k) {
-                        const int32_t cand = __shfl(j, k, kGL);
-                        hit |= (el == cand) ? (1u << k) : 0u;
+                for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
+                    int32_t el[kPrepChunks];
+#pragma unroll
+                    for (int q = 0; q < kPrepChunks; ++q) {
+                        const int64_t t = rb + (int64_t)(c0 + q) * PGL + gl;
+                        el[q] = (t < re) ? a.indices[t] : -1;
                     }
+#pragma unroll
+                    for (int q = 0; q < kPrepChunks; ++q)
+#pragma unroll
+                        for (int k = 0; k < PGL; ++k)
+                            hit |= (k < nw && el[q] == cand[k]) ? (1u << k) : 0u;
                 }
-                hit = gor(hit) & pending;
+                hit = gor8(hit) & pending;
                 if (hit == 0u) break;  // group-uniform
                 if ((hit >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
                 pending = hit;
@@ -311,22 +334,24 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         }
         if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
     }
-    if (MODEL == GBPR && gl < G) {
-        int32_t g;
-        if (a.sample) {
-            // group = np.random.choice(item_posUserList[i], gsize): uniform,
-            // with replacement, may contain u (sampler_gbpr.py:41)
-            const int64_t cb = a.indptr_t[i], ce = a.indptr_t[i + 1];
-            const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + gl) << 32));
-            g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
-            // user-sharded engine: the item's users are global ids; one owned
-            // by another rank is coded -1 - id (fetched by the group exchange)
-            g = (g >= a.shard_u0 && g < a.shard_u1) ? g - a.shard_u0 : -1 - g;
-            a.occU[B + p * G + gl] = g;
-        } else {
-            g = a.occU[B + p * G + gl];
+    if (MODEL == GBPR) {
+        for (int k = gl; k < G; k += PGL) {
+            int32_t g;
+            if (a.sample) {
+                // group = np.random.choice(item_posUserList[i], gsize): uniform,
+                // with replacement, may contain u (sampler_gbpr.py:41)
+                const int64_t cb = a.indptr_t[i], ce = a.indptr_t[i + 1];
+                const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + k) << 32));
+                g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
+                // user-sharded engine: the item's users are global ids; one
+                // owned by another rank is coded -1 - id (fetched by the group exchange)
+                g = (g >= a.shard_u0 && g < a.shard_u1) ? g - a.shard_u0 : -1 - g;
+                a.occU[B + p * G + k] = g;
+            } else {
+                g = a.occU[B + p * G + k];
+            }
+            if (a.count_users && g >= 0) a.rankU[B + p * G + k] = atomicAdd(&a.cntU[g], 1);
         }
-        if (a.count_users && g >= 0) a.rankU[B + p * G + gl] = atomicAdd(&a.cntU[g], 1);
     }
     if (gl == 0) {
         if (a.sample) {
@@ -1435,7 +1460,7 @@ int grad_blocks_max(int B) { return (B + kGroupsPerBlock - 1) / kGroupsPerBlock;
 
 hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    const int blocks = (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    const int blocks = (a.B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock;
     switch (a.model) {
         case GBPR: hipLaunchKernelGGL(prep_kernel<GBPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
         default: hipLaunchKernelGGL(prep_kernel<BPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
@@ -1444,7 +1469,7 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
 }
 
 static int prep_blocks(const StepArgs* nx) {
-    return (nx && nx->B > 0) ? (nx->B + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
+    return (nx && nx->B > 0) ? (nx->B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock : 0;
 }
 
 template <int MODEL, int WT>
@@ -1543,7 +1568,7 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
 template <int MODEL>
 static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     const int na = apply_grid(p);
-    const int np = (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    const int np = (a.B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock;
     const dim3 grid(na + np), block(kBlock);
     switch (epl_for(p.d)) {
         case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL>), grid, block, 0, s, p, a, na); break;
