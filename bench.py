@@ -145,8 +145,7 @@ def main():
     ap.add_argument("--prep-stream", type=int, default=0,
                     help="cf_set_option prep_stream: 0 in-order (default), 1 side stream")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="cf_set_option pipeline: 2 grad(s)+draw(s+1), apply(s)+slots(s+1) (default); "
-                         "1 apply(s)+draw(s+1); 0 stepwise")
+                    help="cf_set_option pipeline: 1 apply(s)+draw(s+1) (default); 0 stepwise")
     ap.add_argument("--slot-max", type=int, default=0,
                     help="cf_set_option slot_max (0 = engine default)")
     ap.add_argument("--n-users", type=int, default=0, help="override the config's users (rehearsals)")
@@ -238,7 +237,7 @@ def main():
     eng.profile_reset()
     # pipeline 2 (default): the dominant launch is the gradient of step s fused
     # with the draw + count of step s+1 ("grad_prep"); otherwise "step"
-    dom = "grad_prep" if (world == 1 and args.pipeline == 2) else "step"
+    dom = "step"
     eng.set_option("profile_mask", 1 << KERNELS[dom])
     eng.profile(not args.no_profile)
     sync()

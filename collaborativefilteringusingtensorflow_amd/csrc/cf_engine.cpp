@@ -78,23 +78,15 @@ struct cf_engine {
     float *GV_own = nullptr, *Gb_own = nullptr;
     int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
     int32_t* cntV_[2] = {nullptr, nullptr};
-    // store-and-sum of duplicated rows (slot_kernel): slot base per row, the
-    // duplicate list (global row ids), [slots used, |dup|] -- one set per batch
-    // buffer set, so that the slot pass of step s+1 can run beside the apply
-    // of step s -- and the slot kernel's per-block status words
-    // [2 launches][kSlotMaxBlocks]
-    int32_t* offU_[2] = {nullptr, nullptr};
-    int32_t* offV_[2] = {nullptr, nullptr};
-    int32_t* dup_[2] = {nullptr, nullptr};
-    int32_t* ctl_[2] = {nullptr, nullptr};
-    uint64_t* status = nullptr;
-    int status_par = 0;
-    float* slotG = nullptr;   // [slot_cap, d]
-    size_t slot_cap = 0;
-    int slot_max = 32;        // cf_set_option("slot_max")
-    // cf_set_option("pipeline") for cf_train_steps: 0 = four launches per
-    // step (prep, slot, grad, apply); 1 = apply(s) + prep(s+1) fused;
-    // 2 = grad(s) + prep(s+1) and apply(s) + slot(s+1) fused (two launches)
+    // store-and-sum of duplicated rows: row r of a table owns the fixed slot
+    // rows [r*cap, (r+1)*cap) (cf_set_option "slot_max" = item cap,
+    // "slot_max_user" = user cap); rows above their cap use float atomics
+    float* slotU = nullptr;   // [n_users * capU, d]
+    float* slotV = nullptr;   // [n_items * capV, d]
+    int capU = 2, capV = 32;
+    bool slots_ready = false;
+    // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
+    // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches)
     int pipeline = 1;
 
     // batch: two buffer sets, so that the sampler of step s+1 runs on the side
@@ -131,6 +123,7 @@ struct cf_engine {
     int32_t* xcounts = nullptr;      // [world + 1] device
     int32_t* h_xcounts = nullptr;    // pinned mirror
     int32_t *x_send_ids = nullptr, *x_recv_ids = nullptr;             // bound (caller) buffers
+    int32_t* x_own = nullptr;        // [recv cap] served row applies it (first server, no local occurrence)
     float *x_rows = nullptr, *x_grads = nullptr, *x_serve_rows = nullptr, *x_serve_grads = nullptr;
     int64_t x_send_cap = 0, x_recv_cap = 0;
     int x_stage = 0;                 // 0 idle, 1 begun, 2 served, 3 grads done
@@ -210,7 +203,20 @@ int users_per_pair(const cf_config& c) { return c.model == CF_GBPR ? 1 + c.gsize
 int items_per_pair(const cf_config& c) { return 1 + c.n_neg; }
 int group_count(const cf_config& c) { return c.model == CF_GBPR ? c.gsize : 0; }
 
+int ensure_slots(cf_engine* e) {
+    if (e->slots_ready) return CF_OK;
+    const cf_config& c = e->cfg;
+    CF_HIP(hipStreamSynchronize(e->stream));
+    dfree(e->slotU);
+    dfree(e->slotV);
+    CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
+    if (!c.dense_item_apply) CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+    e->slots_ready = true;
+    return CF_OK;
+}
+
 int ensure_batch(cf_engine* e, int B) {
+    CF_TRY(ensure_slots(e));
     if (B <= e->Bcap) return CF_OK;
     CF_HIP(hipStreamSynchronize(e->stream));
     CF_HIP(hipStreamSynchronize(e->side));
@@ -227,10 +233,6 @@ int ensure_batch(cf_engine* e, int B) {
         CF_TRY(dalloc(&e->rankU_[k], nU));
         CF_TRY(dalloc(&e->rankV_[k], nV));
     }
-    // every occurrence of a duplicated row may need a slot row
-    dfree(e->slotG);
-    e->slot_cap = nU + nV;
-    CF_TRY(dalloc(&e->slotG, e->slot_cap * (size_t)e->cfg.n_factors));
     CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks_max(B)));
     e->Bcap = B;
     return CF_OK;
@@ -271,10 +273,10 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.cntV = e->cntV_[k];
     a.rankU = e->rankU_[k];
     a.rankV = e->rankV_[k];
-    a.offU = e->offU_[k];
-    a.offV = e->offV_[k];
-    a.slotG = e->slotG;
-    a.slot_max = e->slot_max;
+    a.slotU = e->slotU;
+    a.slotV = e->slotV;
+    a.capU = e->capU;
+    a.capV = e->capV;
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
     a.count_items = c.dense_item_apply ? 0 : 1;
@@ -383,27 +385,6 @@ int begin_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
 // Adagrad), duplicate apply (+ CML clip).  With `next`, the apply launch also
 // draws and counts the next step's batch (launch_apply_prep).  Loss added to
 // *loss_acc.
-// slot pass arguments of the step in buffer set k (counts complete)
-SlotArgs slot_args(cf_engine* e, const StepArgs& a, int k) {
-    const cf_config& c = e->cfg;
-    SlotArgs sa{};
-    sa.n_users = c.n_users;
-    sa.n_items = c.n_items;
-    sa.count_users = a.count_users;
-    sa.count_items = a.count_items;
-    sa.slot_max = e->slot_max;
-    sa.cntU = a.cntU;
-    sa.cntV = a.cntV;
-    sa.offU = e->offU_[k];
-    sa.offV = e->offV_[k];
-    sa.dup = e->dup_[k];
-    sa.status = e->status + (size_t)kSlotMaxBlocks * e->status_par;
-    sa.status_next = e->status + (size_t)kSlotMaxBlocks * (e->status_par ^ 1);
-    sa.ctl = e->ctl_[k];
-    e->status_par ^= 1;
-    return sa;
-}
-
 ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc) {
     const cf_config& c = e->cfg;
     ApplyArgs p{};
@@ -411,24 +392,24 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
     p.clip = c.model == CF_CML ? 1 : 0;
-    p.slot_max = e->slot_max;
-    p.ctl = e->ctl_[k];
-    p.dup = e->dup_[k];
-    p.n_users = c.n_users;
-    p.offU = e->offU_[k];
-    p.offV = e->offV_[k];
-    p.slotG = e->slotG;
+    p.capU = e->capU;
+    p.capV = e->capV;
+    p.count_users = a.count_users;
+    p.count_items = a.count_items;
+    p.occU = e->occU_[k];
+    p.rankU = e->rankU_[k];
+    p.nU = (int64_t)B * users_per_pair(c);
+    p.occV = e->occV_[k];
+    p.rankV = e->rankV_[k];
+    p.nV = (int64_t)B * items_per_pair(c);
+    p.shard_u0 = e->shard_u0;
+    p.slotU = e->slotU;
+    p.slotV = e->slotV;
     p.cntU = e->cntU_[k];
     p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
     p.V = e->V; p.AV = e->AV; p.GV = e->GV;
     p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
-    {
-        const int64_t occU = (int64_t)B * users_per_pair(c), occV = (int64_t)B * items_per_pair(c);
-        const int64_t mu = std::min<int64_t>(c.n_users, occU / 2);
-        const int64_t mv = a.count_items ? std::min<int64_t>(c.n_items, occV / 2) : 0;
-        p.max_groups = (int)(mu + mv);
-    }
     p.loss_partial = e->loss_partial;
     p.n_partial = grad_blocks(a);
     p.loss_acc = loss_acc;
@@ -453,11 +434,6 @@ int pending_clips(cf_engine* e) {
 
 int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
-    {
-        SlotArgs sa = slot_args(e, a, k);
-        ProfScope pr(e, CF_K_SLOT);
-        CF_HIP(launch_slots(sa, e->stream));
-    }
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
@@ -503,42 +479,6 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
     if (e->prep_side) CF_HIP(hipStreamWaitEvent(e->stream, e->apply_done[k], 0));
     StepArgs a;
     CF_TRY(begin_step(e, B, nullptr, nullptr, nullptr, k, e->stream, &a));
-    if (e->pipeline == 2) {
-        // two launches per step: grad(s) | draw(s+1), then apply(s) | slots(s+1)
-        {
-            SlotArgs sa = slot_args(e, a, k);
-            ProfScope pr(e, CF_K_SLOT);
-            CF_HIP(launch_slots(sa, e->stream));
-        }
-        for (int s = 0; s < n; ++s) {
-            StepArgs nx{};
-            const bool more = s + 1 < n;
-            if (more) {
-                nx = base_step_args(e, B, k ^ 1);
-                CF_TRY(sampler_args(e, B, &nx));
-            }
-            {
-                ProfScope ps(e, more ? CF_K_GRAD_PREP : CF_K_STEP);
-                CF_HIP(launch_grad(a, e->stream, more ? &nx : nullptr));
-            }
-            ApplyArgs p = apply_args(e, a, B, k, loss_acc);
-            if (more) {
-                SlotArgs sa = slot_args(e, nx, k ^ 1);
-                ProfScope ps(e, CF_K_APPLY_SLOT);
-                CF_HIP(launch_apply_slots(p, sa, e->stream));
-            } else {
-                ProfScope ps(e, CF_K_APPLY);
-                CF_HIP(launch_apply(p, e->stream));
-            }
-            CF_TRY(pending_clips(e));
-            a = nx;
-            k ^= 1;
-        }
-        if (e->prep_side)
-            for (int q = 0; q < 2; ++q) CF_HIP(hipEventRecord(e->apply_done[q], e->stream));
-        e->set = k;
-        return CF_OK;
-    }
     for (int s = 0; s < n; ++s) {
         StepArgs nx{};
         const bool more = s + 1 < n;
@@ -755,12 +695,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         (r = dalloc(&e->V, id)) || (r = dalloc(&e->AV, id)) || (r = dalloc(&e->GV_own, id)) ||
         (r = dalloc(&e->cntU_[0], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[0], (size_t)c.n_items)) ||
         (r = dalloc(&e->cntU_[1], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[1], (size_t)c.n_items)) ||
-        (r = dalloc(&e->offU_[0], (size_t)c.n_users)) || (r = dalloc(&e->offV_[0], (size_t)c.n_items)) ||
-        (r = dalloc(&e->offU_[1], (size_t)c.n_users)) || (r = dalloc(&e->offV_[1], (size_t)c.n_items)) ||
-        (r = dalloc(&e->dup_[0], (size_t)(c.n_users + c.n_items))) ||
-        (r = dalloc(&e->dup_[1], (size_t)(c.n_users + c.n_items))) ||
-        (r = dalloc(&e->status, 2 * (size_t)kSlotMaxBlocks)) ||
-        (r = dalloc(&e->ctl_[0], 4)) || (r = dalloc(&e->ctl_[1], 4)) || (r = dalloc(&e->loss, 2)))
+        (r = dalloc(&e->loss, 2)))
         return bail(r);
     if (c.model == CF_GBPR) {
         if ((r = dalloc(&e->b, (size_t)c.n_items)) || (r = dalloc(&e->Ab, (size_t)c.n_items)) ||
@@ -781,13 +716,6 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         hipMemsetAsync(e->cntV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
         hipMemsetAsync(e->cntV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offU_[0], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offV_[0], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offU_[1], 0, (size_t)c.n_users * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->offV_[1], 0, (size_t)c.n_items * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->ctl_[0], 0, 4 * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->ctl_[1], 0, 4 * 4, s) != hipSuccess ||
-        hipMemsetAsync(e->status, 0, 2 * kSlotMaxBlocks * sizeof(uint64_t), s) != hipSuccess ||
         hipMemsetAsync(e->loss, 0, 2 * sizeof(double), s) != hipSuccess)
         return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
     if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
@@ -822,12 +750,11 @@ int cf_destroy(cf_engine* e) {
     for (int k = 0; k < 2; ++k) {
         dfree(e->cntU_[k]); dfree(e->cntV_[k]); dfree(e->occU_[k]); dfree(e->occV_[k]);
         dfree(e->rankU_[k]); dfree(e->rankV_[k]);
-        dfree(e->offU_[k]); dfree(e->offV_[k]); dfree(e->dup_[k]); dfree(e->ctl_[k]);
         if (e->prep_done[k]) (void)hipEventDestroy(e->prep_done[k]);
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
-    dfree(e->status); dfree(e->slotG);
+    dfree(e->slotU); dfree(e->slotV); dfree(e->x_own);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -1106,11 +1033,6 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
     }
     {
-        SlotArgs sa = slot_args(e, a, k);
-        ProfScope pr(e, CF_K_SLOT);
-        CF_HIP(launch_slots(sa, e->stream));
-    }
-    {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
@@ -1243,6 +1165,8 @@ int cf_bind_exchange(cf_engine* e, void* send_ids, void* rows, void* grads, int6
     e->x_recv_ids = (int32_t*)recv_ids;
     e->x_serve_rows = (float*)serve_rows;
     e->x_serve_grads = (float*)serve_grads;
+    dfree(e->x_own);
+    CF_TRY(dalloc(&e->x_own, (size_t)(recv_cap > 0 ? recv_cap : 1)));
     e->x_recv_cap = recv_cap;
     return CF_OK;
 }
@@ -1299,7 +1223,8 @@ int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
 int cf_xchg_serve(cf_engine* e, int64_t n_recv) {
     CF_TRY(check_xchg(e, 1));
     if (n_recv < 0 || n_recv > e->x_recv_cap) return fail(CF_EINVAL, "n_recv exceeds the bound receive capacity");
-    CF_HIP(launch_xchg_serve(e->x_recv_ids, n_recv, e->shard_u0, e->cntU_[e->x_set], e->U, e->x_serve_rows,
+    CF_HIP(launch_xchg_serve(e->x_recv_ids, n_recv, e->shard_u0, e->cntU_[e->x_set], e->x_own, e->U,
+                             e->x_serve_rows,
                              e->cfg.n_factors, e->stream));
     e->x_stage = 2;
     return CF_OK;
@@ -1308,11 +1233,6 @@ int cf_xchg_serve(cf_engine* e, int64_t n_recv) {
 int cf_xchg_grad(cf_engine* e) {
     CF_TRY(check_xchg(e, 2));
     const StepArgs& a = e->x_args;
-    {
-        SlotArgs sa = slot_args(e, a, e->x_set);
-        ProfScope pr(e, CF_K_SLOT);
-        CF_HIP(launch_slots(sa, e->stream));
-    }
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
@@ -1327,6 +1247,9 @@ int cf_xchg_finish(cf_engine* e, int64_t n_recv) {
     CF_HIP(launch_xchg_accumulate(e->x_recv_ids, n_recv, e->shard_u0, e->x_serve_grads, e->GU,
                                   e->cfg.n_factors, e->stream));
     ApplyArgs p = apply_args(e, e->x_args, e->x_B, e->x_set, e->loss);
+    p.served_ids = e->x_recv_ids;   // served rows with no local occurrence apply here
+    p.served_own = e->x_own;
+    p.nS = n_recv;
     {
         ProfScope ps(e, CF_K_APPLY);
         CF_HIP(launch_apply(p, e->stream));
@@ -1435,14 +1358,16 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "pipeline") {
-        if (value < 0 || value > 2) return fail(CF_EINVAL, "pipeline must be 0, 1 or 2");
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "pipeline must be 0 or 1");
         e->pipeline = (int)value;
         return CF_OK;
     }
-    if (n == "slot_max") {
-        if (value < 1 || value > (1 << 20)) return fail(CF_EINVAL, "slot_max must be in [1, 2^20]");
+    if (n == "slot_max" || n == "slot_max_user") {
+        if (value < 1 || value > 256) return fail(CF_EINVAL, n + " must be in [1, 256]");
+        CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
-        e->slot_max = (int)value;
+        if (n == "slot_max") e->capV = (int)value; else e->capU = (int)value;
+        e->slots_ready = false;   // re-sized at the next step
         return CF_OK;
     }
     if (n == "grad_path") {

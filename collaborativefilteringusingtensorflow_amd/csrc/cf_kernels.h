@@ -72,14 +72,12 @@ struct StepArgs {
     int32_t* __restrict__ cntU;   // [n_users] occurrences in this batch (0 between steps)
     int32_t* __restrict__ cntV;   // [n_items]
     // duplicated rows (store-and-sum): occurrence rank inside its row (prep's
-    // returning count atomic), slot base of each row with 2..slot_max
-    // occurrences (slot_kernel), one gradient row per slot
+    // returning count atomic); row r owns the slot rows [r*cap, (r+1)*cap)
     int32_t* __restrict__ rankU;  // [B*(1+G)]
     int32_t* __restrict__ rankV;  // [B*(1+W)]
-    const int32_t* __restrict__ offU;  // [n_users]
-    const int32_t* __restrict__ offV;  // [n_items]
-    float* __restrict__ slotG;    // [slot capacity, d]
-    int slot_max;                 // rows above this many occurrences use float atomics into G
+    float* __restrict__ slotU;    // [n_users * capU, d]
+    float* __restrict__ slotV;    // [n_items * capV, d]
+    int capU, capV;               // rows above this many occurrences use float atomics into G
     double* __restrict__ loss_partial;  // [grad grid]
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
@@ -103,47 +101,32 @@ struct XchgArgs {
     int32_t* __restrict__ send_ids;       // [n] global ids packed by owner
 };
 
-// slot allocation (between prep and grad): every row with count >= 2 joins the
-// duplicate list; rows with 2..slot_max occurrences get a contiguous slot range.
-// One pass: each block publishes its totals in an 8-B status word and sums the
-// words of all lower blocks (no contended counter).
-struct SlotArgs {
-    int64_t n_users, n_items;
-    int blocksU;                  // blocks [0, blocksU) scan users, the rest items
-    int rows_per_block;           // kBlock * rows per thread
-    int count_users, count_items;
-    int slot_max;
-    const int32_t* __restrict__ cntU;
-    const int32_t* __restrict__ cntV;
-    int32_t* __restrict__ offU;
-    int32_t* __restrict__ offV;
-    int32_t* __restrict__ dup;    // [n_users + n_items] duplicated rows: user r -> r, item r -> n_users + r
-    uint64_t* __restrict__ status;       // [grid] this step (zero on entry)
-    uint64_t* __restrict__ status_next;  // [kSlotMaxBlocks] zeroed for the next step
-    int32_t* __restrict__ ctl;    // written by the last block: [0] slots used, [1] |dup|
-};
-constexpr int kSlotMaxBlocks = 1024;
-
 struct ApplyArgs {
     int d;
     float lr;
     float clip_norm;
     int clip;            // CML: clip updated rows
-    int slot_max;
-    // duplicated rows (count > 1) listed by slot_kernel (global ids, items
-    // after users)
-    const int32_t* __restrict__ ctl;
-    const int32_t* __restrict__ dup;
-    int64_t n_users;
-    const int32_t* __restrict__ offU;
-    const int32_t* __restrict__ offV;
-    const float* __restrict__ slotG;
+    int capU, capV;      // fixed slot range per row
+    int count_users, count_items;
+    // work items: the batch's occurrences (+ the served rows of the group
+    // exchange); the owner of a duplicated row applies it
+    const int32_t* __restrict__ occU;
+    const int32_t* __restrict__ rankU;
+    int64_t nU;
+    const int32_t* __restrict__ occV;
+    const int32_t* __restrict__ rankV;
+    int64_t nV;
+    const int32_t* __restrict__ served_ids;   // global user ids
+    const int32_t* __restrict__ served_own;   // 1: this served row applies it
+    int64_t nS;
+    int64_t shard_u0;
+    const float* __restrict__ slotU;
+    const float* __restrict__ slotV;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
     float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
     float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;  // nullable
-    int max_groups;      // upper bound of listed rows (sizes the grid)
     // loss reduction (block 0)
     const double* __restrict__ loss_partial;
     int n_partial;
@@ -215,13 +198,10 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = 
 // blocks (= loss partials) of the grad launch for this step shape
 int grad_blocks(const StepArgs& a);
 int grad_blocks_max(int B);  // upper bound over every grad variant
-// duplicate list + slot ranges; fills a.rows_per_block / a.blocksU, returns the grid in *grid
-hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid = nullptr);
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 // apply of step s and prep of step s+1 in one launch (device-sampler pipeline)
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& next, hipStream_t s);
-// apply of step s and the slot pass of step s+1 in one launch
-hipError_t launch_apply_slots(const ApplyArgs& p, SlotArgs next, hipStream_t s);
+
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);
 hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int truncated,
@@ -237,7 +217,7 @@ hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s);
 // group exchange: pack the remote group members of a batch by owner
 hipError_t launch_xchg_pack(const XchgArgs& a, hipStream_t s);
 // owner side: flag + gather the requested rows; scatter-add their gradients
-hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU,
+hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU, int32_t* own,
                              const float* U, float* rows, int d, hipStream_t s);
 hipError_t launch_xchg_accumulate(const int32_t* ids, int64_t n, int64_t u0, const float* grads,
                                   float* GU, int d, hipStream_t s);

@@ -12,22 +12,22 @@
 //                or take a host-fed batch; then count every touched row's
 //                occurrences (returning atomicAdd: the old value is the
 //                occurrence's rank inside its row).
-//  slot_kernel   lists the rows that occur more than once and hands each row
-//                with 2..slot_max occurrences a contiguous range of slot rows
-//                (one atomic per block).
 //  grad_kernel   gather U[u], V[i], V[j] (+U[g], b) rows, group-reduce the
 //                dots / distances, evaluate the loss and dL/dx, form every
 //                per-occurrence gradient row.  A row that occurs ONCE in the
 //                batch is updated right here with SparseApplyAdagrad
 //                (acc += g^2; w -= lr*g/sqrt(acc); CML: clip) -- its
 //                pre-update value is already in registers.  A duplicated
-//                row's gradient is a plain store into its slot row (hot rows,
-//                > slot_max occurrences, scatter-add into a dense fp32
-//                accumulator with float atomics), so duplicates SUM before
+//                row's gradient is a plain store into its slot row: row r
+//                owns the fixed slot range [r*cap, (r+1)*cap) and occurrence
+//                k of r (prep's returning count atomic) writes slot r*cap + k.
+//                Hot rows (> cap occurrences) scatter-add into a dense fp32
+//                accumulator with float atomics.  So duplicates SUM before
 //                the update: TF1's _deduplicate_indexed_slices.
-//  apply_kernel  walks the duplicate list: sums each row's slot rows in rank
-//                order (or takes its atomic sum), applies Adagrad and resets
-//                the row's count.
+//  apply_kernel  one lane per occurrence: the first occurrence (rank 0) of a
+//                duplicated row sums the row's slot rows in rank order (or
+//                takes its atomic sum), applies Adagrad and resets the count.
+//                Fixed slot ranges: no duplicate list, no scan, no extra launch.
 //
 // Float atomics run at the memory side at ~1.3 TB/s chip-wide, plain stores
 // at ~6 TB/s: the store-and-sum form moves the duplicate gradients ~4x faster.
@@ -200,18 +200,19 @@ __device__ __forceinline__ void gstore(float* __restrict__ S, int64_t r, int d, 
     row_st<EPL>(S + r * (int64_t)d, d, gl, g);
 }
 
-// slot row of one occurrence of a duplicated row: rows with 2..slot_max
-// occurrences own the contiguous slots [off, off+count), in rank order; -1 =
-// hot row (more occurrences) or uncounted table -> float atomics into G
-__device__ __forceinline__ int64_t slot_of(int count, int off, int rank, int slot_max) {
-    return (count >= 2 && count <= slot_max) ? (int64_t)off + rank : -1;
+// slot row of one occurrence of a duplicated row: a row with 2..cap
+// occurrences owns the fixed slots [r*cap, r*cap + count), in rank order;
+// -1 = hot row (more occurrences) or uncounted table -> float atomics into G
+__device__ __forceinline__ int64_t slot_of(int count, int64_t r, int rank, int cap) {
+    return (count >= 2 && count <= cap) ? r * (int64_t)cap + rank : -1;
 }
 
 // row r of X: singleton -> apply now; duplicated -> its slot row (summed by
 // apply_kernel in rank order) or, for hot rows, float atomics into G
 template <int EPL>
 __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict__ A,
-                                        float* __restrict__ G, int32_t* __restrict__ cnt,
+                                        float* __restrict__ G, float* __restrict__ S,
+                                        int32_t* __restrict__ cnt,
                                         int64_t r, int count, int64_t slot, int d, int gl,
                                         const float (&x0)[EPL], const float (&g)[EPL],
                                         const StepArgs& a) {
@@ -219,7 +220,7 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
         gapply<EPL>(X, A, r, d, gl, x0, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) cnt[r] = 0;
     } else if (slot >= 0) {
-        gstore<EPL>(a.slotG, slot, d, gl, g);
+        gstore<EPL>(S, slot, d, gl, g);
     } else {
         gatomic<EPL>(G, r, d, gl, g);
     }
@@ -398,8 +399,7 @@ struct NegRows {
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 c[w] = a.count_items ? a.cntV[j[w]] : 0;
-                const int o = a.count_items ? a.offV[j[w]] : 0;
-                sl[w] = slot_of(c[w], o, rk[w], a.slot_max);
+                sl[w] = slot_of(c[w], j[w], rk[w], a.capV);
                 gload<EPL>(a.V, j[w], a.d, gl, v[w]);
             }
         }
@@ -412,8 +412,7 @@ struct NegRows {
             j[0] = a.occV[a.B + p * a.W + w];
             const int rk = a.count_items ? a.rankV[a.B + p * a.W + w] : 0;
             c[0] = a.count_items ? a.cntV[j[0]] : 0;
-            const int o = a.count_items ? a.offV[j[0]] : 0;
-            sl[0] = slot_of(c[0], o, rk, a.slot_max);
+            sl[0] = slot_of(c[0], j[0], rk, a.capV);
             gload<EPL>(a.V, j[0], a.d, gl, v[0]);
             return 0;
         }
@@ -443,8 +442,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
         J.prefetch(a, p, gl);
         const int cu = a.count_users ? a.cntU[u] : 0;
         const int ci = a.count_items ? a.cntV[i] : 0;
-        const int64_t su = slot_of(cu, a.count_users ? a.offU[u] : 0, ru, a.slot_max);
-        const int64_t si = slot_of(ci, a.count_items ? a.offV[i] : 0, ri, a.slot_max);
+        const int64_t su = slot_of(cu, u, ru, a.capU);
+        const int64_t si = slot_of(ci, i, ri, a.capV);
         float uu[EPL], vi[EPL];
         gload<EPL>(a.U, u, d, gl, uu);
         gload<EPL>(a.V, i, d, gl, vi);
@@ -480,7 +479,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gj[s] = -c * uu[s] + a.reg * J.v[sl][s];
                     sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
                 }
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -490,8 +489,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else if (MODEL == GBPR) {
             // ui = rho*mean_k<g_k,i> + (1-rho)<u,i> + b_i ; uj = <u,j> + b_j   (A.2)
             const float bi = a.b[i];
@@ -531,7 +530,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
                 if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj);
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, j, J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j, J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             const float rg = a.rho / Gf;
             float gi[EPL];
@@ -542,7 +541,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
             for (int k2 = 0; k2 < G; ++k2) {
                 const int g = a.occU[B + p * G + k2];
                 float gk[EPL], gg[EPL];
@@ -554,11 +553,11 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     continue;
                 }
                 const int cg = a.cntU[g];
-                const int64_t sg_ = slot_of(cg, a.offU[g], a.rankU[B + p * G + k2], a.slot_max);
-                gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
+                const int64_t sg_ = slot_of(cg, g, a.rankU[B + p * G + k2], a.capU);
+                gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
             if (gl == 0) bias_finish(a, i, ci, sc);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
 #pragma unroll
@@ -610,7 +609,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     }
                 }
                 // a touched row with a zero gradient is still clipped (cml.py:128-129)
-                gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -621,8 +620,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     sq = fmaf(vi[s], vi[s], sq);
                 }
             }
-            gfinish<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         }
     }
 
@@ -706,7 +705,8 @@ __device__ __forceinline__ void gapply_pre(float* __restrict__ X, float* __restr
 
 template <int EPL>
 __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __restrict__ A,
-                                            float* __restrict__ G, int32_t* __restrict__ cnt,
+                                            float* __restrict__ G, float* __restrict__ S,
+                                            int32_t* __restrict__ cnt,
                                             int64_t r, int count, int64_t slot, int d, int gl,
                                             const float (&x0)[EPL], const float (&acc0)[EPL],
                                             const float (&g)[EPL], const StepArgs& a) {
@@ -717,7 +717,7 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
 #endif
         if (gl == 0) cnt[r] = 0;
     } else if (slot >= 0) {
-        gstore<EPL>(a.slotG, slot, d, gl, g);
+        gstore<EPL>(S, slot, d, gl, g);
     } else {
 #ifndef CF_EXP_NO_ATOMIC
         gatomic<EPL>(G, r, d, gl, g);
@@ -732,7 +732,6 @@ struct PairRows {
     int u, i, cu, ci, ru, ri;
     int j[WT], cj[WT], rj[WT];
     int g[NGA], cg[NGA], rg[NGA];
-    int ou_, oi_;                      // slot bases, until load_acc
     int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
     float uu[EPL], vi[EPL], au[EPL], ai[EPL];
     float vj[WT][EPL], aj[WT][EPL];
@@ -758,18 +757,10 @@ struct PairRows {
     __device__ __forceinline__ void load_rows(const StepArgs& a, int gl) {
         cu = a.count_users ? a.cntU[u] : 0;
         ci = a.count_items ? a.cntV[i] : 0;
-        ou_ = a.count_users ? a.offU[u] : 0;
-        oi_ = a.count_items ? a.offV[i] : 0;
 #pragma unroll
-        for (int w = 0; w < WT; ++w) {
-            cj[w] = a.count_items ? a.cntV[j[w]] : 0;
-            sj[w] = a.count_items ? a.offV[j[w]] : 0;
-        }
+        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
 #pragma unroll
-        for (int k = 0; k < NG; ++k) {
-            cg[k] = (a.count_users && g[k] >= 0) ? a.cntU[g[k]] : 0;
-            sg[k] = (a.count_users && g[k] >= 0) ? a.offU[g[k]] : 0;
-        }
+        for (int k = 0; k < NG; ++k) cg[k] = (a.count_users && g[k] >= 0) ? a.cntU[g[k]] : 0;
         gload<EPL>(a.U, u, a.d, gl, uu);
         gload<EPL>(a.V, i, a.d, gl, vi);
 #pragma unroll
@@ -784,12 +775,12 @@ struct PairRows {
         }
     }
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
-        su = slot_of(cu, ou_, ru, a.slot_max);
-        si = slot_of(ci, oi_, ri, a.slot_max);
+        su = slot_of(cu, u, ru, a.capU);
+        si = slot_of(ci, i, ri, a.capV);
 #pragma unroll
-        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], (int)sj[w], rj[w], a.slot_max);
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV);
 #pragma unroll
-        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], (int)sg[k], rg[k], a.slot_max);
+        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
         gload_acc<EPL>(a.AV, i, a.d, gl, ci == 1, ai);
 #pragma unroll
@@ -828,7 +819,7 @@ struct PairRows {
                     gj[s] = -c * uu[s] + a.reg * vj[w][s];
                     sq = fmaf(vj[w][s], vj[w][s], sq);
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             float gi[EPL];
 #pragma unroll
@@ -838,8 +829,8 @@ struct PairRows {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else if (MODEL == GBPR) {  // G == 1
             const float ui_u = gdot<EPL>(uu, vi);
 #pragma unroll
@@ -862,7 +853,7 @@ struct PairRows {
                     gj[s] = -c * uu[s];
                 }
                 if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w]);
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             const float rg = a.rho;  // rho / G with G == 1
             float gi[EPL], gg[EPL];
@@ -874,13 +865,13 @@ struct PairRows {
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
             if (g[0] >= 0)
-                gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
+                gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
             else  // another rank's user: its gradient row goes back to the owner
                 gstore<EPL>(a.xgrads, -1 - g[0], d, gl, gg);
             if (gl == 0) bias_finish(a, i, ci, sc);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else {  // CML
             float du[EPL];
 #pragma unroll
@@ -928,7 +919,7 @@ struct PairRows {
                         sq = fmaf(vj[w][s], vj[w][s], sq);
                     }
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             if (l2) {
 #pragma unroll
@@ -939,8 +930,8 @@ struct PairRows {
                     sq = fmaf(vi[s], vi[s], sq);
                 }
             }
-            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
+            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         }
     }
 };
@@ -1000,143 +991,62 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 }
 
 // ---------------------------------------------------------------------------
-// slots: after prep's counts are final, list every duplicated row (count >= 2)
-// and give each row with 2..slot_max occurrences a contiguous range of slot
-// rows.  Ranges are allocated per block with ONE atomic per block (their
-// order does not matter, only that each row's slots are contiguous).
-// ---------------------------------------------------------------------------
-constexpr int kSlotRPT = 8;  // rows per thread per chunk
-
-__device__ __forceinline__ void slot_counts(const SlotArgs& a, const int32_t* cnt, int64_t n,
-                                            bool counted, int64_t r0, int (&c)[kSlotRPT]) {
-#pragma unroll
-    for (int q = 0; q < kSlotRPT; q += 4) {
-        const int64_t r = r0 + q;
-        if (counted && r + 3 < n) {
-            const int4 v = *reinterpret_cast<const int4*>(cnt + r);
-            c[q] = v.x; c[q + 1] = v.y; c[q + 2] = v.z; c[q + 3] = v.w;
-        } else {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) c[q + t] = (counted && r + t < n) ? cnt[r + t] : 0;
-        }
-    }
-}
-
-__device__ __forceinline__ void slot_body(const SlotArgs& a, int blk, int nblocks) {
-    __shared__ int s_wd[kWavesPerBlock], s_ws[kWavesPerBlock];
-    __shared__ int s_base[2];
-    if (blk == 0)
-        for (int k = threadIdx.x; k < kSlotMaxBlocks; k += kBlock)
-            __hip_atomic_store(a.status_next + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool isU = blk < a.blocksU;
-    const int64_t n = isU ? a.n_users : a.n_items;
-    const bool counted = isU ? a.count_users != 0 : a.count_items != 0;
-    const int32_t* cnt = isU ? a.cntU : a.cntV;
-    const int64_t rb = (int64_t)(isU ? blk : blk - a.blocksU) * a.rows_per_block;
-    const int chunks = a.rows_per_block / (kBlock * kSlotRPT);
-    // pass 1: this thread's duplicated rows and slot rows (any order is valid:
-    // only per-row contiguity of the slot ranges matters)
-    int nd = 0, ns = 0;
-    for (int ch = 0; ch < chunks; ++ch) {
-        int c[kSlotRPT];
-        slot_counts(a, cnt, n, counted, rb + (int64_t)ch * kBlock * kSlotRPT + threadIdx.x * kSlotRPT, c);
-#pragma unroll
-        for (int q = 0; q < kSlotRPT; ++q) {
-            nd += (c[q] >= 2) ? 1 : 0;
-            ns += (c[q] >= 2 && c[q] <= a.slot_max) ? c[q] : 0;
-        }
-    }
-    const int lane = lane_id(), wv = threadIdx.x >> 6;
-    const int id = wave_incl_scan(nd), is = wave_incl_scan(ns);
-    if (lane == 63) {
-        s_wd[wv] = id;
-        s_ws[wv] = is;
-    }
-    __syncthreads();
-    int pd = id - nd, ps = is - ns, td = 0, ts = 0;
-#pragma unroll
-    for (int k = 0; k < kWavesPerBlock; ++k) {
-        if (k < wv) {
-            pd += s_wd[k];
-            ps += s_ws[k];
-        }
-        td += s_wd[k];
-        ts += s_ws[k];
-    }
-    // publish this block's totals (flag bit 63 | dups << 32 | slots) in ONE
-    // 8-B agent-scope store, then sum every lower block's word (relaxed agent
-    // loads, L1 bypassed).  Each block publishes before it waits and waits only
-    // on lower ids, and the grid is <= kSlotMaxBlocks, so it always drains.
-    if (threadIdx.x == 0)
-        __hip_atomic_store(a.status + blk,
-                           (1ull << 63) | ((uint64_t)(uint32_t)td << 32) | (uint64_t)(uint32_t)ts,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int bd = 0, bs = 0;
-    for (int k = threadIdx.x; k < blk; k += kBlock) {
-        uint64_t w;
-        do {
-            w = __hip_atomic_load(a.status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } while ((w >> 63) == 0ull);
-        bd += (int)((w >> 32) & 0x7FFFFFFFull);
-        bs += (int)(uint32_t)w;
-    }
-    bd = wave_sum_i(bd);
-    bs = wave_sum_i(bs);
-    __syncthreads();  // s_wd / s_ws are reused
-    if (lane == 0) {
-        s_wd[wv] = bd;
-        s_ws[wv] = bs;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int x = 0, y = 0;
-#pragma unroll
-        for (int k = 0; k < kWavesPerBlock; ++k) {
-            x += s_wd[k];
-            y += s_ws[k];
-        }
-        s_base[0] = x;
-        s_base[1] = y;
-        if (blk == nblocks - 1) {
-            a.ctl[0] = y + ts;
-            a.ctl[1] = x + td;
-        }
-    }
-    __syncthreads();
-    if (td == 0) return;  // block-uniform
-    pd += s_base[0];
-    ps += s_base[1];
-    // pass 2: write the list entries and slot bases (counts re-read, L2-warm)
-    int32_t* off = isU ? a.offU : a.offV;
-    const int64_t gbase = isU ? 0 : a.n_users;
-    for (int ch = 0; ch < chunks && nd > 0; ++ch) {
-        const int64_t r0 = rb + (int64_t)ch * kBlock * kSlotRPT + threadIdx.x * kSlotRPT;
-        int c[kSlotRPT];
-        slot_counts(a, cnt, n, counted, r0, c);
-#pragma unroll
-        for (int q = 0; q < kSlotRPT; ++q) {
-            if (c[q] >= 2) {
-                a.dup[pd++] = (int32_t)(gbase + r0 + q);
-                if (c[q] <= a.slot_max) {
-                    off[r0 + q] = ps;
-                    ps += c[q];
-                }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void slot_kernel(SlotArgs a) {
-    slot_body(a, blockIdx.x, gridDim.x);
-}
-
-// ---------------------------------------------------------------------------
 // apply the summed gradient of every duplicated row: the TF1 IndexedSlices
-// dedup-sum + SparseApplyAdagrad (bprmf.py:74-75 and siblings).  One group
-// per listed row: the slot rows [off, off+count) summed in rank order, or the
-// atomic sum in G for a hot row (G re-zeroed); then the row's count is reset.
+// dedup-sum + SparseApplyAdagrad (bprmf.py:74-75 and siblings).
+// One lane per work item -- the batch's user occurrences, item occurrences
+// and (group exchange) served rows.  The owner of a duplicated row is its
+// rank-0 occurrence (or, for a served row with no local occurrence, its first
+// server).  Owners are ballot-compacted and handed to the wave's four 16-lane
+// groups: the row's slot rows r*cap + [0, count) summed in rank order, or the
+// atomic sum in G for a hot row (G re-zeroed); Adagrad; the count reset.
 // Block 0 also folds the grad kernel's loss partials.
 // ---------------------------------------------------------------------------
+template <int EPL>
+__device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool isU, int gl) {
+    int32_t* cnt = isU ? a.cntU : a.cntV;
+    float* X = isU ? a.U : a.V;
+    float* A = isU ? a.AU : a.AV;
+    float* G = isU ? a.GU : a.GV;
+    const int cap = isU ? a.capU : a.capV;
+    const int c = cnt[r];
+    float x[EPL], acc[EPL], g[EPL];
+    gload<EPL>(X, r, a.d, gl, x);
+    gload_acc<EPL>(A, r, a.d, gl, true, acc);
+    if (c <= cap) {
+        const float* S = isU ? a.slotU : a.slotV;
+        const int64_t s0 = r * (int64_t)cap;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] = 0.f;
+        constexpr int NF = 4;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
+        for (int t0 = 0; t0 < c; t0 += NF) {
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < c) gload<EPL>(S, s0 + t0 + q, a.d, gl, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < c) {
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+                }
+        }
+    } else {
+        gload<EPL>(G, r, a.d, gl, g);
+        row_zero<EPL>(G + r * a.d, a.d, gl);
+    }
+    gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
+    if (gl == 0) {
+        cnt[r] = 0;
+        if (!isU && a.b != nullptr) {
+            const float gb = a.Gb[r];
+            const float ab = fmaf(gb, gb, a.Ab[r]);
+            a.Ab[r] = ab;
+            a.b[r] -= (a.lr * gb) / sqrtf(ab);
+            a.Gb[r] = 0.f;
+        }
+    }
+}
+
 template <int EPL>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     __shared__ double s_red[kWavesPerBlock];
@@ -1151,52 +1061,57 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         __syncthreads();
         if (threadIdx.x == 0) a.loss_acc[0] += (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
-    const int64_t total = a.ctl[1];
-    const int64_t ngrp = ((int64_t)nblocks * kBlock) >> 4;
-    for (int64_t t = ((int64_t)block * kBlock + threadIdx.x) >> 4; t < total; t += ngrp) {
-        const int64_t id = a.dup[t];
-        const bool isU = id < a.n_users;  // group-uniform
-        const int64_t r = isU ? id : id - a.n_users;
-        int32_t* cnt = isU ? a.cntU : a.cntV;
-        float* X = isU ? a.U : a.V;
-        float* A = isU ? a.AU : a.AV;
-        float* G = isU ? a.GU : a.GV;
-        const int c = cnt[r];
-        const int64_t s0 = (c <= a.slot_max) ? (isU ? a.offU[r] : a.offV[r]) : -1;
-        float x[EPL], acc[EPL], g[EPL];
-        gload<EPL>(X, r, a.d, gl, x);
-        gload_acc<EPL>(A, r, a.d, gl, true, acc);
-        if (s0 >= 0) {
-#pragma unroll
-            for (int s = 0; s < EPL; ++s) g[s] = 0.f;
-            constexpr int NF = 4;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
-            for (int t0 = 0; t0 < c; t0 += NF) {
-                float h[NF][EPL];
-#pragma unroll
-                for (int q = 0; q < NF; ++q)
-                    if (t0 + q < c) gload<EPL>(a.slotG, s0 + t0 + q, a.d, gl, h[q]);
-#pragma unroll
-                for (int q = 0; q < NF; ++q)
-                    if (t0 + q < c) {
-#pragma unroll
-                        for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+    // a block takes 64 work items at a time: wave 0 finds their owners (~18 %
+    // of the occurrences at cfg2), then the block's 16 groups apply them --
+    // about one row per group per chunk, so a row's dependent loads are not
+    // queued behind other rows'
+    __shared__ unsigned long long s_mask;
+    __shared__ int64_t s_row[kWave];
+    __shared__ int s_isU[kWave];
+    const int64_t nU = a.count_users ? a.nU : 0, nV = a.count_items ? a.nV : 0;
+    const int64_t total = nU + nV + a.nS;
+    const int group = threadIdx.x >> 4;
+    for (int64_t base = (int64_t)block * kWave; base < total; base += (int64_t)nblocks * kWave) {
+        if (wv == 0) {
+            const int64_t q = base + lane;
+            int64_t row = -1;
+            int isU = 0;
+            if (q < nU) {
+                if (a.rankU[q] == 0) {
+                    const int32_t r = a.occU[q];
+                    if (r >= 0 && a.cntU[r] >= 2) {
+                        row = r;
+                        isU = 1;
                     }
+                }
+            } else if (q < nU + nV) {
+                const int64_t k = q - nU;
+                if (a.rankV[k] == 0) {
+                    const int32_t r = a.occV[k];
+                    if (a.cntV[r] >= 2) row = r;
+                }
+            } else if (q < total) {
+                const int64_t k = q - nU - nV;
+                if (a.served_own[k]) {
+                    row = (int64_t)a.served_ids[k] - a.shard_u0;
+                    isU = 1;
+                }
             }
-        } else {
-            gload<EPL>(G, r, a.d, gl, g);
-            row_zero<EPL>(G + r * a.d, a.d, gl);
+            const unsigned long long m = __ballot(row >= 0);
+            s_row[lane] = row;
+            s_isU[lane] = isU;
+            if (lane == 0) s_mask = m;
         }
-        gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
-        if (gl == 0) {
-            cnt[r] = 0;
-            if (!isU && a.b != nullptr) {
-                const float gb = a.Gb[r];
-                const float ab = fmaf(gb, gb, a.Ab[r]);
-                a.Ab[r] = ab;
-                a.b[r] -= (a.lr * gb) / sqrtf(ab);
-                a.Gb[r] = 0.f;
-            }
+        __syncthreads();
+        unsigned long long m = s_mask;
+        // group g applies the owners of rank g, g + 16, ... among the set bits
+        for (int k = 0; k < group && m != 0ull; ++k) m &= m - 1ull;
+        while (m != 0ull) {  // group-uniform
+            const int src = __ffsll((long long)m) - 1;
+            apply_row<EPL>(a, s_row[src], s_isU[src] != 0, gl);
+            for (int k = 0; k < kGroupsPerBlock && m != 0ull; ++k) m &= m - 1ull;
         }
+        __syncthreads();  // s_* reused by the next chunk
     }
 }
 
@@ -1214,18 +1129,6 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
         apply_body<EPL>(p, blockIdx.x, napply);
     else
         prep_body<MODEL>(a, blockIdx.x - napply);
-}
-
-// the slot pass of step s+1 (blocks [0, nslot): its look-back only waits on
-// lower slot blocks, all dispatched earlier) beside the apply of step s (the
-// rest).  Needs step s+1's counts complete, i.e. its draw ran in the gradient
-// launch of step s; the slot ranges / duplicate list are double-buffered.
-template <int EPL>
-__global__ __launch_bounds__(kBlock) void apply_slot_kernel(ApplyArgs p, SlotArgs sa, int nslot) {
-    if ((int)blockIdx.x < nslot)
-        slot_body(sa, blockIdx.x, nslot);
-    else
-        apply_body<EPL>(p, blockIdx.x - nslot, gridDim.x - nslot);
 }
 
 // ---------------------------------------------------------------------------
@@ -1401,13 +1304,18 @@ __global__ __launch_bounds__(kBlock) void xchg_scatter_kernel(XchgArgs a) {
 template <int EPL>
 __global__ __launch_bounds__(kBlock) void xchg_serve_kernel(const int32_t* __restrict__ ids, int64_t n,
                                                             int64_t u0, int32_t* __restrict__ cntU,
+                                                            int32_t* __restrict__ own,
                                                             const float* __restrict__ U,
                                                             float* __restrict__ rows, int d) {
     const int gl = threadIdx.x & (kGL - 1);
     const int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
     if (j >= n) return;
     const int64_t r = (int64_t)ids[j] - u0;
-    if (gl == 0) atomicOr(&cntU[r], kRemoteFlag);
+    if (gl == 0) {
+        // the first server of a row with no local occurrence applies it
+        const int32_t old = atomicOr(&cntU[r], kRemoteFlag);
+        own[j] = (old == 0) ? 1 : 0;
+    }
     float x[EPL];
     gload<EPL>(U, r, d, gl, x);
     gstore<EPL>(rows, j, d, gl, x);
@@ -1526,29 +1434,11 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
     }
 }
 
-// rows per block: the smallest multiple of one chunk (kBlock * kSlotRPT) that
-// keeps the grid within kSlotMaxBlocks; returns the grid (0 on overflow)
-static int slot_shape(SlotArgs& a) {
-    const int64_t chunk = (int64_t)kBlock * kSlotRPT;
-    int64_t rpb = chunk;
-    while ((a.n_users + rpb - 1) / rpb + (a.n_items + rpb - 1) / rpb > kSlotMaxBlocks) rpb += chunk;
-    if (rpb > (int64_t)1 << 30) return 0;
-    a.rows_per_block = (int)rpb;
-    a.blocksU = (int)((a.n_users + rpb - 1) / rpb);
-    return a.blocksU + (int)((a.n_items + rpb - 1) / rpb);
-}
-
-hipError_t launch_slots(SlotArgs a, hipStream_t s, int* grid) {
-    const int blocks = slot_shape(a);
-    if (blocks == 0) return hipErrorInvalidValue;
-    if (grid) *grid = blocks;
-    hipLaunchKernelGGL(slot_kernel, dim3(blocks), dim3(kBlock), 0, s, a);
-    return hipGetLastError();
-}
-
 static int apply_grid(const ApplyArgs& a) {
-    int64_t blocks = ((int64_t)a.max_groups + kGroupsPerBlock - 1) / kGroupsPerBlock;
-    if (blocks > 2048) blocks = 2048;  // grid-stride over the list
+    // 64 work items (user occurrences, item occurrences, served rows) per block
+    const int64_t items = (a.count_users ? a.nU : 0) + (a.count_items ? a.nV : 0) + a.nS;
+    int64_t blocks = (items + kWave - 1) / kWave;
+    if (blocks > 4096) blocks = 4096;  // grid-stride over the work items
     if (blocks < 1) blocks = 1;        // block 0 still reduces the loss
     return (int)blocks;
 }
@@ -1583,20 +1473,6 @@ static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hip
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return launch_apply(p, s);
     return a.model == GBPR ? launch_apply_prep_m<GBPR>(p, a, s) : launch_apply_prep_m<BPR>(p, a, s);
-}
-
-hipError_t launch_apply_slots(const ApplyArgs& p, SlotArgs sa, hipStream_t s) {
-    const int ns = slot_shape(sa);
-    if (ns == 0) return hipErrorInvalidValue;
-    const dim3 grid(ns + apply_grid(p)), block(kBlock);
-    switch (epl_for(p.d)) {
-        case 1: hipLaunchKernelGGL(apply_slot_kernel<1>, grid, block, 0, s, p, sa, ns); break;
-        case 2: hipLaunchKernelGGL(apply_slot_kernel<2>, grid, block, 0, s, p, sa, ns); break;
-        case 4: hipLaunchKernelGGL(apply_slot_kernel<4>, grid, block, 0, s, p, sa, ns); break;
-        case 8: hipLaunchKernelGGL(apply_slot_kernel<8>, grid, block, 0, s, p, sa, ns); break;
-        default: hipLaunchKernelGGL(apply_slot_kernel<16>, grid, block, 0, s, p, sa, ns); break;
-    }
-    return hipGetLastError();
 }
 
 static int row_grid(int64_t n_rows) {
@@ -1668,16 +1544,16 @@ hipError_t launch_xchg_pack(const XchgArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU,
+hipError_t launch_xchg_serve(const int32_t* ids, int64_t n, int64_t u0, int32_t* cntU, int32_t* own,
                              const float* U, float* rows, int d, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const dim3 grid((unsigned)((n + kGroupsPerBlock - 1) / kGroupsPerBlock)), block(kBlock);
     switch (epl_for(d)) {
-        case 1: hipLaunchKernelGGL(xchg_serve_kernel<1>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
-        case 2: hipLaunchKernelGGL(xchg_serve_kernel<2>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
-        case 4: hipLaunchKernelGGL(xchg_serve_kernel<4>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
-        case 8: hipLaunchKernelGGL(xchg_serve_kernel<8>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
-        default: hipLaunchKernelGGL(xchg_serve_kernel<16>, grid, block, 0, s, ids, n, u0, cntU, U, rows, d); break;
+        case 1: hipLaunchKernelGGL(xchg_serve_kernel<1>, grid, block, 0, s, ids, n, u0, cntU, own, U, rows, d); break;
+        case 2: hipLaunchKernelGGL(xchg_serve_kernel<2>, grid, block, 0, s, ids, n, u0, cntU, own, U, rows, d); break;
+        case 4: hipLaunchKernelGGL(xchg_serve_kernel<4>, grid, block, 0, s, ids, n, u0, cntU, own, U, rows, d); break;
+        case 8: hipLaunchKernelGGL(xchg_serve_kernel<8>, grid, block, 0, s, ids, n, u0, cntU, own, U, rows, d); break;
+        default: hipLaunchKernelGGL(xchg_serve_kernel<16>, grid, block, 0, s, ids, n, u0, cntU, own, U, rows, d); break;
     }
     return hipGetLastError();
 }

@@ -69,10 +69,10 @@ enum cf_kernel_id {
     CF_K_CLIP = 4,       /* CML full-table clip_by_norm                       */
     CF_K_SCORE = 5,      /* user x item scoring tile kernel                   */
     CF_K_TOPK = 6,       /* masked per-user top-k                             */
-    CF_K_SLOT = 7,       /* duplicate-row list + slot ranges (store-and-sum)   */
+    CF_K_SLOT = 7,       /* (retired: fixed per-row slot ranges need no pass)  */
     CF_K_APPLY_PREP = 8, /* apply of step s fused with the draw of step s+1    */
-    CF_K_GRAD_PREP = 9,  /* gradient of step s fused with the draw of step s+1 */
-    CF_K_APPLY_SLOT = 10,/* apply of step s fused with the slot pass of s+1    */
+    CF_K_GRAD_PREP = 9,  /* (retired pipeline 2)                               */
+    CF_K_APPLY_SLOT = 10,/* (retired pipeline 2)                               */
     CF_K_COUNT = 11
 };
 
@@ -284,17 +284,17 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "prep_stream" 0 = everything in order on the engine stream (default);
  *                1 = sample/count on a side stream, overlapping the previous
  *                step's gradient.  Same results.
- *   "slot_max"   rows occurring 2..slot_max times in a batch sum their
- *                per-occurrence gradient rows from plain-stored slots; rows
- *                occurring more often use float atomics (default 32; 1 = atomics
- *                for every duplicated row).  Same arithmetic up to fp32
- *                summation order.
+ *   "slot_max"   an item row occurring 2..slot_max times in a batch sums its
+ *                per-occurrence gradient rows from plain-stored slot rows
+ *                (row r owns the fixed range [r*slot_max, (r+1)*slot_max));
+ *                rows occurring more often use float atomics (default 32;
+ *                1 = atomics for every duplicated row).  Same arithmetic up
+ *                to fp32 summation order.
+ *   "slot_max_user" the same for user rows (default 2).
  *   "pipeline"   how cf_train_steps overlaps consecutive steps (same results):
  *                1 = the duplicate apply of step s with the draw + count of
- *                step s+1, three launches per step (default); 2 = two
- *                launches, the gradient of step s with the draw + count of
- *                step s+1, then the duplicate apply of step s with the slot
- *                pass of step s+1; 0 = one step at a time, four launches.
+ *                step s+1, two launches per step (default); 0 = one step at a
+ *                time, three launches.
  *   "profile_mask" bit k set = cf_profile_enable times kernel id k (default
  *                all): timing only the kernel of interest keeps the event
  *                pairs of the others out of a timed loop.
