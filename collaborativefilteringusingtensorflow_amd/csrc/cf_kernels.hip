@@ -302,15 +302,20 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         int32_t j = -1;
         if (a.sample) {
             // negItems = randint(0, n_items), redrawn while j in Pos(u)
-            // (sampler_ranking.py:30-36); lane w owns candidate w
-            uint64_t ctr = (uint64_t)w << 32;
-            if (gl < nw) j = draw_item(key, ctr++, a.n_items);
-            uint32_t pending = (1u << nw) - 1u;
-            for (;;) {
+            // (sampler_ranking.py:30-36).  Negative w takes the first
+            // candidate of the sequence draw(key, (w << 32) + k), k = 0, 1, ..
+            // that is not a positive.  The first C = 8 / nw candidates of every
+            // negative are tested in ONE row scan (lane l holds attempt l / nw
+            // of negative l % nw), so a rejection rarely costs another pass.
+            const int C = PGL / nw;
+            const int nl = C * nw;
+            int32_t jl = -1;
+            if (gl < nl) jl = draw_item(key, ((uint64_t)(w0 + gl % nw) << 32) + (uint64_t)(gl / nw), a.n_items);
+            uint32_t hit = 0;
+            {
                 int32_t cand[PGL];
 #pragma unroll
-                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
-                uint32_t hit = 0;
+                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(jl, k, PGL);
                 for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
                     int32_t el[kPrepChunks];
 #pragma unroll
@@ -322,12 +327,46 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
                     for (int q = 0; q < kPrepChunks; ++q)
 #pragma unroll
                         for (int k = 0; k < PGL; ++k)
-                            hit |= (k < nw && el[q] == cand[k]) ? (1u << k) : 0u;
+                            hit |= (k < nl && el[q] == cand[k]) ? (1u << k) : 0u;
                 }
-                hit = gor8(hit) & pending;
-                if (hit == 0u) break;  // group-uniform
-                if ((hit >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
-                pending = hit;
+                hit = gor8(hit);
+            }
+            // lane w < nw: the first accepted attempt of negative w
+            bool done = false;
+            for (int c = 0; c < C; ++c) {
+                const int src = c * nw + (gl % nw);
+                const int32_t cv = __shfl(jl, src, PGL);
+                if (!done && gl < nw && !((hit >> src) & 1u)) {
+                    j = cv;
+                    done = true;
+                }
+            }
+            // rare: every tested attempt of some negative was a positive ->
+            // continue its sequence at attempt C, one candidate per lane
+            uint32_t pending = gor8((gl < nw && !done) ? (1u << gl) : 0u);
+            uint64_t ctr = ((uint64_t)w << 32) + (uint64_t)C;
+            if ((pending >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
+            while (pending != 0u) {  // group-uniform
+                int32_t cand[PGL];
+#pragma unroll
+                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
+                uint32_t h2 = 0;
+                for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
+                    int32_t el[kPrepChunks];
+#pragma unroll
+                    for (int q = 0; q < kPrepChunks; ++q) {
+                        const int64_t t = rb + (int64_t)(c0 + q) * PGL + gl;
+                        el[q] = (t < re) ? a.indices[t] : -1;
+                    }
+#pragma unroll
+                    for (int q = 0; q < kPrepChunks; ++q)
+#pragma unroll
+                        for (int k = 0; k < PGL; ++k)
+                            h2 |= (k < nw && el[q] == cand[k]) ? (1u << k) : 0u;
+                }
+                h2 = gor8(h2) & pending;
+                if ((h2 >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
+                pending = h2;
             }
             if (gl < nw) a.occV[B + p * W + w] = j;
         } else if (gl < nw) {
@@ -678,6 +717,9 @@ __device__ __forceinline__ void gload_acc(const float* __restrict__ A, int64_t r
 #ifdef CF_EXP_NO_ACC
     want = false;
 #endif
+#ifdef CF_EXP_ACC_ALWAYS  // issue the accumulator rows with the table rows (no dependent phase)
+    want = true;
+#endif
     if (want) row_ld<EPL>(A + r * (int64_t)d, d, gl, 1.f, acc);
 }
 
@@ -1002,13 +1044,12 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 // Block 0 also folds the grad kernel's loss partials.
 // ---------------------------------------------------------------------------
 template <int EPL>
-__device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool isU, int gl) {
+__device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool isU, int c, int gl) {
     int32_t* cnt = isU ? a.cntU : a.cntV;
     float* X = isU ? a.U : a.V;
     float* A = isU ? a.AU : a.AV;
     float* G = isU ? a.GU : a.GV;
     const int cap = isU ? a.capU : a.capV;
-    const int c = cnt[r];
     float x[EPL], acc[EPL], g[EPL];
     gload<EPL>(X, r, a.d, gl, x);
     gload_acc<EPL>(A, r, a.d, gl, true, acc);
@@ -1068,6 +1109,7 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
     __shared__ unsigned long long s_mask;
     __shared__ int64_t s_row[kWave];
     __shared__ int s_isU[kWave];
+    __shared__ int s_cnt[kWave];   // the owner's count, read once in the check
     const int64_t nU = a.count_users ? a.nU : 0, nV = a.count_items ? a.nV : 0;
     const int64_t total = nU + nV + a.nS;
     const int group = threadIdx.x >> 4;
@@ -1075,11 +1117,12 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         if (wv == 0) {
             const int64_t q = base + lane;
             int64_t row = -1;
-            int isU = 0;
+            int isU = 0, c = 0;
             if (q < nU) {
                 if (a.rankU[q] == 0) {
                     const int32_t r = a.occU[q];
-                    if (r >= 0 && a.cntU[r] >= 2) {
+                    c = r >= 0 ? a.cntU[r] : 0;
+                    if (c >= 2) {
                         row = r;
                         isU = 1;
                     }
@@ -1088,18 +1131,21 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 const int64_t k = q - nU;
                 if (a.rankV[k] == 0) {
                     const int32_t r = a.occV[k];
-                    if (a.cntV[r] >= 2) row = r;
+                    c = a.cntV[r];
+                    if (c >= 2) row = r;
                 }
             } else if (q < total) {
                 const int64_t k = q - nU - nV;
                 if (a.served_own[k]) {
                     row = (int64_t)a.served_ids[k] - a.shard_u0;
                     isU = 1;
+                    c = a.cntU[row];
                 }
             }
             const unsigned long long m = __ballot(row >= 0);
             s_row[lane] = row;
             s_isU[lane] = isU;
+            s_cnt[lane] = c;
             if (lane == 0) s_mask = m;
         }
         __syncthreads();
@@ -1108,7 +1154,7 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         for (int k = 0; k < group && m != 0ull; ++k) m &= m - 1ull;
         while (m != 0ull) {  // group-uniform
             const int src = __ffsll((long long)m) - 1;
-            apply_row<EPL>(a, s_row[src], s_isU[src] != 0, gl);
+            apply_row<EPL>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
             for (int k = 0; k < kGroupsPerBlock && m != 0ull; ++k) m &= m - 1ull;
         }
         __syncthreads();  // s_* reused by the next chunk
