@@ -1170,11 +1170,28 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
 // [0, napply)) beside the draw + count of step s+1 (the rest) -- independent
 // work (other buffer set), one launch instead of two
 template <int EPL, int MODEL>
+#ifndef CF_APPLY_PREP_ORDER
+#define CF_APPLY_PREP_ORDER 0  // 0: apply blocks first, 1: draw blocks first, 2: interleaved
+#endif
 __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArgs a, int napply) {
+    const int nprep = (int)gridDim.x - napply;
+#if CF_APPLY_PREP_ORDER == 2
+    int idx;
+    if (minor_block(blockIdx.x, napply, nprep, idx))
+        prep_body<MODEL>(a, idx);
+    else
+        apply_body<EPL>(p, idx, napply);
+#elif CF_APPLY_PREP_ORDER == 1
+    if ((int)blockIdx.x < nprep)
+        prep_body<MODEL>(a, blockIdx.x);
+    else
+        apply_body<EPL>(p, blockIdx.x - nprep, napply);
+#else
     if ((int)blockIdx.x < napply)
         apply_body<EPL>(p, blockIdx.x, napply);
     else
         prep_body<MODEL>(a, blockIdx.x - napply);
+#endif
 }
 
 // ---------------------------------------------------------------------------
