@@ -11,9 +11,10 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CF_ENGINE_LIB", os.path.join(_PKG, "build", "libcf_engine.so"))
 HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "cf_engine.h")
 
-CF_BPR, CF_GBPR, CF_CML, CF_AMF = 0, 1, 2, 3
+CF_BPR, CF_GBPR, CF_CML, CF_AMF, CF_PLR = 0, 1, 2, 3, 4
+CF_PLR_PRIGP, CF_PLR_CPLR = 0, 1
 MODEL_IDS = {"bpr": CF_BPR, "bprmf": CF_BPR, "gbpr": CF_GBPR, "gbprmf": CF_GBPR,
-             "cml": CF_CML, "amf": CF_AMF}
+             "cml": CF_CML, "amf": CF_AMF, "plr": CF_PLR, "prigp": CF_PLR, "cplr": CF_PLR}
 TABLES = {"user": 0, "item": 1, "bias": 2, "acc_user": 3, "acc_item": 4, "acc_bias": 5}
 KERNELS = {"sample": 0, "step": 1, "apply": 2, "apply_dense": 3, "clip": 4, "score": 5,
            "topk": 6, "slot": 7, "apply_prep": 8, "grad_prep": 9, "apply_slot": 10}
@@ -44,8 +45,12 @@ class CfConfig(ctypes.Structure):
         ("use_rank_weight", ctypes.c_int32),
         ("device", ctypes.c_int32),
         ("dense_item_apply", ctypes.c_int32),
-        ("reserved0", ctypes.c_int32),
+        ("plr_kind", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("alpha", ctypes.c_float),
+        ("beta", ctypes.c_float),
+        ("gamma", ctypes.c_float),
+        ("reserved1", ctypes.c_int32),
     ]
 
 
@@ -85,6 +90,7 @@ SIGNATURES = {
     "cf_step_local_grad": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_local_apply": (ctypes.c_int, [_P, _I32]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
+    "cf_step_plr": (ctypes.c_int, [_P, _PI32, _I32, _PF, _I32, _PD]),
     "cf_set_shard": (ctypes.c_int, [_P, _I32, _I32, _PI64]),
     "cf_set_group_source": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
     "cf_bind_exchange": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P, _I64]),

@@ -102,6 +102,8 @@ struct cf_engine {
     hipEvent_t apply_done[2] = {nullptr, nullptr};
     double* loss_partial = nullptr;
     double* loss = nullptr;   // [0] running accumulator, [1] per-call scratch
+    float* coefs = nullptr;   // [B, 2] CPLR tuple coefficients (cf_step_plr)
+    int coefs_cap = 0;
     double* h_loss = nullptr; // pinned
     int32_t* h_stage = nullptr;
     size_t stage_cap = 0;
@@ -199,6 +201,7 @@ struct ProfScope {
     }
 };
 
+bool has_bias(const cf_config& c) { return c.model == CF_GBPR || c.model == CF_PLR; }
 int users_per_pair(const cf_config& c) { return c.model == CF_GBPR ? 1 + c.gsize : 1; }
 int items_per_pair(const cf_config& c) { return 1 + c.n_neg; }
 int group_count(const cf_config& c) { return c.model == CF_GBPR ? c.gsize : 0; }
@@ -282,6 +285,12 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.count_items = c.dense_item_apply ? 0 : 1;
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
+    a.plr_kind = c.plr_kind;
+    a.alpha = c.alpha;
+    a.beta = c.beta;
+    a.gamma = c.gamma;
+    a.train_bias = (c.model == CF_GBPR || (c.model == CF_PLR && c.plr_kind == CF_PLR_CPLR)) ? 1 : 0;
+    a.coefs = e->coefs;
     a.xrows = e->x_rows;
     a.xgrads = e->x_grads;
     return a;
@@ -409,7 +418,8 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
     p.V = e->V; p.AV = e->AV; p.GV = e->GV;
-    p.b = e->b; p.Ab = e->Ab; p.Gb = e->Gb;
+    p.b = a.train_bias ? e->b : nullptr;  // PRIGP keeps b fixed (prigp.py:145)
+    p.Ab = e->Ab; p.Gb = e->Gb;
     p.loss_partial = e->loss_partial;
     p.n_partial = grad_blocks(a);
     p.loss_acc = loss_acc;
@@ -583,7 +593,7 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
         return r;
     }
     FusedTopkArgs f{};
-    f.model = c.model;
+    f.model = c.model == CF_PLR ? CF_GBPR : c.model;  // U.V^T + b (prigp.py:137, cplr_u.py:146)
     f.d = c.n_factors;
     f.Dp = (c.n_factors + 7) & ~7;
     f.Dh = f.Dp / 2;
@@ -647,13 +657,17 @@ void cf_config_defaults(cf_config* c) {
     c->acc_init = 0.1f;      // tf.train.AdagradOptimizer initial_accumulator_value
     c->use_rank_weight = 1;  // cml.py:16
     c->seed = 20261015ull;
+    c->alpha = c->beta = c->gamma = 1.0f;  // prigp.py:22, cplr_u.py:21
 }
 
 int cf_create(const cf_config* cfg, cf_engine** out) {
     if (!cfg || !out) return fail(CF_EINVAL, "null argument");
     *out = nullptr;
     const cf_config& c = *cfg;
-    if (c.model < CF_BPR || c.model > CF_AMF) return fail(CF_EINVAL, "unknown model");
+    if (c.model < CF_BPR || c.model > CF_PLR) return fail(CF_EINVAL, "unknown model");
+    if (c.model == CF_PLR && !((c.plr_kind == CF_PLR_PRIGP && c.n_neg == 3) ||
+                               (c.plr_kind == CF_PLR_CPLR && c.n_neg == 2)))
+        return fail(CF_EINVAL, "PLR: PRIGP takes n_neg 3 (tuple width 5), CPLR n_neg 2 (width 4)");
     if (c.n_factors < 1 || c.n_factors > kMaxFactors) return fail(CF_EINVAL, "n_factors must be 1..256");
     if (c.n_users < 1 || c.n_users > INT32_MAX) return fail(CF_EINVAL, "n_users out of range");
     if (c.n_items < 2 || c.n_items > INT32_MAX) return fail(CF_EINVAL, "n_items out of range");
@@ -697,7 +711,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
         (r = dalloc(&e->cntU_[1], (size_t)c.n_users)) || (r = dalloc(&e->cntV_[1], (size_t)c.n_items)) ||
         (r = dalloc(&e->loss, 2)))
         return bail(r);
-    if (c.model == CF_GBPR) {
+    if (has_bias(c)) {
         if ((r = dalloc(&e->b, (size_t)c.n_items)) || (r = dalloc(&e->Ab, (size_t)c.n_items)) ||
             (r = dalloc(&e->Gb_own, (size_t)c.n_items)))
             return bail(r);
@@ -721,7 +735,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     if (launch_fill(e->AU, (int64_t)ud, c.acc_init, s) != hipSuccess ||
         launch_fill(e->AV, (int64_t)id, c.acc_init, s) != hipSuccess)
         return bail(fail(CF_EHIP, "fill kernel failed"));
-    if (c.model == CF_GBPR) {
+    if (has_bias(c)) {
         if (hipMemsetAsync(e->b, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
             hipMemsetAsync(e->Gb, 0, (size_t)c.n_items * 4, s) != hipSuccess ||
             launch_fill(e->Ab, c.n_items, c.acc_init, s) != hipSuccess)
@@ -754,7 +768,7 @@ int cf_destroy(cf_engine* e) {
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
-    dfree(e->slotU); dfree(e->slotV); dfree(e->x_own);
+    dfree(e->slotU); dfree(e->slotV); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -846,7 +860,7 @@ int cf_init_params(cf_engine* e, float mean, float stddev, int32_t truncated, ui
     CF_HIP(launch_init_normal(e->V, id, mean, stddev, truncated, mix64_host(seed ^ 0xAAu), e->stream));
     CF_HIP(launch_fill(e->AU, ud, c.acc_init, e->stream));
     CF_HIP(launch_fill(e->AV, id, c.acc_init, e->stream));
-    if (c.model == CF_GBPR) {
+    if (has_bias(c)) {
         CF_HIP(launch_init_normal(e->b, c.n_items, mean, stddev, truncated, mix64_host(seed ^ 0xBBu), e->stream));
         CF_HIP(launch_fill(e->Ab, c.n_items, c.acc_init, e->stream));
     }
@@ -885,6 +899,7 @@ int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
 int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32_t* groups,
             int32_t B, double* loss_out) {
     CF_TRY(check_engine(e));
+    if (e->cfg.model == CF_PLR) return fail(CF_EINVAL, "tuple models step through cf_step_plr");
     CF_TRY(discard_pending(e));
     CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
@@ -898,8 +913,40 @@ int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32
     return CF_OK;
 }
 
+int cf_step_plr(cf_engine* e, const int32_t* tuples, int32_t width, const float* coefs, int32_t B,
+                double* loss_out) {
+    CF_TRY(check_engine(e));
+    CF_TRY(discard_pending(e));
+    const cf_config& c = e->cfg;
+    if (c.model != CF_PLR) return fail(CF_EINVAL, "cf_step_plr needs model CF_PLR");
+    if (B < 1 || !tuples) return fail(CF_EINVAL, "bad arguments");
+    if (width != c.n_neg + 2) return fail(CF_EINVAL, "tuple width must be n_neg + 2");
+    if (c.plr_kind == CF_PLR_CPLR && !coefs) return fail(CF_EINVAL, "CPLR needs coefs [B, 2]");
+    const int W = c.n_neg;
+    std::vector<int32_t> pairs((size_t)B * 2), negs((size_t)B * W);
+    for (int p = 0; p < B; ++p) {
+        pairs[2 * p] = tuples[(size_t)p * width];
+        pairs[2 * p + 1] = tuples[(size_t)p * width + 1];
+        for (int w = 0; w < W; ++w) negs[(size_t)p * W + w] = tuples[(size_t)p * width + 2 + w];
+    }
+    if (c.plr_kind == CF_PLR_CPLR) {
+        CF_HIP(hipStreamSynchronize(e->stream));  // the previous step may still read the buffer
+        if (B > e->coefs_cap) {
+            dfree(e->coefs);
+            CF_TRY(dalloc(&e->coefs, (size_t)B * 2));
+            e->coefs_cap = B;
+        }
+        CF_HIP(hipMemcpy(e->coefs, coefs, (size_t)B * 2 * sizeof(float), hipMemcpyHostToDevice));
+    }
+    double* acc = loss_out ? e->loss + 1 : e->loss;
+    CF_TRY(run_step(e, B, pairs.data(), negs.data(), nullptr, acc));
+    if (loss_out) CF_TRY(read_loss(e, 1, loss_out));
+    return CF_OK;
+}
+
 int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_out) {
     CF_TRY(check_engine(e));
+    if (e->cfg.model == CF_PLR) return fail(CF_EINVAL, "tuple models are host-fed (cf_step_plr)");
     CF_TRY(discard_pending(e));
     CF_TRY(check_not_xchg(e));
     if (B < 1 || n_steps < 0) return fail(CF_EINVAL, "bad B / n_steps");
@@ -996,7 +1043,7 @@ int cf_bind_item_grad(cf_engine* e, void* ptr, int64_t n) {
     const cf_config& c = e->cfg;
     if (!c.dense_item_apply) return fail(CF_ESTATE, "cf_bind_item_grad needs dense_item_apply=1");
     const int64_t id = c.n_items * (int64_t)c.n_factors;
-    const int64_t want = id + (c.model == CF_GBPR ? c.n_items : 0);
+    const int64_t want = id + (has_bias(c) ? c.n_items : 0);
     if (n != want) return fail(CF_EINVAL, "item-grad buffer must hold " + std::to_string(want) + " floats");
     if (!ptr) {
         e->GV = e->GV_own;
@@ -1007,7 +1054,7 @@ int cf_bind_item_grad(cf_engine* e, void* ptr, int64_t n) {
     if (hipPointerGetAttributes(&attr, ptr) != hipSuccess || attr.type != hipMemoryTypeDevice)
         return fail(CF_EINVAL, "item-grad buffer is not device memory");
     e->GV = (float*)ptr;
-    e->Gb = (c.model == CF_GBPR) ? (float*)ptr + id : e->Gb_own;
+    e->Gb = has_bias(c) ? (float*)ptr + id : e->Gb_own;
     CF_HIP(hipMemsetAsync(ptr, 0, (size_t)n * 4, e->stream));
     return CF_OK;
 }
@@ -1301,7 +1348,7 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     for (int u0 = 0; he == hipSuccess && u0 < n; u0 += chunk) {
         const int m = std::min(chunk, n - u0);
         ScoreArgs s{};
-        s.model = c.model;
+        s.model = c.model == CF_PLR ? CF_GBPR : c.model;
         s.d = c.n_factors;
         s.n_users = m;
         s.n_items = c.n_items;

@@ -21,7 +21,7 @@ constexpr int kMaxNeg = 64;
 constexpr int kMaxGroup = 16;
 constexpr int kMaxFactors = 256;
 
-enum Model { BPR = 0, GBPR = 1, CML = 2, AMF = 3 };
+enum Model { BPR = 0, GBPR = 1, CML = 2, AMF = 3, PLR = 4 };
 
 // Keyed bijection on [0, n) used as the per-epoch shuffle of the nnz pairs
 // (replaces np.random.shuffle(useritem_pairs), sampler_ranking.py:24).
@@ -85,6 +85,11 @@ struct StepArgs {
     int64_t shard_u0, shard_u1;
     const float* __restrict__ xrows;  // [sent, d] rows of other ranks' group users
     float* __restrict__ xgrads;       // [sent, d] their gradient rows
+    // tuple ranking (PLR): occV holds the tuple's items, W = width - 2
+    int plr_kind;                     // 0 PRIGP, 1 CPLR
+    float alpha, beta, gamma;
+    int train_bias;                   // CPLR trains b (cplr_u.py:152); PRIGP does not (prigp.py:145)
+    const float* __restrict__ coefs;  // [B, 2] CPLR (coefMat[u,i], coefMat[u,t])
 };
 
 // a row of this rank's user table that other ranks' batches touch: its count

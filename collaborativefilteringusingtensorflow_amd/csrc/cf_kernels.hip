@@ -597,6 +597,68 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             }
             if (gl == 0) bias_finish(a, i, ci, sc);
             gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+        } else if (MODEL == PLR) {
+            // tuple ranking: s_x = <u, v_x> + b_x over the tuple's items
+            // (x0 = i, x1.. = J); weighted -log sigmoid(coef (s_a - s_b)) terms
+            //   PRIGP (u,i,j,t,k): (i,j; 1; 1), (t,k; 1; alpha)       prigp.py:99-130
+            //   CPLR (u,i,t,j) + (c0,c1): (i,t; (c0+1)/(c1+1); alpha),
+            //        (t,j; c1+1; beta), (i,j; c0+1; gamma)           cplr_u.py:106-137
+            constexpr int NX = WT + 1;
+            float sx[NX], bx[NX], ds[NX];
+            sx[0] = gdot<EPL>(uu, vi);
+            bx[0] = a.b[i];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                sx[w + 1] = gdot<EPL>(uu, J.v[w]);
+                bx[w + 1] = a.b[J.j[w]];
+            }
+#pragma unroll
+            for (int x = 0; x < NX; ++x) {
+                sx[x] += bx[x];
+                ds[x] = 0.f;
+                loss_g += 0.5f * a.reg * bx[x] * bx[x];
+            }
+            auto term = [&](int xa, int xb, float coef, float wt) {
+                const float z = coef * (sx[xa] - sx[xb]);
+                loss_g += wt * neg_log_sigmoid(z);
+                const float g = wt * coef * (-1.f / (1.f + expf(z)));
+                ds[xa] += g;
+                ds[xb] -= g;
+            };
+            if (a.plr_kind == 0) {
+                term(0, 1, 1.f, 1.f);
+                if (NX > 3) term(2, 3 < NX ? 3 : 2, 1.f, a.alpha);
+            } else {
+                const float uij = a.coefs[2 * p] + 1.f, utj = a.coefs[2 * p + 1] + 1.f;
+                term(0, 1, uij / utj, a.alpha);
+                term(1, 2 < NX ? 2 : 1, utj, a.beta);
+                term(0, 2 < NX ? 2 : 1, uij, a.gamma);
+            }
+            float gu[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) gu[s] = a.reg * uu[s] + ds[0] * vi[s];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                float gj[EPL];
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] = fmaf(ds[w + 1], J.v[w][s], gu[s]);
+                    gj[s] = ds[w + 1] * uu[s] + a.reg * J.v[w][s];
+                    sq = fmaf(J.v[w][s], J.v[w][s], sq);
+                }
+                if (a.train_bias && gl == 0) bias_finish(a, J.j[w], J.c[w], ds[w + 1] + a.reg * bx[w + 1]);
+                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[w], J.c[w], J.sl[w], d, gl, J.v[w], gj, a);
+            }
+            float gi[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gi[s] = ds[0] * uu[s] + a.reg * vi[s];
+                sq = fmaf(uu[s], uu[s], sq);
+                sq = fmaf(vi[s], vi[s], sq);
+            }
+            gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+            if (a.train_bias && gl == 0) bias_finish(a, i, ci, ds[0] + a.reg * bx[0]);
+            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
 #pragma unroll
@@ -1174,7 +1236,9 @@ template <int EPL, int MODEL>
 #define CF_APPLY_PREP_ORDER 0  // 0: apply blocks first, 1: draw blocks first, 2: interleaved
 #endif
 __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArgs a, int napply) {
+#if CF_APPLY_PREP_ORDER != 0
     const int nprep = (int)gridDim.x - napply;
+#endif
 #if CF_APPLY_PREP_ORDER == 2
     int idx;
     if (minor_block(blockIdx.x, napply, nprep, idx))
@@ -1475,6 +1539,13 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
 
 // W = 1 (BPRMF driver) and W = 5 (AMF / CML / GBPR drivers) with G <= 1 and
 // d <= 128 take the phased fast path; anything else the generic kernel
+// tuple ranking: prefetched tuples of width 4 (CPLR, W = 2) or 5 (PRIGP, W = 3)
+static hipError_t launch_grad_plr(const StepArgs& a, hipStream_t s) {
+    if (a.W == 2) return launch_grad_w<PLR, 2>(a, nullptr, s);
+    if (a.W == 3) return launch_grad_w<PLR, 3>(a, nullptr, s);
+    return hipErrorInvalidValue;
+}
+
 template <int MODEL>
 static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     const int e = epl_for(a.d);
@@ -1493,6 +1564,7 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
         case BPR: return launch_grad_m<BPR>(a, next, s);
         case GBPR: return launch_grad_m<GBPR>(a, next, s);
         case CML: return launch_grad_m<CML>(a, next, s);
+        case PLR: return next ? hipErrorInvalidValue : launch_grad_plr(a, s);
         default: return launch_grad_m<AMF>(a, next, s);
     }
 }

@@ -24,10 +24,17 @@ class Engine(object):
     def __init__(self, model, n_users, n_items, n_factors, n_neg=1, gsize=1, lr=0.1,
                  reg=0.02, rho=0.5, margin=1.5, reg_cov=1.0, clip_norm=1.0, reg_adv=1.0,
                  epsilon=0.5, acc_init=0.1, use_rank_weight=True, device=0,
-                 dense_item_apply=False, seed=20261015):
+                 dense_item_apply=False, seed=20261015, plr_kind=None, alpha=1.0, beta=1.0,
+                 gamma=1.0):
         L = N.lib()
         if isinstance(model, str):
-            model = N.MODEL_IDS[model.lower()]
+            name = model.lower()
+            model = N.MODEL_IDS[name]
+            if name in ("prigp", "cplr"):   # tuple models: the tuple width fixes n_neg
+                plr_kind = N.CF_PLR_PRIGP if name == "prigp" else N.CF_PLR_CPLR
+        if int(model) == N.CF_PLR:
+            plr_kind = N.CF_PLR_PRIGP if plr_kind is None else int(plr_kind)
+            n_neg = 3 if plr_kind == N.CF_PLR_PRIGP else 2
         cfg = N.CfConfig()
         L.cf_config_defaults(ctypes.byref(cfg))
         cfg.model = int(model)
@@ -48,12 +55,15 @@ class Engine(object):
         cfg.use_rank_weight = 1 if use_rank_weight else 0
         cfg.device = int(device)
         cfg.dense_item_apply = 1 if dense_item_apply else 0
+        cfg.plr_kind = int(plr_kind or 0)
+        cfg.alpha, cfg.beta, cfg.gamma = float(alpha), float(beta), float(gamma)
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.cfg = cfg
         self.model = int(model)
         self.n_users, self.n_items, self.d = int(n_users), int(n_items), int(n_factors)
         self.n_neg = int(n_neg)
         self.gsize = int(gsize) if self.model == N.CF_GBPR else 0
+        self.plr_kind = int(plr_kind or 0)
         self._h = ctypes.c_void_p()
         N.check(L.cf_create(ctypes.byref(cfg), ctypes.byref(self._h)), "cf_create")
         self._L = L
@@ -132,6 +142,20 @@ class Engine(object):
         N.check(self._L.cf_step(self._h, _ptr(pairs, ctypes.c_int32), _ptr(negs, ctypes.c_int32),
                                 gp, B, ctypes.byref(loss) if return_loss else None), "cf_step")
         return float(loss.value) if return_loss else None
+
+    def step_plr(self, tuples, coefs=None, return_loss=True):
+        """One host-fed tuple step (CF_PLR): tuples [B, n_neg + 2] int
+        ((u,i,j,t,k) PRIGP / (u,i,t,j) CPLR), coefs [B, 2] float (CPLR)."""
+        t = _i32(tuples)
+        B, width = t.shape
+        cp = None
+        if coefs is not None:
+            c = np.ascontiguousarray(coefs, dtype=np.float32).reshape(B, 2)
+            cp = _ptr(c, ctypes.c_float)
+        out = ctypes.c_double(0.0)
+        N.check(self._L.cf_step_plr(self._h, _ptr(t, ctypes.c_int32), int(width), cp, int(B),
+                                    ctypes.byref(out) if return_loss else None), "cf_step_plr")
+        return float(out.value) if return_loss else None
 
     def train_steps(self, batch_size, n_steps, return_loss=True):
         loss = ctypes.c_double(0.0)

@@ -39,7 +39,14 @@ enum cf_model {
     CF_BPR = 0,   /* src/models/pl/models/bprmf.py   */
     CF_GBPR = 1,  /* src/models/pl/models/gbprmf.py  */
     CF_CML = 2,   /* src/models/pl/models/cml.py     */
-    CF_AMF = 3    /* src/models/others/models/amf.py */
+    CF_AMF = 3,   /* src/models/others/models/amf.py */
+    CF_PLR = 4    /* tuple ranking: PRIGP (prigp.py:99-130) / CPLR (cplr_u.py:106-137) */
+};
+
+enum cf_plr_kind {
+    CF_PLR_PRIGP = 0,  /* (u,i,j,t,k): -log s(ui-uj) - alpha log s(ut-uk); U,V trained, b fixed */
+    CF_PLR_CPLR = 1    /* (u,i,t,j)+(c_ui,c_ut): alpha/beta/gamma weighted, coefficient-scaled;
+                          U,V,b trained */
 };
 
 enum cf_status {
@@ -108,8 +115,10 @@ typedef struct cf_config {
     int32_t use_rank_weight;  /* CML rank weight on/off                         */
     int32_t device;           /* HIP device ordinal                             */
     int32_t dense_item_apply; /* 1: item Adagrad over all rows (multi-rank)     */
-    int32_t reserved0;
+    int32_t plr_kind;         /* enum cf_plr_kind (CF_PLR)                      */
     uint64_t seed;            /* device sampler / init seed                     */
+    float alpha, beta, gamma; /* PLR term weights (prigp.py:128, cplr_u.py:136) */
+    int32_t reserved1;
 } cf_config;
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -258,6 +267,16 @@ int cf_xchg_finish(cf_engine* eng, int64_t n_recv);
 
 /* Pre-update loss accumulated since the last call (syncs), then reset. */
 int cf_take_loss(cf_engine* eng, double* loss_sum_out);
+
+/* ---- tuple ranking step (CF_PLR) ------------------------------------------------
+ * One host-fed optimizer step on B tuples [B, width] (int32):
+ *   PRIGP width 5: (u, i, j, t, k)  (sampler_prigp.py:51; prigp.py:99-130)
+ *   CPLR  width 4: (u, i, t, j)     (sampler_uitj_ranking.py:35; cplr_u.py:106-137)
+ * with coefs [B, 2] = (coefMat[u,i], coefMat[u,t]) for CPLR (NULL for PRIGP).
+ * Scores s_x = <U_u, V_x> + b_x; loss = sum of weighted -log sigmoid terms
+ * + reg (l2(U_u) + l2(V_items) + l2(b_items)); TF1 dedup-sum Adagrad. */
+int cf_step_plr(cf_engine* eng, const int32_t* host_tuples, int32_t width, const float* host_coefs,
+                int32_t B, double* loss_out);
 
 /* ---- evaluation ----------------------------------------------------------- */
 /*

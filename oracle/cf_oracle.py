@@ -279,6 +279,56 @@ def cml_step(U, V, AU, AV, pairs, negs, margin, reg_cov, clip_norm,
 
 
 # ----------------------------------------------------------------------------
+# tuple ranking: PRIGP (src/models/pl/models/prigp.py:99-147) and
+# CPLR (src/models/pl/models/cplr_u.py:98-154)
+# ----------------------------------------------------------------------------
+def plr_terms(kind, coefs, B, alpha, beta, gamma, dt):
+    """(a, b, coef[B], weight) per loss term over the tuple's item positions.
+    PRIGP (u,i,j,t,k) -> items (i,j,t,k): uij + alpha*utk      (prigp.py:125-128)
+    CPLR  (u,i,t,j) -> items (i,t,j), coef_ui = c0+1, coef_ut = c1+1:
+        alpha*uit(coef (c0+1)/(c1+1)) + beta*utj(c1+1) + gamma*uij(c0+1)
+                                                              (cplr_u.py:128-136)"""
+    one = np.ones(B, dtype=dt)
+    if kind == 0:
+        return [(0, 1, one, dt(1)), (2, 3, one, dt(alpha))]
+    c = np.asarray(coefs, dtype=np.float32).astype(dt)   # tf.float32 placeholder
+    uij, utj = c[:, 0] + dt(1), c[:, 1] + dt(1)
+    return [(0, 1, uij / utj, dt(alpha)), (1, 2, utj, dt(beta)), (0, 2, uij, dt(gamma))]
+
+
+def plr_step(U, V, b, AU, AV, Ab, tuples, coefs, kind, reg, alpha=1.0, beta=1.0, gamma=1.0,
+             lr=0.1):
+    """One PRIGP (kind 0) / CPLR (kind 1) train step on tuples [B, 1+T].
+    s_x = <U_u, V_x> + b_x; loss = sum_terms w * -log sigmoid(coef (s_a - s_b))
+    + reg (l2(U_u) + l2(V_x) + l2(b_x)) over every tuple position.  PRIGP trains
+    U, V only (prigp.py:145); CPLR trains U, V, b (cplr_u.py:152)."""
+    dt = U.dtype.type
+    t = np.asarray(tuples)
+    B = t.shape[0]
+    u, X = t[:, 0], t[:, 1:]
+    Uu, VX, bX = U[u], V[X], b[X]
+    s = np.sum(Uu[:, None, :] * VX, axis=-1) + bX
+    reg = dt(reg)
+    loss = reg * (_l2(Uu) + _l2(VX) + _l2(bX))
+    ds = np.zeros_like(s)
+    for a, bb, coef, w in plr_terms(kind, coefs, B, alpha, beta, gamma, dt):
+        z = coef * (s[:, a] - s[:, bb])
+        loss += w * np.sum(_neg_log_sigmoid(z))
+        g = w * coef * _c_bpr(z).astype(U.dtype)
+        ds[:, a] += g
+        ds[:, bb] -= g
+    d = U.shape[1]
+    gU = np.sum(ds[:, :, None] * VX, axis=1) + reg * Uu
+    gV = ds[:, :, None] * Uu[:, None, :] + reg * VX
+    gb = ds + reg * bX
+    dedup_adagrad(U, AU, u, gU, lr)
+    dedup_adagrad(V, AV, X.reshape(-1), gV.reshape(-1, d), lr)
+    if kind == 1:
+        dedup_adagrad(b, Ab, X.reshape(-1), gb.reshape(-1), lr)
+    return float(loss)
+
+
+# ----------------------------------------------------------------------------
 # scoring / recommend  (bprmf.py:77-103 and siblings)
 # ----------------------------------------------------------------------------
 def predict(model, U, V, b, users):
@@ -289,7 +339,7 @@ def predict(model, U, V, b, users):
         diff = Uu[:, None, :] - V[None, :, :]
         return -np.sum(diff * diff, axis=-1)
     S = Uu @ V.T
-    if model == "gbpr":
+    if model in ("gbpr", "prigp", "cplr"):
         S = S + b[None, :]
     return S
 

@@ -1,0 +1,91 @@
+"""Tuple ranking models on the engine (CF_PLR): PRIGP (prigp.py:99-147) and
+CPLR (cplr_u.py:98-154), host-fed through cf_step_plr, against the float64
+oracle (oracle/cf_oracle.py plr_step, itself pinned to autograd of the literal
+loss graphs in tests/test_oracle.py): 1e-5 relative after K steps on tuples
+with repeated users / items (the TF1 dedup-sum path) and in every slot regime;
+the recommend step scores U.V^T + b."""
+import numpy as np
+import pytest
+
+from oracle import cf_oracle as O
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a, np.float64) - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def tuples_for(rng, fold1, B, width):
+    """Valid-looking tuples: (u, i in Pos(u), ...) plus repeats inside the batch."""
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    users = rng.randint(0, 943, B)
+    users[: B // 5] = users[0]                            # one hot user
+    out = np.zeros((B, width), np.int32)
+    for r, u in enumerate(users):
+        row = ix[ip[u]:ip[u + 1]]
+        out[r, 0] = u
+        out[r, 1] = row[rng.randint(len(row))] if len(row) else rng.randint(1682)
+        out[r, 2:] = rng.randint(0, 1682, width - 2)
+    out[B // 3: B // 2, -1] = out[B // 3: B // 2, 1]      # item repeated inside a tuple
+    out[: B // 4, 2] = 7                                  # a hot item
+    return out
+
+
+@pytest.mark.parametrize("name,kind,width,hp", [
+    ("prigp", 0, 5, dict(reg=0.01, alpha=1.0)),
+    ("prigp", 0, 5, dict(reg=0.05, alpha=0.5)),
+    ("cplr", 1, 4, dict(reg=0.01, alpha=1.0, beta=1.0, gamma=1.0)),
+    ("cplr", 1, 4, dict(reg=0.02, alpha=0.7, beta=1.3, gamma=0.5)),
+])
+@pytest.mark.parametrize("slot_max", [32, 2])
+def test_plr_trajectory_matches_oracle(fold1, name, kind, width, hp, slot_max):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    rng = np.random.RandomState(21 + kind)
+    d = 24
+    U = O.init_table(rng, (943, d))
+    V = O.init_table(rng, (1682, d))
+    b = O.init_table(rng, (1682,))
+    e = Engine(name, 943, 1682, d, reg=hp["reg"], alpha=hp.get("alpha", 1.0),
+               beta=hp.get("beta", 1.0), gamma=hp.get("gamma", 1.0))
+    e.set_option("slot_max", slot_max)
+    e.set_option("slot_max_user", slot_max)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.set_table("user", U)
+    e.set_table("item", V)
+    e.set_table("bias", b)
+    U64, V64, b64 = U.astype(np.float64), V.astype(np.float64), b.astype(np.float64)
+    AU, AV, Ab = np.full_like(U64, 0.1), np.full_like(V64, 0.1), np.full_like(b64, 0.1)
+    for s in range(12):
+        tup = tuples_for(rng, fold1, 300, width)
+        coefs = rng.gamma(1.0, 1.0, (300, 2)).astype(np.float32) if kind == 1 else None
+        lg = e.step_plr(tup, coefs)
+        lo = O.plr_step(U64, V64, b64, AU, AV, Ab, tup, coefs, kind, hp["reg"],
+                        hp.get("alpha", 1.0), hp.get("beta", 1.0), hp.get("gamma", 1.0))
+        assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
+    for t, o in (("user", U64), ("item", V64), ("bias", b64), ("acc_user", AU),
+                 ("acc_item", AV), ("acc_bias", Ab)):
+        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+    if kind == 0:   # PRIGP trains U and V only (prigp.py:145)
+        assert np.array_equal(e.get_table("bias"), b)
+    users = np.arange(0, 943, 7, dtype=np.int32)
+    idx = e.score_topk(users, 10)
+    S = O.predict(name, U64, V64, b64, users)
+    ref = O.recommend(S, fold1["train_indptr"], fold1["train_indices"], users, 10)
+    assert sum(1 for a, c in zip(idx.tolist(), ref) if a != c) <= 2
+    e.close()
+
+
+def test_plr_rejects_wrong_width(fold1):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    from collaborativefilteringusingtensorflow_amd._native import NativeError
+    e = Engine("cplr", 943, 1682, 8)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    with pytest.raises(NativeError):
+        e.step_plr(np.zeros((4, 5), np.int32), np.zeros((4, 2), np.float32))
+    with pytest.raises(NativeError):
+        e.step_plr(np.zeros((4, 4), np.int32), None)          # CPLR needs coefficients
+    with pytest.raises(NativeError):
+        e.train_steps(4, 1)
+    e.close()

@@ -259,3 +259,58 @@ def test_recommend_filter_equivalence():
     a = O.recommend(S, ip, ix, list(range(30)), 10)
     b = O.recommend_literal(S, sets, 10)
     assert a == b
+
+
+def literal_plr_loss(kind, U, V, b, tuples, coefs, hp):
+    """Literal transcription of prigp.py:99-130 / cplr_u.py:98-137."""
+    t = torch.as_tensor(tuples, dtype=torch.long)
+    reg = hp["reg"] * (0.5 * (U[t[:, 0]] ** 2).sum() + 0.5 * (V[t[:, 1:]] ** 2).sum()
+                       + 0.5 * (b[t[:, 1:]] ** 2).sum())
+    s = [(U[t[:, 0]] * V[t[:, c]]).sum(1) + b[t[:, c]] for c in range(1, t.shape[1])]
+    nls = lambda x: (-torch.log(torch.sigmoid(x))).sum()
+    if kind == 0:   # (u,i,j,t,k): uij + alpha * utk
+        return nls(s[0] - s[1]) + hp["alpha"] * nls(s[2] - s[3]) + reg
+    c = torch.as_tensor(np.asarray(coefs, np.float32), dtype=torch.float64)
+    utj_coef, uij_coef = c[:, 1] + 1.0, c[:, 0] + 1.0
+    uit_coef = uij_coef / utj_coef
+    i_, t_, j_ = s
+    return (hp["alpha"] * nls(uit_coef * (i_ - t_)) + hp["beta"] * nls(utj_coef * (t_ - j_))
+            + hp["gamma"] * nls(uij_coef * (i_ - j_)) + reg)
+
+
+def random_tuples(rng, B, width, nu=943, ni=1682):
+    t = np.concatenate([rng.randint(0, nu, (B, 1)), rng.randint(0, ni, (B, width - 1))], 1)
+    t[: B // 4, 3 if width == 5 else 2] = t[: B // 4, 1]   # repeated items inside tuples
+    return t.astype(np.int32)
+
+
+@pytest.mark.parametrize("kind,width,hp", [
+    (0, 5, dict(reg=0.01, alpha=1.0)), (0, 5, dict(reg=0.05, alpha=0.5)),
+    (1, 4, dict(reg=0.01, alpha=1.0, beta=1.0, gamma=1.0)),
+    (1, 4, dict(reg=0.02, alpha=0.7, beta=1.3, gamma=0.5)),
+])
+def test_plr_oracle_matches_literal_autograd(kind, width, hp):
+    rng = np.random.RandomState(7 + kind)
+    tabs = init(5, bias=True)
+    ora = {k: v.copy() for k, v in tabs.items()}
+    oacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    tacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    for s in range(5):
+        tup = random_tuples(rng, 200, width)
+        coefs = rng.gamma(1.0, 1.0, (200, 2)) if kind == 1 else None
+        T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tabs.items()}
+        loss = literal_plr_loss(kind, T["U"], T["V"], T["b"], tup, coefs, hp)
+        loss.backward()
+        for k, tt in T.items():
+            if k == "b" and kind == 0:   # PRIGP's var_list excludes item_bias (prigp.py:145)
+                continue
+            g = tt.grad.numpy()
+            tacc[k] = tacc[k] + g * g
+            tabs[k] = tt.detach().numpy() - 0.1 * g / np.sqrt(tacc[k])
+        lo = O.plr_step(ora["U"], ora["V"], ora["b"], oacc["U"], oacc["V"], oacc["b"], tup, coefs,
+                        kind, hp["reg"], hp.get("alpha", 1.0), hp.get("beta", 1.0),
+                        hp.get("gamma", 1.0))
+        assert abs(lo - float(loss.detach())) <= TOL * abs(float(loss.detach()))
+        for k in tabs:
+            assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
+            assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
