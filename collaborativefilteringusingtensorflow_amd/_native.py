@@ -111,6 +111,16 @@ SIGNATURES = {
     "cf_mt_sampler_next": (ctypes.c_int, [_P, _PI32, _PI32, _PI32]),
     "cf_mt_sampler_state": (ctypes.c_int, [_P, _PI64, _PI64]),
     "cf_mt_sampler_free": (ctypes.c_int, [_P]),
+    "cf_ens_create": (ctypes.c_int, [_I64, _I64, _I32, _I32, _F, _F, _F, _I32, ctypes.POINTER(_P)]),
+    "cf_ens_destroy": (ctypes.c_int, [_P]),
+    "cf_ens_init_params": (ctypes.c_int, [_P, _F, _F, _I32, _U64]),
+    "cf_ens_set_lr": (ctypes.c_int, [_P, _F]),
+    "cf_ens_set_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
+    "cf_ens_get_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
+    "cf_ens_set_interactions": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
+    "cf_ens_step": (ctypes.c_int, [_P, _PI32, _I32, _PD]),
+    "cf_ens_take_loss": (ctypes.c_int, [_P, _PD]),
+    "cf_ens_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
     "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
     "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),
 }

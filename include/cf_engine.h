@@ -357,6 +357,34 @@ int cf_mt_sampler_next(cf_mt_sampler* s, int32_t* pairs /*[B,2]*/, int32_t* negs
 int cf_mt_sampler_state(const cf_mt_sampler* s, int64_t* epoch_out, int64_t* batch_out);
 int cf_mt_sampler_free(cf_mt_sampler* s);
 
+/* ---- attention-weighted MF ensemble ----------------------
+ * src/models/pl/models/ensemble.py: K members U[K,n_users,d], V[K,n_items,d],
+ * H[K,d] (all truncated-normal), trained on sampler_uij_ranking (u,i,j)
+ * batches with dense Adagrad (ensemble.py:146) and lr decayed 0.98/epoch by
+ * the caller (cf_ens_set_lr, ensemble.py:218).  The loss is the reference
+ * graph's, including its [B] x [B,1] broadcast (ensemble.py:84-91): all B x B
+ * (p, q) pairs of z = sum_k w_k(i_p) s_k(i_q) - w_k(j_p) s_k(j_q),
+ * w_k = softmax_k(<U_k[u] o V_k[x], h_k>) -- plus reg * (l2 of the looked-up
+ * rows + l2(H)).  Tables for get/set: 0 U, 1 V, 2 H, 3-5 their Adagrad
+ * accumulators; sizes in floats.  Recommend = ensemble.py:128-140 scores
+ * + the top-k / exclude rules of cf_score_topk. */
+typedef struct cf_ensemble cf_ensemble;
+int cf_ens_create(int64_t n_users, int64_t n_items, int32_t K, int32_t d, float reg, float lr,
+                  float acc_init, int32_t device, cf_ensemble** out);
+int cf_ens_destroy(cf_ensemble* e);
+int cf_ens_init_params(cf_ensemble* e, float mean, float stddev, int32_t truncated, uint64_t seed);
+int cf_ens_set_lr(cf_ensemble* e, float lr);
+int cf_ens_set_table(cf_ensemble* e, int32_t table, const float* host_src, int64_t n);
+int cf_ens_get_table(cf_ensemble* e, int32_t table, float* host_dst, int64_t n);
+int cf_ens_set_interactions(cf_ensemble* e, const int64_t* indptr, const int32_t* indices, int64_t nnz);
+/* one optimizer step on B host triplets [B,3] int32; loss_out (may be NULL,
+ * else syncs) = the pre-update loss of the batch */
+int cf_ens_step(cf_ensemble* e, const int32_t* host_uij, int32_t B, double* loss_out);
+/* sum of the step losses since the last call (syncs), then reset */
+int cf_ens_take_loss(cf_ensemble* e, double* sum_out);
+int cf_ens_score_topk(cf_ensemble* e, const int32_t* host_users, int32_t n, int32_t k,
+                      int32_t exclude_train, int32_t* host_idx_out, float* host_val_out);
+
 /* ---- synthetic implicit-feedback graphs (bench configs) --------- */
 /*
  * Users [u_begin, u_end) of a graph with per-user degree 1 + Poisson(mean-1)

@@ -328,6 +328,68 @@ def plr_step(U, V, b, AU, AV, Ab, tuples, coefs, kind, reg, alpha=1.0, beta=1.0,
     return float(loss)
 
 
+def ens_forward(U, V, H, uij):
+    """Per-member quantities of ensemble.py:71-93 for a [B, 3] batch:
+    s_k(x) = <U_k[u], V_k[x]>, w_k(x) = exp(<U_k[u] o V_k[x], h_k>) / sum_k'
+    (x = i, j), each [K, B]."""
+    t = np.asarray(uij)
+    u, i, j = t[:, 0], t[:, 1], t[:, 2]
+    Uu, Vi, Vj = U[:, u], V[:, i], V[:, j]           # [K, B, d]
+    ui, uj = Uu * Vi, Uu * Vj
+    si, sj = ui.sum(-1), uj.sum(-1)
+    ai = np.exp(np.einsum("kbd,kd->kb", ui, H))     # ensemble.py:84
+    aj = np.exp(np.einsum("kbd,kd->kb", uj, H))
+    return Uu, Vi, Vj, si, sj, ai / ai.sum(0), aj / aj.sum(0)
+
+
+def ens_step(U, V, H, AU, AV, AH, uij, reg, lr=0.1):
+    """One Ensemble train step (ensemble.py:58-114, 144-148), in place.
+
+    The reference multiplies the [B] score vector by the [B, 1] attention
+    column (ensemble.py:89-91), so ui_rating - uj_rating is a [B, B] matrix:
+    z[p, q] = sum_k w_k(i_p) s_k(i_q) - w_k(j_p) s_k(j_q), and the loss sums
+    -log sigmoid over all of it.  reg * (sum_k l2(U_k[u]) + l2(V_k[(i, j)]))
+    + reg * l2(H) (ensemble.py:58-69).  The strided slices U[k] make every
+    gradient dense, so the update is dense ApplyAdagrad on U, V, H (rows with
+    zero gradient do not move).  Returns the pre-update loss."""
+    dt = U.dtype.type
+    reg = dt(reg)
+    t = np.asarray(uij)
+    u, i, j = t[:, 0], t[:, 1], t[:, 2]
+    Uu, Vi, Vj, si, sj, wi, wj = ens_forward(U, V, H, t)
+    z = wi.T @ si - wj.T @ sj                        # [p, q]
+    loss = float(np.sum(_neg_log_sigmoid(z)))
+    loss += float(reg * (_l2(Uu) + _l2(Vi) + _l2(Vj) + _l2(H)))
+    c = _c_bpr(z).astype(U.dtype)                    # dL/dz
+    dwi, dwj = si @ c.T, -(sj @ c.T)                 # [K, p]
+    dsi, dsj = wi @ c, -(wj @ c)                     # [K, q]
+    dei = wi * (dwi - np.sum(wi * dwi, axis=0))      # softmax backward
+    dej = wj * (dwj - np.sum(wj * dwj, axis=0))
+    vi = dsi[:, :, None] + dei[:, :, None] * H[:, None, :]   # dL/d(u o i)
+    vj = dsj[:, :, None] + dej[:, :, None] * H[:, None, :]
+    GU, GV = np.zeros_like(U), np.zeros_like(V)
+    K = U.shape[0]
+    for k in range(K):
+        np.add.at(GU[k], u, vi[k] * Vi[k] + vj[k] * Vj[k] + reg * Uu[k])
+        np.add.at(GV[k], i, vi[k] * Uu[k] + reg * Vi[k])
+        np.add.at(GV[k], j, vj[k] * Uu[k] + reg * Vj[k])
+    GH = (np.einsum("kb,kbd->kd", dei, Uu * Vi) + np.einsum("kb,kbd->kd", dej, Uu * Vj)
+          + reg * H)
+    lr = dt(lr)
+    for X, A, G in ((U, AU, GU), (V, AV, GV), (H, AH, GH)):
+        A += G * G
+        X -= lr * G / np.sqrt(A)
+    return loss
+
+
+def ens_predict(U, V, H, users):
+    """ensemble.py:116-140: sum_k s_k exp(e_k) / sum_k exp(e_k) over all items."""
+    Uu = U[:, np.asarray(users)]                     # [K, n, d]
+    S = np.einsum("knd,kmd->knm", Uu, V)
+    E = np.exp(np.einsum("knd,kmd->knm", Uu * H[:, None, :], V))
+    return np.sum(S * E, axis=0) / np.sum(E, axis=0)
+
+
 # ----------------------------------------------------------------------------
 # scoring / recommend  (bprmf.py:77-103 and siblings)
 # ----------------------------------------------------------------------------

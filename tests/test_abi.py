@@ -89,3 +89,15 @@ def test_synth_graph_deterministic_and_shardable():
     # Zipf popularity: the most popular items dominate
     cnt = np.bincount(ix, minlength=500)
     assert cnt.max() > 10 * np.median(cnt)
+
+
+def test_ensemble_no_cpu_fallback_and_einval():
+    L = N.lib()
+    h = ctypes.c_void_p()
+    assert L.cf_ens_create(10, 10, 9, 4, 0.1, 0.1, 0.1, 0, ctypes.byref(h)) == -1   # K > 8
+    assert b"K 1..8" in L.cf_last_error()
+    if N.device_count() > 0:
+        return
+    from collaborativefilteringusingtensorflow_amd.ensemble import EnsembleEngine
+    with pytest.raises(N.NativeError, match="no HIP device"):
+        EnsembleEngine(10, 10, 3, 4)

@@ -1,0 +1,126 @@
+"""Ensemble (src/models/pl/models/ensemble.py) on the native ensemble object
+(csrc/cf_ensemble.hip) against the float64 oracle (oracle/cf_oracle.py
+ens_step / ens_predict, pinned to autograd of the literal TF graph -- with its
+[B] x [B, 1] broadcast -- in tests/test_oracle.py).
+
+Tolerance: 1e-4 relative on the loss and on U, V, H and their accumulators
+after several steps (fp32 device arithmetic, float atomics in any order,
+against float64), batches from the reference's own sampler_uij_ranking
+stream (tests/golden/sampler_streams.npz "uij_b100") and synthetic batches
+with ragged B, hot rows and repeated items."""
+import numpy as np
+import pytest
+
+from conftest import get_stream
+from oracle import cf_oracle as O
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def rel(a, b):
+    return float(np.max(np.abs(np.asarray(a, np.float64) - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def make(K, nu, ni, d, reg, seed=5):
+    from collaborativefilteringusingtensorflow_amd.ensemble import EnsembleEngine
+    rng = np.random.RandomState(seed)
+    U = O.init_table(rng, (K, nu, d))
+    V = O.init_table(rng, (K, ni, d))
+    H = O.init_table(rng, (K, d))
+    e = EnsembleEngine(nu, ni, K, d, reg=reg)
+    e.set_table("user", U)
+    e.set_table("item", V)
+    e.set_table("h", H)
+    return e, U.astype(np.float64), V.astype(np.float64), H.astype(np.float64)
+
+
+def check_tables(e, U, V, H, AU, AV, AH):
+    for name, o in (("user", U), ("item", V), ("h", H), ("acc_user", AU), ("acc_item", AV),
+                    ("acc_h", AH)):
+        r = rel(e.get_table(name), o)
+        assert r <= RTOL, (name, r)
+
+
+@pytest.mark.parametrize("K,d,reg", [(3, 100, 0.01), (2, 20, 0.1), (1, 16, 0.05)])
+def test_ensemble_reference_stream_matches_oracle(streams, fold1, K, d, reg):
+    st = get_stream(streams, "uij_b100")
+    e, U, V, H = make(K, 943, 1682, d, reg)
+    AU, AV, AH = (np.full_like(x, 0.1) for x in (U, V, H))
+    for s in range(10):
+        uij = np.concatenate([st["pairs"][s], st["negs"][s]], 1)
+        lg = e.step(uij)
+        lo = O.ens_step(U, V, H, AU, AV, AH, uij, reg)
+        assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
+    check_tables(e, U, V, H, AU, AV, AH)
+    e.close()
+
+
+@pytest.mark.parametrize("K,B,d", [(8, 257, 33), (3, 64, 100), (4, 1, 8), (2, 130, 256)])
+def test_ensemble_ragged_hot_rows(K, B, d):
+    rng = np.random.RandomState(K * 100 + B)
+    nu, ni = 50, 80                     # small tables: many duplicates per batch
+    e, U, V, H = make(K, nu, ni, d, 0.02, seed=B)
+    AU, AV, AH = (np.full_like(x, 0.1) for x in (U, V, H))
+    for s in range(6):
+        uij = np.stack([rng.randint(0, nu, B), rng.randint(0, ni, B), rng.randint(0, ni, B)], 1)
+        uij[: B // 3, 0] = 3            # a hot user
+        uij[B // 2:, 2] = uij[B // 2:, 1]   # i == j rows
+        lg = e.step(uij)
+        lo = O.ens_step(U, V, H, AU, AV, AH, uij, 0.02)
+        assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
+    check_tables(e, U, V, H, AU, AV, AH)
+    e.close()
+
+
+def test_ensemble_take_loss_and_recommend(fold1):
+    e, U, V, H = make(3, 943, 1682, 20, 0.01)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    rng = np.random.RandomState(1)
+    AU, AV, AH = (np.full_like(x, 0.1) for x in (U, V, H))
+    tot = 0.0
+    for s in range(5):
+        uij = np.stack([rng.randint(0, 943, 100), rng.randint(0, 1682, 100),
+                        rng.randint(0, 1682, 100)], 1)
+        e.step(uij, return_loss=False)
+        tot += O.ens_step(U, V, H, AU, AV, AH, uij, 0.01)
+    assert abs(e.take_loss() - tot) <= RTOL * tot
+    assert e.take_loss() == 0.0
+    users = np.arange(0, 943, 5, dtype=np.int32)
+    idx, val = e.score_topk(users, 10, return_values=True)
+    S = O.ens_predict(U, V, H, users)
+    ref = O.recommend(S, fold1["train_indptr"], fold1["train_indices"], users, 10)
+    assert sum(1 for a, c in zip(idx.tolist(), ref) if a != c) <= 2
+    got = np.take_along_axis(S, idx.astype(np.int64), 1)
+    np.testing.assert_allclose(val, got, rtol=1e-4, atol=1e-6)
+    e.close()
+
+
+def test_ensemble_rejects_bad_ids():
+    from collaborativefilteringusingtensorflow_amd import _native as N
+    e, *_ = make(2, 10, 20, 8, 0.1)
+    with pytest.raises(N.NativeError, match="out of range"):
+        e.step(np.array([[0, 1, 20]]))
+    with pytest.raises(N.NativeError, match="exclude_train"):
+        e.score_topk(np.array([0]), 5, exclude_train=True)
+    e.close()
+
+
+def test_ensemble_train_loop(fold1):
+    """Ensemble.train on ml-100k fold 1 with the exact reference stream:
+    losses fall and the top-10 precision beats random by a wide margin."""
+    import scipy.sparse as sp
+    from collaborativefilteringusingtensorflow_amd.ensemble import Ensemble
+    from collaborativefilteringusingtensorflow_amd.sampler_uij_ranking import ExactSampler
+    f = fold1
+    tra = sp.csr_matrix((np.ones(len(f["train_indices"])), f["train_indices"], f["train_indptr"]),
+                        shape=(943, 1682))
+    tst = sp.csr_matrix((np.ones(len(f["test_indices"])), f["test_indices"], f["test_indptr"]),
+                        shape=(943, 1682))
+    sampler = ExactSampler(tra, batch_size=100, seed=0)
+    en = Ensemble(943, 1682, 3, 10, 'cv', ['pre', 'recall', 'map', 'mrr', 'ndcg'], 0.01, 20, 100,
+                  max_iter=3, device=0, seed=3, verbose=True)
+    scores = en.train(1, tra, tst, sampler)
+    assert np.all(np.isfinite(scores))
+    assert scores[0] > 0.05, scores
+    en.close()

@@ -314,3 +314,67 @@ def test_plr_oracle_matches_literal_autograd(kind, width, hp):
         for k in tabs:
             assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
             assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
+
+
+def literal_ens_loss(U, V, H, uij, reg):
+    """Torch transcription of ensemble.py:58-114, keeping the reference's
+    shapes: ``reduce_sum(ui, -1)`` is [B] and ``exp(matmul(ui, h))`` is [B, 1],
+    so their product -- and the loss -- is [B, B]."""
+    t = torch.as_tensor(uij, dtype=torch.long)
+    l2 = lambda x: 0.5 * (x * x).sum()
+    K = U.shape[0]
+    reg_loss = 0
+    for k in range(K):                                           # ensemble.py:58-69
+        reg_loss = reg_loss + l2(U[k][t[:, 0]]) + l2(V[k][t[:, 1:]])
+    reg_loss = reg * (reg_loss + l2(H))
+    parts, ai_base, aj_base = [], 0, 0
+    for k in range(K):                                           # ensemble.py:71-93
+        u, i, j = U[k][t[:, 0]], V[k][t[:, 1]], V[k][t[:, 2]]
+        ui, uj = u * i, u * j
+        ui_a = torch.exp(ui @ H[k][:, None])                    # [B, 1]
+        uj_a = torch.exp(uj @ H[k][:, None])
+        parts.append((ui.sum(-1) * ui_a, uj.sum(-1) * uj_a))     # [B] * [B, 1] -> [B, B]
+        ai_base, aj_base = ai_base + ui_a, aj_base + uj_a
+    ui_r = sum(p[0] / ai_base for p in parts)
+    uj_r = sum(p[1] / aj_base for p in parts)
+    return (-torch.log(torch.sigmoid(ui_r - uj_r))).sum() + reg_loss
+
+
+@pytest.mark.parametrize("K,B,reg", [(3, 100, 0.01), (2, 57, 0.1), (1, 64, 0.05)])
+def test_ensemble_oracle_matches_literal_autograd(K, B, reg):
+    rng = np.random.RandomState(11 + K)
+    nu, ni, d = 60, 90, 8          # small tables: plenty of duplicate rows in a batch
+    tabs = {"U": O.init_table(rng, (K, nu, d), dtype=np.float64),
+            "V": O.init_table(rng, (K, ni, d), dtype=np.float64),
+            "H": O.init_table(rng, (K, d), dtype=np.float64)}
+    ora = {k: v.copy() for k, v in tabs.items()}
+    oacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    tacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    for s in range(4):
+        uij = np.stack([rng.randint(0, nu, B), rng.randint(0, ni, B), rng.randint(0, ni, B)], 1)
+        T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tabs.items()}
+        loss = literal_ens_loss(T["U"], T["V"], T["H"], uij, reg)
+        loss.backward()
+        for k, tt in T.items():                                  # dense ApplyAdagrad
+            g = tt.grad.numpy()
+            tacc[k] = tacc[k] + g * g
+            tabs[k] = tt.detach().numpy() - 0.1 * g / np.sqrt(tacc[k])
+        lo = O.ens_step(ora["U"], ora["V"], ora["H"], oacc["U"], oacc["V"], oacc["H"], uij, reg)
+        assert abs(lo - float(loss.detach())) <= TOL * abs(float(loss.detach()))
+        for k in tabs:
+            assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
+            assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
+
+
+def test_ensemble_predict_literal():
+    rng = np.random.RandomState(3)
+    K, nu, ni, d = 3, 20, 30, 6
+    U, V, H = (O.init_table(rng, s, dtype=np.float64) for s in ((K, nu, d), (K, ni, d), (K, d)))
+    users = np.array([0, 5, 19])
+    Ut, Vt, Ht = (torch.tensor(x) for x in (U, V, H))
+    num, base = 0, 0
+    for k in range(K):                                           # ensemble.py:116-140
+        ui = Ut[k][users][:, None, :] * Vt[k][None]
+        s, a = ui.sum(-1), torch.exp((ui * Ht[k][None]).sum(-1))
+        num, base = num + s * a, base + a
+    np.testing.assert_allclose(O.ens_predict(U, V, H, users), (num / base).numpy(), rtol=1e-12)
