@@ -101,32 +101,63 @@ def load_pmc(workload, n_gpus):
         return None
 
 
-def cpu_baseline(cfg, indptr, indices, budget_s=15.0):
-    """The C oracle (oracle/cf_oracle.c, single thread): the same sample +
-    step work unit on the same graph, timed on this host on a bounded sample."""
+def cpu_threads():
+    """Host threads for the all-cores CPU baseline: OMP_NUM_THREADS when set
+    (the GPU box sets it to the job's CPU share), else every visible CPU."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return n if n > 0 else (os.cpu_count() or 1)
+
+
+def cpu_baseline(cfg, indptr, indices, budget_s=12.0):
+    """The C oracle (oracle/cf_oracle.c): the same sample + step work unit on
+    the same graph, timed on this host on a bounded sample -- on all cores
+    (oracle_train_mt, BPR / AMF) and on one core (oracle_train)."""
     from oracle.build_oracle import COracle
     from oracle import cf_oracle as O
     rng = np.random.RandomState(1)
     U = O.init_table(rng, (cfg["n_users"], cfg["d"]))
     V = O.init_table(rng, (cfg["n_items"], cfg["d"]))
-    c = COracle(cfg["model"], U, V, W=cfg["W"], reg=cfg["reg"], margin=cfg.get("margin", 1.0),
-                reg_cov=cfg.get("reg_cov", 1.0), clip_norm=cfg.get("clip_norm", 1.0),
-                reg_adv=cfg.get("reg_adv", 1.0), max_batch=cfg["B"])
+
+    def make():
+        return COracle(cfg["model"], U, V, W=cfg["W"], reg=cfg["reg"],
+                       margin=cfg.get("margin", 1.0), reg_cov=cfg.get("reg_cov", 1.0),
+                       clip_norm=cfg.get("clip_norm", 1.0), reg_adv=cfg.get("reg_adv", 1.0),
+                       max_batch=cfg["B"])
     users = np.repeat(np.arange(len(indptr) - 1, dtype=np.int32), np.diff(indptr))
     coo = np.stack([users, indices], axis=1)
     del users
     B = cfg["B"]
-    t0 = time.perf_counter()
-    c.train(indptr, indices, coo, B, 1, 12345)
-    one = time.perf_counter() - t0
-    n = max(1, int(budget_s / max(one, 1e-3)))
-    t0 = time.perf_counter()
-    c.train(indptr, indices, coo, B, n, 6789)
-    dt = time.perf_counter() - t0
-    trip = n * B * cfg["W"]
-    return {"value": trip / dt, "unit": "triplets/s", "cores": 1, "kind": "port",
+
+    def timed(run):
+        t0 = time.perf_counter()
+        run(1, 12345)
+        one = time.perf_counter() - t0
+        n = max(1, int(budget_s / max(one, 1e-3)))
+        t0 = time.perf_counter()
+        run(n, 6789)
+        return n, time.perf_counter() - t0
+
+    c1 = make()
+    n1, dt1 = timed(lambda n, seed: c1.train(indptr, indices, coo, B, n, seed))
+    del c1
+    single = {"value": n1 * B * cfg["W"] / dt1, "cores": 1,
+              "sample": "%d steps, oracle_train, %.1f s" % (n1, dt1)}
+    T = cpu_threads()
+    if cfg["model"] in ("bpr", "amf") and T > 1:
+        cm = make()
+        nm, dtm = timed(lambda n, seed: cm.train_mt(indptr, indices, coo, B, n, seed, T))
+        del cm
+        return {"value": nm * B * cfg["W"] / dtm, "unit": "triplets/s", "cores": T, "kind": "port",
+                "sample": "%d steps x %d pairs (W=%d) of %s: sample+forward+backward+dedup+Adagrad, "
+                          "oracle/cf_oracle.c oracle_train_mt on %d threads, %.1f s"
+                          % (nm, B, cfg["W"], cfg["desc"], T, dtm),
+                "single_thread": single}
+    return {"value": single["value"], "unit": "triplets/s", "cores": 1, "kind": "port",
             "sample": "%d steps x %d pairs (W=%d) of %s: sample+forward+backward+dedup+Adagrad, "
-                      "oracle/cf_oracle.c single thread, %.1f s" % (n, B, cfg["W"], cfg["desc"], dt)}
+                      "oracle/cf_oracle.c single thread, %.1f s" % (n1, B, cfg["W"], cfg["desc"], dt1)}
 
 
 def main():

@@ -20,8 +20,8 @@ LIB = os.path.join(HERE, "build", "libcf_oracle.so")
 def build(verbose=True):
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-        subprocess.run(["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-o", LIB, SRC, "-lm"],
-                       check=True)
+        subprocess.run(["gcc", "-O2", "-std=c11", "-fopenmp", "-fPIC", "-shared", "-o", LIB, SRC,
+                        "-lm"], check=True)
     if verbose:
         print("built", LIB)
     return LIB
@@ -55,6 +55,10 @@ class COracle(object):
         self.L = ctypes.CDLL(build(verbose=False))
         self.L.oracle_step.restype = ctypes.c_double
         self.L.oracle_step.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int]
+        self.L.oracle_train_mt.restype = ctypes.c_double
+        self.L.oracle_train_mt.argtypes = ([ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int])
         self.L.oracle_train.restype = ctypes.c_double
         self.L.oracle_train.argtypes = ([ctypes.c_void_p] * 5 + [ctypes.c_int64, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p,
@@ -105,6 +109,20 @@ class COracle(object):
         return self.L.oracle_train(ctypes.byref(self.cfg), ctypes.byref(self.st), _p(indptr),
                                    _p(indices), _p(pairs_coo), indices.shape[0], B,
                                    n_steps, seed & 0xFFFFFFFFFFFFFFFF, _p(bp), _p(bn))
+
+    def train_mt(self, indptr, indices, pairs_coo, B, n_steps, seed, n_threads):
+        """oracle_train's work unit on n_threads cores (BPR / AMF only)."""
+        indptr = np.ascontiguousarray(indptr, np.int64)
+        indices = np.ascontiguousarray(indices, np.int32)
+        pairs_coo = np.ascontiguousarray(pairs_coo, np.int32)
+        bp = np.zeros((B, 2), np.int32)
+        bn = np.zeros((B, self.cfg.W), np.int32)
+        r = self.L.oracle_train_mt(ctypes.byref(self.cfg), ctypes.byref(self.st), _p(indptr),
+                                   _p(indices), _p(pairs_coo), indices.shape[0], B, n_steps,
+                                   seed & 0xFFFFFFFFFFFFFFFF, _p(bp), _p(bn), int(n_threads))
+        if r < 0:
+            raise ValueError("oracle_train_mt covers BPR / AMF only")
+        return r
 
 
 if __name__ == "__main__":

@@ -378,3 +378,21 @@ def test_ensemble_predict_literal():
         s, a = ui.sum(-1), torch.exp((ui * Ht[k][None]).sum(-1))
         num, base = num + s * a, base + a
     np.testing.assert_allclose(O.ens_predict(U, V, H, users), (num / base).numpy(), rtol=1e-12)
+
+
+@pytest.mark.parametrize("model,W,threads", [("bpr", 1, 4), ("bpr", 5, 3), ("amf", 5, 8)])
+def test_c_oracle_multithread_matches_single(fold1, model, W, threads):
+    """oracle_train_mt (the all-cores CPU baseline) draws the same batches and
+    applies the same dedup-sum Adagrad as oracle_train, row-partitioned."""
+    from oracle.build_oracle import COracle
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    users = np.repeat(np.arange(len(ip) - 1, dtype=np.int32), np.diff(ip))
+    coo = np.stack([users, ix], 1)
+    tabs = init(3, d=24)
+    a = COracle(model, tabs["U"], tabs["V"], W=W, reg=0.05)
+    b = COracle(model, tabs["U"], tabs["V"], W=W, reg=0.05)
+    la = a.train(ip, ix, coo, 300, 40, 99)
+    lb = b.train_mt(ip, ix, coo, 300, 40, 99, threads)
+    assert abs(la - lb) <= 1e-5 * abs(la)
+    for x, y in ((a.U, b.U), (a.V, b.V), (a.AU, b.AU), (a.AV, b.AV)):
+        assert rel(y, x.astype(np.float64)) < 1e-5
