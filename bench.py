@@ -172,7 +172,7 @@ def main():
     ap.add_argument("--score-pass", action="store_true",
                     help="also time one full scoring + top-10 pass over this rank's users")
     ap.add_argument("--grad-path", type=int, default=0,
-                    help="cf_set_option grad_path: 0 auto (phased kernel), 1 generic kernel")
+                    help="cf_set_option grad_path: 0 auto, 1 generic kernel, 2 phased kernel when eligible")
     ap.add_argument("--prep-stream", type=int, default=0,
                     help="cf_set_option prep_stream: 0 in-order (default), 1 side stream")
     ap.add_argument("--pipeline", type=int, default=1,

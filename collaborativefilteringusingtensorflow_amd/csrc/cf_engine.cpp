@@ -1418,7 +1418,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "grad_path") {
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "grad_path must be 0 or 1");
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "grad_path must be 0, 1 or 2");
         e->grad_path = (int)value;
         return CF_OK;
     }

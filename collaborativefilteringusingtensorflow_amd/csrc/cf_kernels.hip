@@ -1479,7 +1479,11 @@ static int epl_for(int d) {
 // which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
 // fast, 0 = generic
 static int fast_w(const StepArgs& a) {
-    const bool ok = a.grad_path != 1 && epl_for(a.d) <= 8 && (a.model != GBPR || a.G == 1);
+    // CML at W = 5 keeps five distance rows and the clip live per pair: the
+    // generic kernel measured faster there (cfg3: 160 vs 184 us), so auto
+    // (grad_path 0) leaves it on the generic kernel; 2 forces the fast path
+    const bool ok = a.grad_path != 1 && epl_for(a.d) <= 8 && (a.model != GBPR || a.G == 1) &&
+                    !(a.grad_path == 0 && a.model == CML && a.W == 5);
     return ok && (a.W == 1 || a.W == 5) ? a.W : 0;
 }
 

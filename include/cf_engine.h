@@ -298,8 +298,9 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
  *   "grad_path"  0 = auto (phased gradient kernel for W in {1,5}, d <= 128,
- *                GBPR group size 1; generic kernel otherwise), 1 = generic
- *                kernel always.  Both give the same arithmetic.
+ *                GBPR group size 1, except CML at W = 5; generic kernel
+ *                otherwise), 1 = generic kernel always, 2 = phased kernel
+ *                whenever eligible.  All give the same arithmetic.
  *   "prep_stream" 0 = everything in order on the engine stream (default);
  *                1 = sample/count on a side stream, overlapping the previous
  *                step's gradient.  Same results.

@@ -20,7 +20,7 @@ _GRAD_PATH = [0]
 _OPTS = {}   # extra cf_set_option values for make_engine
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["phased", "generic"])
+@pytest.fixture(autouse=True, params=[2, 1], ids=["phased", "generic"])
 def grad_path(request):
     """Every step test runs on both gradient kernels (cf_set_option grad_path):
     the phased W in {1,5} kernel and the generic one."""
