@@ -136,11 +136,33 @@ def header_symbols(path=HEADER_PATH):
     return sorted(set(re.findall(r"\b(cf_[a-z_0-9]+)\s*\(", text)))
 
 
+def _preload_torch_hip():
+    """One HIP runtime per process.  PyTorch ships its own libamdhip64 /
+    libhsa-runtime64 (same sonames as /opt/rocm's); if this library loaded
+    /opt/rocm's first, a later ``torch.cuda`` init would start a second
+    runtime and find no device.  Loading torch's copies first (RTLD_GLOBAL,
+    without importing torch) makes the engine bind to them, so engine and
+    torch share one runtime in either import order.  CF_HIP_RUNTIME=system
+    keeps /opt/rocm's."""
+    if os.environ.get("CF_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    d = os.path.join(os.path.dirname(spec.origin), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(d, name)
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib():
     """Load libcf_engine.so once; raise NativeError if it is not built."""
     global _lib
     if _lib is not None:
         return _lib
+    _preload_torch_hip()
     if not os.path.exists(LIB_PATH):
         raise NativeError(
             "libcf_engine.so not found at %s -- build it with "

@@ -107,6 +107,9 @@ struct cf_engine {
     double* h_loss = nullptr; // pinned
     int32_t* h_stage = nullptr;
     size_t stage_cap = 0;
+    int tuple_stride = 0;            // cf_step_plr: ids read from tuples [B, width]
+    int32_t* d_bad = nullptr;        // device-batch range check (pack kernel)
+    int32_t* h_bad = nullptr;        // pinned
     hipEvent_t stage_ev = nullptr;
 
     // device sampler position
@@ -321,12 +324,65 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
     return CF_OK;
 }
 
+static bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable host memory: not an error for us
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice;
+}
+
+// A batch in device memory: de-interleave and range-check on the device,
+// then read the check back (one sync; the host path checks on the host).
+static int stage_device_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
+                       const int32_t* groups, int B, int k, hipStream_t st) {
+    const cf_config& c = e->cfg;
+    const int W = c.n_neg, G = group_count(c);
+    if (!is_device_ptr(negs) || (G > 0 && !is_device_ptr(groups)))
+        return fail(CF_EINVAL, "a batch must be all host or all device memory");
+    if (!e->d_bad) {
+        CF_TRY(dalloc(&e->d_bad, 1));
+        CF_HIP(hipHostMalloc((void**)&e->h_bad, sizeof(int32_t), hipHostMallocDefault));
+    }
+    PackArgs a{};
+    a.u = pairs;
+    a.us = e->tuple_stride ? e->tuple_stride : 2;
+    a.j = negs;
+    a.js = e->tuple_stride ? e->tuple_stride : W;
+    a.g = groups;
+    a.gs = G;
+    a.B = B; a.W = W; a.G = G;
+    a.n_users = c.n_users;
+    a.n_items = c.n_items;
+    a.sharded = e->world > 1 ? 1 : 0;
+    a.shard_u0 = e->shard_u0;
+    a.shard_u1 = e->shard_u1;
+    a.total_users = e->world > 1 ? e->h_bounds[e->world] : c.n_users;
+    a.occU = e->occU_[k];
+    a.occV = e->occV_[k];
+    a.bad = e->d_bad;
+    CF_HIP(hipMemsetAsync(e->d_bad, 0x7F, sizeof(int32_t), st));
+    CF_HIP(launch_pack_batch(a, st));
+    CF_HIP(hipMemcpyAsync(e->h_bad, e->d_bad, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    CF_HIP(hipStreamSynchronize(st));
+    if (*e->h_bad != kPackOk)
+        return fail(CF_EINVAL, "device batch row " + std::to_string(*e->h_bad) + " has an id out of range");
+    return CF_OK;
+}
+
 int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
                      const int32_t* groups, int B, int k, hipStream_t st) {
     const cf_config& c = e->cfg;
     const int W = c.n_neg, G = group_count(c);
     if (!pairs || !negs) return fail(CF_EINVAL, "pairs and negs are required");
     if (G > 0 && !groups) return fail(CF_EINVAL, "GBPR needs groups");
+    if (is_device_ptr(pairs)) return stage_device_batch(e, pairs, negs, groups, B, k, st);
+    if (is_device_ptr(negs) || (G > 0 && is_device_ptr(groups)))
+        return fail(CF_EINVAL, "a batch must be all host or all device memory");
+    const size_t us = e->tuple_stride ? (size_t)e->tuple_stride : 2;
+    const size_t js = e->tuple_stride ? (size_t)e->tuple_stride : (size_t)W;
     const size_t nU = (size_t)B * (1 + G), nV = (size_t)B * (1 + W);
     const size_t need = nU + nV;
     if (need > e->stage_cap) {
@@ -344,13 +400,13 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
     int32_t* sv = e->h_stage + nU;
     const int64_t nu = c.n_users, ni = c.n_items;
     for (int p = 0; p < B; ++p) {
-        const int32_t u = pairs[2 * p], i = pairs[2 * p + 1];
+        const int32_t u = pairs[us * p], i = pairs[us * p + 1];
         if (u < 0 || u >= nu || i < 0 || i >= ni)
             return fail(CF_EINVAL, "pair " + std::to_string(p) + " out of range");
         su[p] = u;
         sv[p] = i;
         for (int w = 0; w < W; ++w) {
-            const int32_t j = negs[(size_t)p * W + w];
+            const int32_t j = negs[js * p + w];
             if (j < 0 || j >= ni) return fail(CF_EINVAL, "negative item out of range");
             sv[B + (size_t)p * W + w] = j;
         }
@@ -615,9 +671,9 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
         he = launch_fused_topk(f, e->stream);
     }
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDefault);
     if (he == hipSuccess && val_out)
-        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDefault);
     dfree(d_users); dfree(d_idx); dfree(d_val);
     if (he != hipSuccess) return fail(CF_EHIP, std::string("cf_score_topk (fused): ") + hipGetErrorString(he));
     return CF_OK;
@@ -773,6 +829,8 @@ int cf_destroy(cf_engine* e) {
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_bad) (void)hipHostFree(e->h_bad);
+    dfree(e->d_bad);
     if (e->stage_ev) (void)hipEventDestroy(e->stage_ev);
     if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
     if (e->side) (void)hipStreamDestroy(e->side);
@@ -875,7 +933,7 @@ int cf_set_table(cf_engine* e, int32_t t, const float* src, int64_t n) {
     float* p = table_ptr(e, t, &want);
     if (!p) return fail(CF_EINVAL, "table not present in this model");
     if (n != want || !src) return fail(CF_EINVAL, "table size mismatch: want " + std::to_string(want));
-    CF_HIP(hipMemcpyAsync(p, src, (size_t)n * 4, hipMemcpyHostToDevice, e->stream));
+    CF_HIP(hipMemcpyAsync(p, src, (size_t)n * 4, hipMemcpyDefault, e->stream));
     CF_HIP(hipStreamSynchronize(e->stream));
     if (e->cfg.model == CF_CML) {
         if (t == CF_TABLE_USER) e->need_clip_U = true;
@@ -892,7 +950,7 @@ int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
     if (!p) return fail(CF_EINVAL, "table not present in this model");
     if (n != want || !dst) return fail(CF_EINVAL, "table size mismatch: want " + std::to_string(want));
     CF_HIP(hipStreamSynchronize(e->stream));
-    CF_HIP(hipMemcpy(dst, p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    CF_HIP(hipMemcpy(dst, p, (size_t)n * 4, hipMemcpyDefault));
     return CF_OK;
 }
 
@@ -922,13 +980,6 @@ int cf_step_plr(cf_engine* e, const int32_t* tuples, int32_t width, const float*
     if (B < 1 || !tuples) return fail(CF_EINVAL, "bad arguments");
     if (width != c.n_neg + 2) return fail(CF_EINVAL, "tuple width must be n_neg + 2");
     if (c.plr_kind == CF_PLR_CPLR && !coefs) return fail(CF_EINVAL, "CPLR needs coefs [B, 2]");
-    const int W = c.n_neg;
-    std::vector<int32_t> pairs((size_t)B * 2), negs((size_t)B * W);
-    for (int p = 0; p < B; ++p) {
-        pairs[2 * p] = tuples[(size_t)p * width];
-        pairs[2 * p + 1] = tuples[(size_t)p * width + 1];
-        for (int w = 0; w < W; ++w) negs[(size_t)p * W + w] = tuples[(size_t)p * width + 2 + w];
-    }
     if (c.plr_kind == CF_PLR_CPLR) {
         CF_HIP(hipStreamSynchronize(e->stream));  // the previous step may still read the buffer
         if (B > e->coefs_cap) {
@@ -936,10 +987,14 @@ int cf_step_plr(cf_engine* e, const int32_t* tuples, int32_t width, const float*
             CF_TRY(dalloc(&e->coefs, (size_t)B * 2));
             e->coefs_cap = B;
         }
-        CF_HIP(hipMemcpy(e->coefs, coefs, (size_t)B * 2 * sizeof(float), hipMemcpyHostToDevice));
+        CF_HIP(hipMemcpy(e->coefs, coefs, (size_t)B * 2 * sizeof(float), hipMemcpyDefault));
     }
     double* acc = loss_out ? e->loss + 1 : e->loss;
-    CF_TRY(run_step(e, B, pairs.data(), negs.data(), nullptr, acc));
+    // ids straight from the tuples: u, i at columns 0, 1; the rest as negatives
+    e->tuple_stride = width;
+    const int r = run_step(e, B, tuples, tuples + 2, nullptr, acc);
+    e->tuple_stride = 0;
+    CF_TRY(r);
     if (loss_out) CF_TRY(read_loss(e, 1, loss_out));
     return CF_OK;
 }
@@ -1319,6 +1374,12 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     if (k < 1 || k > 4096) return fail(CF_EINVAL, "k must be 1..4096");
     if (exclude_train && !e->indptr) return fail(CF_ESTATE, "exclude_train needs cf_set_interactions");
     if (n == 0) return CF_OK;
+    std::vector<int32_t> host_users;
+    if (is_device_ptr(users)) {  // device ids (torch): checked from a host copy
+        host_users.resize((size_t)n);
+        CF_HIP(hipMemcpy(host_users.data(), users, (size_t)n * 4, hipMemcpyDeviceToHost));
+        users = host_users.data();
+    }
     for (int r = 0; r < n; ++r)
         if (users[r] < 0 || users[r] >= c.n_users) return fail(CF_EINVAL, "user id out of range");
     CF_HIP(hipStreamSynchronize(e->side));
@@ -1377,9 +1438,9 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
         }
     }
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+    if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDefault);
     if (he == hipSuccess && val_out)
-        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDeviceToHost);
+        he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDefault);
     dfree(d_users); dfree(d_idx); dfree(d_val);
     if (he != hipSuccess) return fail(CF_EHIP, std::string("cf_score_topk: ") + hipGetErrorString(he));
     return CF_OK;

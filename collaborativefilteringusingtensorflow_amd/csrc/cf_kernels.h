@@ -214,6 +214,24 @@ hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int
 hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s);
 // zero the counts of a batch's occurrences (a drawn-ahead batch is dropped)
 hipError_t launch_uncount(const int32_t* occ, int64_t n, int32_t* cnt, hipStream_t s);
+
+// A caller batch already in device memory (torch tensors): user / item /
+// negative / group ids read with row strides (cf_step: pairs [B,2], negs
+// [B,W], groups [B,G]; cf_step_plr: tuples [B,width]) into the occurrence
+// arrays, range-checked on the device; *bad = the first offending row
+// (initialised to kPackOk by the caller).  Out-of-range ids are stored as 0.
+constexpr int32_t kPackOk = 0x7F7F7F7F;
+struct PackArgs {
+    const int32_t* u; int us;        // u = u[p*us], i = u[p*us + 1]
+    const int32_t* j; int js;        // negative w = j[p*js + w]
+    const int32_t* g; int gs;        // group k = g[p*gs + k]
+    int B, W, G;
+    int64_t n_users, n_items;
+    int sharded;                     // group ids are global: own -> local, else -1 - id
+    int64_t shard_u0, shard_u1, total_users;
+    int32_t* occU; int32_t* occV; int32_t* bad;
+};
+hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
                               int4* pairs, hipStream_t s);
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);

@@ -1726,6 +1726,44 @@ hipError_t launch_uncount(const int32_t* occ, int64_t n, int32_t* cnt, hipStream
     return hipGetLastError();
 }
 
+__global__ void pack_batch_kernel(PackArgs a) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= a.B) return;
+    bool ok = true;
+    const int32_t u = a.u[(int64_t)p * a.us], i = a.u[(int64_t)p * a.us + 1];
+    const bool uok = u >= 0 && u < a.n_users, iok = i >= 0 && i < a.n_items;
+    ok = uok && iok;
+    a.occU[p] = uok ? u : 0;
+    a.occV[p] = iok ? i : 0;
+    for (int w = 0; w < a.W; ++w) {
+        const int32_t j = a.j[(int64_t)p * a.js + w];
+        const bool jok = j >= 0 && j < a.n_items;
+        ok = ok && jok;
+        a.occV[a.B + (int64_t)p * a.W + w] = jok ? j : 0;
+    }
+    for (int k = 0; k < a.G; ++k) {
+        const int32_t g = a.g[(int64_t)p * a.gs + k];
+        int32_t v;
+        if (a.sharded) {
+            const bool gok = g >= 0 && g < a.total_users;
+            ok = ok && gok;
+            v = !gok ? 0 : (g >= a.shard_u0 && g < a.shard_u1) ? (int32_t)(g - a.shard_u0) : -1 - g;
+        } else {
+            const bool gok = g >= 0 && g < a.n_users;
+            ok = ok && gok;
+            v = gok ? g : 0;
+        }
+        a.occU[a.B + (int64_t)p * a.G + k] = v;
+    }
+    if (!ok) atomicMin(a.bad, p);
+}
+
+hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_batch_kernel, dim3((a.B + kBlock - 1) / kBlock), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
 uint64_t mix64_host(uint64_t z) { return mix64(z); }
 
 PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch) {

@@ -20,6 +20,31 @@ def _i32(a):
     return np.ascontiguousarray(a, dtype=np.int32)
 
 
+def _is_dev(x):
+    """A torch tensor in HIP device memory (the C ABI takes its pointer as is)."""
+    return hasattr(x, "data_ptr") and bool(getattr(x, "is_cuda", False))
+
+
+def _dev(t, dtype, ctype):
+    """Contiguous device tensor of ``dtype`` and its pointer; torch's stream is
+    synchronised first, because the engine reads it on its own stream."""
+    import torch
+    t = t.to(dtype).contiguous()
+    torch.cuda.current_stream(t.device).synchronize()
+    return t, ctypes.cast(t.data_ptr(), ctypes.POINTER(ctype))
+
+
+class _DevArg(object):
+    """A device tensor plus its ctypes pointer (keeps the tensor alive)."""
+
+    def __init__(self, t, p):
+        self.t, self.p = t, p
+
+
+def _arg(x, ctype):
+    return x.p if isinstance(x, _DevArg) else _ptr(x, ctype)
+
+
 class Engine(object):
     def __init__(self, model, n_users, n_items, n_factors, n_neg=1, gsize=1, lr=0.1,
                  reg=0.02, rho=0.5, margin=1.5, reg_cov=1.0, clip_norm=1.0, reg_adv=1.0,
@@ -123,6 +148,19 @@ class Engine(object):
 
     # ---- training -------------------------------------------------------------
     def _batch(self, pairs, negs, groups):
+        if _is_dev(pairs):   # torch device tensors: staged on the device (cf_step docs)
+            import torch
+            pairs, pp = _dev(pairs.reshape(-1, 2), torch.int32, ctypes.c_int32)
+            B = pairs.shape[0]
+            negs, npt = _dev(negs.reshape(B, -1), torch.int32, ctypes.c_int32)
+            if negs.shape[1] != self.n_neg:
+                raise ValueError("negs must have %d columns" % self.n_neg)
+            gp = None
+            if self.model == N.CF_GBPR:
+                groups, gp = _dev(groups.reshape(B, -1), torch.int32, ctypes.c_int32)
+                if groups.shape[1] != self.gsize:
+                    raise ValueError("groups must have %d columns" % self.gsize)
+            return B, _DevArg(pairs, pp), _DevArg(negs, npt), gp, groups
         pairs = _i32(pairs).reshape(-1, 2)
         B = pairs.shape[0]
         negs = _i32(negs).reshape(B, -1)
@@ -139,13 +177,25 @@ class Engine(object):
     def step(self, pairs, negs, groups=None, return_loss=True):
         B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
         loss = ctypes.c_double(0.0)
-        N.check(self._L.cf_step(self._h, _ptr(pairs, ctypes.c_int32), _ptr(negs, ctypes.c_int32),
+        N.check(self._L.cf_step(self._h, _arg(pairs, ctypes.c_int32), _arg(negs, ctypes.c_int32),
                                 gp, B, ctypes.byref(loss) if return_loss else None), "cf_step")
         return float(loss.value) if return_loss else None
 
     def step_plr(self, tuples, coefs=None, return_loss=True):
         """One host-fed tuple step (CF_PLR): tuples [B, n_neg + 2] int
-        ((u,i,j,t,k) PRIGP / (u,i,t,j) CPLR), coefs [B, 2] float (CPLR)."""
+        ((u,i,j,t,k) PRIGP / (u,i,t,j) CPLR), coefs [B, 2] float (CPLR);
+        numpy arrays or torch device tensors."""
+        if _is_dev(tuples):
+            import torch
+            t, tp = _dev(tuples, torch.int32, ctypes.c_int32)
+            B, width = t.shape
+            cp = None
+            if coefs is not None:
+                c, cp = _dev(coefs.reshape(B, 2), torch.float32, ctypes.c_float)
+            out = ctypes.c_double(0.0)
+            N.check(self._L.cf_step_plr(self._h, tp, int(width), cp, int(B),
+                                        ctypes.byref(out) if return_loss else None), "cf_step_plr")
+            return float(out.value) if return_loss else None
         t = _i32(tuples)
         B, width = t.shape
         cp = None
@@ -199,8 +249,8 @@ class Engine(object):
                     "cf_step_local")
             return
         B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
-        N.check(self._L.cf_step_local(self._h, B, _ptr(pairs, ctypes.c_int32),
-                                      _ptr(negs, ctypes.c_int32), gp), "cf_step_local")
+        N.check(self._L.cf_step_local(self._h, B, _arg(pairs, ctypes.c_int32),
+                                      _arg(negs, ctypes.c_int32), gp), "cf_step_local")
 
     def step_local_grad(self, batch_size=None, pairs=None, negs=None, groups=None):
         if pairs is None:
@@ -208,8 +258,8 @@ class Engine(object):
                     "cf_step_local_grad")
             return
         B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
-        N.check(self._L.cf_step_local_grad(self._h, B, _ptr(pairs, ctypes.c_int32),
-                                           _ptr(negs, ctypes.c_int32), gp), "cf_step_local_grad")
+        N.check(self._L.cf_step_local_grad(self._h, B, _arg(pairs, ctypes.c_int32),
+                                           _arg(negs, ctypes.c_int32), gp), "cf_step_local_grad")
 
     def step_local_apply(self, next_batch_size=0):
         N.check(self._L.cf_step_local_apply(self._h, int(next_batch_size)), "cf_step_local_apply")
@@ -267,6 +317,18 @@ class Engine(object):
 
     # ---- evaluation -------------------------------------------------------------
     def score_topk(self, users, k, exclude_train=True, return_values=False):
+        if _is_dev(users):   # device ids in, device results out
+            import torch
+            u, up = _dev(users.reshape(-1), torch.int32, ctypes.c_int32)
+            n = u.shape[0]
+            idx = torch.empty((n, int(k)), dtype=torch.int32, device=u.device)
+            val = torch.empty((n, int(k)), dtype=torch.float32, device=u.device) if return_values else None
+            N.check(self._L.cf_score_topk(
+                self._h, up, n, int(k), 1 if exclude_train else 0,
+                ctypes.cast(idx.data_ptr(), ctypes.POINTER(ctypes.c_int32)),
+                ctypes.cast(val.data_ptr(), ctypes.POINTER(ctypes.c_float)) if return_values else None),
+                "cf_score_topk")
+            return (idx, val) if return_values else idx
         users = _i32(users).reshape(-1)
         n = users.shape[0]
         idx = np.empty((n, int(k)), dtype=np.int32)

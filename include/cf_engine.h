@@ -13,8 +13,14 @@
  *  - Every function returns 0 (CF_OK) on success or a negative cf_status;
  *    cf_last_error() returns a thread-local message for the last failure.
  *    No C++ exception crosses this boundary.
- *  - Pointers named host_* / taking "host" buffers are host memory; the
- *    engine copies them.  The engine owns all device memory.
+ *  - Caller buffers are borrowed for the call and copied; the engine owns
+ *    all device memory.  Batches (cf_step, cf_step_local*, cf_xchg_begin,
+ *    cf_step_plr), tables (cf_set_table / cf_get_table) and cf_score_topk's
+ *    users / outputs may be host memory or HIP device memory (e.g.
+ *    torch.Tensor.data_ptr()), told apart by a pointer-attribute query
+ *    (SURVEY 8(b)); a device batch is unpacked and range-checked on the
+ *    device.  A batch is all host or all device.  Device inputs must be
+ *    complete (their producer stream synchronised) before the call.
  *  - A handle is not thread-safe: one handle per thread.  All device work is
  *    enqueued on the engine's HIP stream; functions that write host outputs
  *    synchronise that stream before returning.
