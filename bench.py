@@ -101,6 +101,48 @@ def load_pmc(workload, n_gpus):
         return None
 
 
+def ndcg_cfg1(device):
+    """BASELINE configs[0] quality check: BPRMF on ml-100k fold 1 with the
+    testbprmf.py settings (d=32, reg=.1, B=100, W=1, 50 epochs), fed the
+    reference sampler's exact stream for np.random.seed(11) from the seeded
+    tables of tests/golden/make_cfg1_golden.py, scored by the drop-in's own
+    recommend + evaluateCV; the oracle's metrics for the same run are the
+    committed fixture tests/golden/cfg1_oracle_metrics.json."""
+    import scipy.sparse as sp
+    from collaborativefilteringusingtensorflow_amd.bprmf import BPRMF
+    from collaborativefilteringusingtensorflow_amd.init_util import seeded_table
+    from collaborativefilteringusingtensorflow_amd.sampler_ranking import ExactSampler
+    gdir = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(gdir, "cfg1_oracle_metrics.json")) as f:
+        ref = json.load(f)
+    c = ref["config"]
+    z = np.load(os.path.join(gdir, "ml100k_fold1.npz"))
+    shape = (int(z["n_users"]), int(z["n_items"]))
+    tra = sp.lil_matrix(sp.csr_matrix((np.ones(len(z["train_indices"]), np.float32),
+                                       z["train_indices"], z["train_indptr"]), shape=shape))
+    tst = sp.lil_matrix(sp.csr_matrix((np.ones(len(z["test_indices"]), np.float32),
+                                       z["test_indices"], z["test_indptr"]), shape=shape))
+    rng = np.random.RandomState(c["init_seed"])
+    U0 = seeded_table(rng, (shape[0], c["d"]))
+    V0 = seeded_table(rng, (shape[1], c["d"]))
+    t0 = time.perf_counter()
+    m = BPRMF(shape[0], shape[1], c["topN"], 'cv', c["metrics"], c["reg"], c["d"], c["B"],
+              max_iter=c["epochs"], device=device, verbose=False)
+    m.set_initial_tables(user=U0, item=V0)
+    es = ExactSampler(tra, n_neg=c["W"], batch_size=c["B"], seed=c["sampler_seed"])
+    got = m.train(1, tra, tst, es)
+    es.close()
+    m.close()
+    dt = time.perf_counter() - t0
+    g = dict(zip(c["metrics"], [float(x) for x in got]))
+    return {"value": g["ndcg"], "ref_oracle": ref["metrics"]["ndcg"],
+            "rel_diff": abs(g["ndcg"] - ref["metrics"]["ndcg"]) / ref["metrics"]["ndcg"],
+            "metrics": g, "seconds": dt,
+            "config": "cfg1: BPRMF ml-100k fold 1, d=32, reg=.1, B=100, W=1, 50 epochs, "
+                      "reference sampler stream (seed 11), NDCG@10 vs the oracle on the same "
+                      "batches and init"}
+
+
 def cpu_threads():
     """Host threads for the all-cores CPU baseline: OMP_NUM_THREADS when set
     (the GPU box sets it to the job's CPU share), else every visible CPU."""
@@ -169,6 +211,7 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="pairs per GPU per step (0 = config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-ndcg", action="store_true", help="skip the cfg1 NDCG@10 check")
     ap.add_argument("--score-pass", action="store_true",
                     help="also time one full scoring + top-10 pass over this rank's users")
     ap.add_argument("--grad-path", type=int, default=0,
@@ -367,6 +410,12 @@ def main():
                              "TFLOPs": flop / ts / 1e12,
                              "frac_fp32_mfma_peak": flop / ts / 1e12 / (157.3 * world),
                              "kernel": "fused_topk_kernel (v_mfma_f32_32x32x2_f32 + streaming top-k)"}
+    if rank == 0 and world == 1 and not args.no_ndcg:
+        try:
+            out["ndcg10_vs_ref"] = ndcg_cfg1(local_rank)
+        except Exception as ex:  # the bench line must still print
+            log("cfg1 ndcg run failed: %r" % (ex,))
+            out["ndcg10_vs_ref"] = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg, indptr, indices)

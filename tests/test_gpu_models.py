@@ -83,6 +83,13 @@ def test_cfg1_bprmf_metrics_match_oracle(fold1, epochs):
     for m, a, b in zip(metrics, got, ref):
         assert abs(a - b) <= 2e-3 * abs(b), (m, a, b)
     assert ref[metrics.index('ndcg')] > 0.2   # trained, not random
+    # the committed cfg1 golden (tests/golden/make_cfg1_golden.py) is this
+    # same oracle run: bench.py reports NDCG@10 against it
+    import json, os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "cfg1_oracle_metrics.json")) as f:
+        g = json.load(f)["metrics"]
+    for m, b in zip(metrics, ref):
+        assert abs(g[m] - b) <= 1e-9 * abs(b), (m, g[m], b)
 
 
 def test_device_sampled_drivers_train(fold1):

@@ -3,7 +3,7 @@
 # with extra option sets: VARIANT_OPTS="name:args;name:args"
 set -o pipefail
 mkdir -p gpurun_out
-ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline --no-ndcg}
 OPTS=${VARIANT_OPTS:-"base:"}
 run() {  # name lib args...
   local n=$1 lib=$2; shift 2

@@ -9,7 +9,7 @@ OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
 mkdir -p $OUT
 timeout -k 10 400 python bench.py > $OUT/rp_bench_cfg2.json 2> $OUT/rp_bench_cfg2.err || { echo "bench failed"; tail -20 $OUT/rp_bench_cfg2.err; exit 1; }
 cat $OUT/rp_bench_cfg2.json
-A="--steps 100 --warmup 10 --no-cpu-baseline"
+A="--steps 100 --warmup 10 --no-cpu-baseline --no-ndcg"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/rp_trace -o run -- python bench.py $A > $OUT/rp_trace.log 2>&1 || { echo "trace pass failed"; tail -20 $OUT/rp_trace.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/rp_fetch -o run -- python bench.py $A --no-profile > $OUT/rp_fetch.log 2>&1 || { echo "fetch pass failed"; tail -20 $OUT/rp_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/rp_write -o run -- python bench.py $A --no-profile > $OUT/rp_write.log 2>&1 || { echo "write pass failed"; tail -20 $OUT/rp_write.log; exit 1; }

@@ -5,7 +5,7 @@
 # (in-order prep so kernel times are standalone).
 set -o pipefail
 mkdir -p gpurun_out
-ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 200 --warmup 20 --no-cpu-baseline --no-ndcg}
 run() {  # name, extra args...
   local n=$1; shift
   timeout -k 10 300 python bench.py $ARGS "$@" > gpurun_out/var_$n.json 2> gpurun_out/var_$n.err || { echo "variant $n failed"; tail -5 gpurun_out/var_$n.err; exit 1; }
