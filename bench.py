@@ -224,6 +224,10 @@ def main():
                     help="cf_set_option slot_max (0 = engine default)")
     ap.add_argument("--n-users", type=int, default=0, help="override the config's users (rehearsals)")
     ap.add_argument("--n-items", type=int, default=0, help="override the config's items (rehearsals)")
+    ap.add_argument("--hot-replicas", type=int, default=0,
+                    help="cf_set_option hot_replicas (0 = engine default)")
+    ap.add_argument("--zipf", type=float, default=-1.0,
+                    help="override the item popularity exponent (experiments; 0 = uniform)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -232,6 +236,9 @@ def main():
         cfg["n_users"] = args.n_users or cfg["n_users"]
         cfg["n_items"] = args.n_items or cfg["n_items"]
         cfg["desc"] += " [rehearsal: %d users x %d items]" % (cfg["n_users"], cfg["n_items"])
+    if args.zipf >= 0:
+        cfg["zipf"] = args.zipf
+        cfg["desc"] += " [experiment: zipf %.2f]" % args.zipf
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -269,6 +276,8 @@ def main():
     eng.set_option("grad_path", args.grad_path)
     eng.set_option("prep_stream", args.prep_stream)
     eng.set_option("pipeline", args.pipeline)
+    if args.hot_replicas:
+        eng.set_option("hot_replicas", args.hot_replicas)
     if args.slot_max:
         eng.set_option("slot_max", args.slot_max)
     eng.set_interactions(indptr, indices)

@@ -84,6 +84,10 @@ struct cf_engine {
     float* slotU = nullptr;   // [n_users * capU, d]
     float* slotV = nullptr;   // [n_items * capV, d]
     int capU = 2, capV = 32;
+    // hot item rows (occurrences past capV) spread their float atomics over
+    // GV and hot_rep - 1 extra copies (cf_set_option "hot_replicas")
+    float* GVrep = nullptr;   // [hot_rep - 1][n_items, d]
+    int hot_rep = 1;
     bool slots_ready = false;
     // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
     // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches)
@@ -215,8 +219,16 @@ int ensure_slots(cf_engine* e) {
     CF_HIP(hipStreamSynchronize(e->stream));
     dfree(e->slotU);
     dfree(e->slotV);
+    dfree(e->GVrep);
     CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
-    if (!c.dense_item_apply) CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+    if (!c.dense_item_apply) {
+        CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+        if (e->hot_rep > 1) {
+            const size_t n = (size_t)(e->hot_rep - 1) * c.n_items * c.n_factors;
+            CF_TRY(dalloc(&e->GVrep, n));
+            CF_HIP(hipMemsetAsync(e->GVrep, 0, n * sizeof(float), e->stream));
+        }
+    }
     e->slots_ready = true;
     return CF_OK;
 }
@@ -283,6 +295,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.slotV = e->slotV;
     a.capU = e->capU;
     a.capV = e->capV;
+    a.GVrep = e->GVrep;
+    a.repV = e->GVrep ? e->hot_rep - 1 : 0;
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
     a.count_items = c.dense_item_apply ? 0 : 1;
@@ -459,6 +473,9 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.clip = c.model == CF_CML ? 1 : 0;
     p.capU = e->capU;
     p.capV = e->capV;
+    p.GVrep = e->GVrep;
+    p.repV = e->GVrep ? e->hot_rep - 1 : 0;
+    p.n_items = c.n_items;
     p.count_users = a.count_users;
     p.count_items = a.count_items;
     p.occU = e->occU_[k];
@@ -824,7 +841,7 @@ int cf_destroy(cf_engine* e) {
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
-    dfree(e->slotU); dfree(e->slotV); dfree(e->x_own); dfree(e->coefs);
+    dfree(e->slotU); dfree(e->slotV); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -1476,6 +1493,15 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_HIP(hipStreamSynchronize(e->stream));
         if (n == "slot_max") e->capV = (int)value; else e->capU = (int)value;
         e->slots_ready = false;   // re-sized at the next step
+        return CF_OK;
+    }
+    if (n == "hot_replicas") {
+        if (value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
+            return fail(CF_EINVAL, "hot_replicas must be 1, 2, 4, 8 or 16");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        e->hot_rep = (int)value;
+        e->slots_ready = false;
         return CF_OK;
     }
     if (n == "grad_path") {

@@ -77,7 +77,9 @@ struct StepArgs {
     int32_t* __restrict__ rankV;  // [B*(1+W)]
     float* __restrict__ slotU;    // [n_users * capU, d]
     float* __restrict__ slotV;    // [n_items * capV, d]
-    int capU, capV;               // rows above this many occurrences use float atomics into G
+    int capU, capV;               // occurrences at rank >= cap use float atomics into G
+    float* __restrict__ GVrep;    // [repV][n_items, d] extra item accumulators (hot rows)
+    int repV;                     // replica mask: item occurrence k >= capV adds to copy k & repV
     double* __restrict__ loss_partial;  // [grad grid]
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
@@ -112,6 +114,9 @@ struct ApplyArgs {
     float clip_norm;
     int clip;            // CML: clip updated rows
     int capU, capV;      // fixed slot range per row
+    float* __restrict__ GVrep;  // hot item rows: extra accumulators (StepArgs)
+    int repV;
+    int64_t n_items;
     int count_users, count_items;
     // work items: the batch's occurrences (+ the served rows of the group
     // exchange); the owner of a duplicated row applies it

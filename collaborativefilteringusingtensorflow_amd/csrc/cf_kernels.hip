@@ -200,11 +200,20 @@ __device__ __forceinline__ void gstore(float* __restrict__ S, int64_t r, int d, 
     row_st<EPL>(S + r * (int64_t)d, d, gl, g);
 }
 
-// slot row of one occurrence of a duplicated row: a row with 2..cap
-// occurrences owns the fixed slots [r*cap, r*cap + count), in rank order;
-// -1 = hot row (more occurrences) or uncounted table -> float atomics into G
-__device__ __forceinline__ int64_t slot_of(int count, int64_t r, int rank, int cap) {
-    return (count >= 2 && count <= cap) ? r * (int64_t)cap + rank : -1;
+// slot row of one occurrence of a duplicated row: row r owns the fixed slots
+// [r*cap, (r+1)*cap) and occurrence `rank` < cap stores there.  Occurrences
+// at rank >= cap of a hot row, every occurrence of a row flagged by the group
+// exchange and those of an uncounted table go to float atomics: -1 - k means
+// accumulator copy k (0 = G itself; items spread a hot row over repV + 1
+// copies by rank, so its atomics do not all queue on one address)
+__device__ __forceinline__ int64_t slot_of(int count, int64_t r, int rank, int cap, int rep) {
+    if (count >= 2 && !(count & kRemoteFlag) && rank < cap) return r * (int64_t)cap + rank;
+    return -1 - (rank & rep);
+}
+
+// the accumulator an atomic-path occurrence adds to (see slot_of)
+__device__ __forceinline__ float* acc_of(float* G, int64_t slot, const StepArgs& a) {
+    return slot == -1 ? G : a.GVrep + (-2 - slot) * a.n_items * (int64_t)a.d;
 }
 
 // row r of X: singleton -> apply now; duplicated -> its slot row (summed by
@@ -222,7 +231,7 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
     } else if (slot >= 0) {
         gstore<EPL>(S, slot, d, gl, g);
     } else {
-        gatomic<EPL>(G, r, d, gl, g);
+        gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
     }
 }
 
@@ -438,7 +447,7 @@ struct NegRows {
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 c[w] = a.count_items ? a.cntV[j[w]] : 0;
-                sl[w] = slot_of(c[w], j[w], rk[w], a.capV);
+                sl[w] = slot_of(c[w], j[w], rk[w], a.capV, a.repV);
                 gload<EPL>(a.V, j[w], a.d, gl, v[w]);
             }
         }
@@ -451,7 +460,7 @@ struct NegRows {
             j[0] = a.occV[a.B + p * a.W + w];
             const int rk = a.count_items ? a.rankV[a.B + p * a.W + w] : 0;
             c[0] = a.count_items ? a.cntV[j[0]] : 0;
-            sl[0] = slot_of(c[0], j[0], rk, a.capV);
+            sl[0] = slot_of(c[0], j[0], rk, a.capV, a.repV);
             gload<EPL>(a.V, j[0], a.d, gl, v[0]);
             return 0;
         }
@@ -481,8 +490,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
         J.prefetch(a, p, gl);
         const int cu = a.count_users ? a.cntU[u] : 0;
         const int ci = a.count_items ? a.cntV[i] : 0;
-        const int64_t su = slot_of(cu, u, ru, a.capU);
-        const int64_t si = slot_of(ci, i, ri, a.capV);
+        const int64_t su = slot_of(cu, u, ru, a.capU, 0);
+        const int64_t si = slot_of(ci, i, ri, a.capV, a.repV);
         float uu[EPL], vi[EPL];
         gload<EPL>(a.U, u, d, gl, uu);
         gload<EPL>(a.V, i, d, gl, vi);
@@ -592,7 +601,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     continue;
                 }
                 const int cg = a.cntU[g];
-                const int64_t sg_ = slot_of(cg, g, a.rankU[B + p * G + k2], a.capU);
+                const int64_t sg_ = slot_of(cg, g, a.rankU[B + p * G + k2], a.capU, 0);
                 gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
             if (gl == 0) bias_finish(a, i, ci, sc);
@@ -824,7 +833,7 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
         gstore<EPL>(S, slot, d, gl, g);
     } else {
 #ifndef CF_EXP_NO_ATOMIC
-        gatomic<EPL>(G, r, d, gl, g);
+        gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
 #endif
     }
 }
@@ -879,12 +888,12 @@ struct PairRows {
         }
     }
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
-        su = slot_of(cu, u, ru, a.capU);
-        si = slot_of(ci, i, ri, a.capV);
+        su = slot_of(cu, u, ru, a.capU, 0);
+        si = slot_of(ci, i, ri, a.capV, a.repV);
 #pragma unroll
-        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV);
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV);
 #pragma unroll
-        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU);
+        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
         gload_acc<EPL>(a.AV, i, a.d, gl, ci == 1, ai);
 #pragma unroll
@@ -1115,27 +1124,44 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     float x[EPL], acc[EPL], g[EPL];
     gload<EPL>(X, r, a.d, gl, x);
     gload_acc<EPL>(A, r, a.d, gl, true, acc);
-    if (c <= cap) {
+    // c = the row's count word: occurrences, plus kRemoteFlag for a row the
+    // group exchange served (all its contributions went to G)
+    const int flagged = c & kRemoteFlag;
+    const int local = c & (kRemoteFlag - 1);
+    const int ns = flagged ? 0 : (local < cap ? local : cap);
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) g[s] = 0.f;
+    {
         const float* S = isU ? a.slotU : a.slotV;
         const int64_t s0 = r * (int64_t)cap;
-#pragma unroll
-        for (int s = 0; s < EPL; ++s) g[s] = 0.f;
         constexpr int NF = 4;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
-        for (int t0 = 0; t0 < c; t0 += NF) {
+        for (int t0 = 0; t0 < ns; t0 += NF) {
             float h[NF][EPL];
 #pragma unroll
             for (int q = 0; q < NF; ++q)
-                if (t0 + q < c) gload<EPL>(S, s0 + t0 + q, a.d, gl, h[q]);
+                if (t0 + q < ns) gload<EPL>(S, s0 + t0 + q, a.d, gl, h[q]);
 #pragma unroll
             for (int q = 0; q < NF; ++q)
-                if (t0 + q < c) {
+                if (t0 + q < ns) {
 #pragma unroll
                     for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
                 }
         }
-    } else {
-        gload<EPL>(G, r, a.d, gl, g);
+    }
+    if (flagged || local > cap) {  // the atomic sums: G, and for items the copies in use
+        const int nrep = isU ? 0 : a.repV;   // copies 1..repV (unused ones are zero)
+        float h[EPL];
+        gload<EPL>(G, r, a.d, gl, h);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] += h[s];
         row_zero<EPL>(G + r * a.d, a.d, gl);
+        for (int k = 0; k < nrep; ++k) {
+            float* Gk = a.GVrep + (int64_t)k * a.n_items * a.d;
+            gload<EPL>(Gk, r, a.d, gl, h);
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) g[s] += h[s];
+            row_zero<EPL>(Gk + r * a.d, a.d, gl);
+        }
     }
     gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
     if (gl == 0) {

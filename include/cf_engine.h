@@ -310,13 +310,17 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "prep_stream" 0 = everything in order on the engine stream (default);
  *                1 = sample/count on a side stream, overlapping the previous
  *                step's gradient.  Same results.
- *   "slot_max"   an item row occurring 2..slot_max times in a batch sums its
- *                per-occurrence gradient rows from plain-stored slot rows
- *                (row r owns the fixed range [r*slot_max, (r+1)*slot_max));
- *                rows occurring more often use float atomics (default 32;
- *                1 = atomics for every duplicated row).  Same arithmetic up
- *                to fp32 summation order.
+ *   "slot_max"   occurrence k < slot_max of a duplicated item row stores its
+ *                gradient row in a plain slot row (row r owns the fixed range
+ *                [r*slot_max, (r+1)*slot_max)); later occurrences of a hot row
+ *                add into a float accumulator with atomics; the apply sums
+ *                both (default 32).  Same arithmetic up to fp32 summation
+ *                order.
  *   "slot_max_user" the same for user rows (default 2).
+ *   "hot_replicas" the atomic part of a hot item row is spread over this many
+ *                accumulator copies by occurrence rank (1, 2, 4, 8, 16;
+ *                default 1: at cfg2 the copies' extra apply reads cost more
+ *                than the spread atomics save).
  *   "pipeline"   how cf_train_steps overlaps consecutive steps (same results):
  *                1 = the duplicate apply of step s with the draw + count of
  *                step s+1, two launches per step (default); 0 = one step at a

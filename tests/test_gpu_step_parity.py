@@ -162,17 +162,57 @@ def opts():
     _OPTS.clear()
 
 
+@pytest.mark.parametrize("hot_replicas", [1, 8])
 @pytest.mark.parametrize("slot_max", [1, 2, 3, 256])
 @pytest.mark.parametrize("model,name,d", [("bpr", "rank_b50_w5", 24), ("amf", "rank_b100_w5", 40)])
-def test_slot_regimes_match_oracle(fold1, streams, opts, slot_max, model, name, d):
-    """Duplicated rows: every split between slot store-and-sum (2..slot_max
-    occurrences, fixed per-row slot ranges) and float atomics (more) gives
-    the TF1 dedup-sum, for item and user rows."""
+def test_slot_regimes_match_oracle(fold1, streams, opts, slot_max, hot_replicas, model, name, d):
+    """Duplicated rows: every split between slot store-and-sum (the first
+    slot_max occurrences, fixed per-row slot ranges) and float atomics (the
+    rest, over hot_replicas accumulator copies) gives the TF1 dedup-sum, for
+    item and user rows."""
     opts["slot_max"] = slot_max
     opts["slot_max_user"] = slot_max
+    opts["hot_replicas"] = hot_replicas
     out = run_bpr_like(model, fold1, get_stream(streams, name), d, 0.05, K=40)
     for t, (g, o) in out.items():
         assert rel(g, o) <= RTOL, (t, rel(g, o))
+
+
+@pytest.mark.parametrize("slot_max,hot", [(3, 4), (32, 8), (32, 16)])
+def test_hot_item_over_every_replica(fold1, opts, slot_max, hot):
+    """One item as the positive of 600 pairs and the negative of 300 more:
+    its first slot_max occurrences use slots and the other ~900 spread over
+    every accumulator copy; the sum still equals the oracle's dedup-sum."""
+    opts["slot_max"] = slot_max
+    opts["hot_replicas"] = hot
+    d = 16
+    U, V, _ = init_tables(fold1, d, 13)
+    e = make_engine("bpr", fold1, d, 1, reg=0.02)
+    e.set_table("user", U)
+    e.set_table("item", V)
+    rng = np.random.RandomState(5)
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    hot = 49
+    pairs, negs = [], []
+    for r in range(900):
+        u = int(rng.randint(943))
+        row = set(ix[ip[u]:ip[u + 1]].tolist())
+        if r < 600 or hot in row:
+            pairs.append([u, hot if hot in row or r < 600 else int(ix[ip[u]])])
+            negs.append([next(x for x in rng.randint(0, 1682, 50) if x not in row)])
+        else:
+            pairs.append([u, int(ix[ip[u]]) if ip[u + 1] > ip[u] else 0])
+            negs.append([hot])
+    pairs, negs = np.array(pairs, np.int32), np.array(negs, np.int32)
+    U64, V64 = U.astype(np.float64), V.astype(np.float64)
+    AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
+    for s in range(3):
+        lg = e.step(pairs, negs)
+        lo = O.bpr_step(U64, V64, AU, AV, pairs, negs, 0.02)
+        assert abs(lg - lo) <= RTOL * abs(lo)
+    for t, o in (("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV)):
+        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+    e.close()
 
 
 @pytest.mark.parametrize("slot_max", [32, 64])
