@@ -250,7 +250,16 @@ def main():
     backend = os.environ.get("CF_DIST_BACKEND", "nccl")
     if os.environ.get("CF_SHARE_DEVICE") == "1":
         local_rank = 0
-    if world > 1:
+    # CF_BENCH_SHARDED=1 at N=1: the multi-GPU code path (dense item gradient,
+    # all-reduce over a one-rank group) -- the local cost of a sharded step
+    sharded = world > 1 or os.environ.get("CF_BENCH_SHARDED") == "1"
+    if sharded and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        cfg["desc"] += " [sharded code path, 1 rank]"
+    if sharded:
         import torch  # noqa: F811
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local_rank)
@@ -272,7 +281,7 @@ def main():
         if k in cfg:
             kw[k] = cfg[k]
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
-                 dense_item_apply=(world > 1), seed=1000 + rank, **kw)
+                 dense_item_apply=sharded, seed=1000 + rank, **kw)
     eng.set_option("grad_path", args.grad_path)
     eng.set_option("prep_stream", args.prep_stream)
     eng.set_option("pipeline", args.pipeline)
@@ -285,7 +294,7 @@ def main():
     if cfg["model"] == "amf":
         eng.begin_phase(1)
 
-    if world > 1 and cfg["model"] == "gbpr":
+    if sharded and cfg["model"] == "gbpr":
         # group members come from every shard: the global CSR feeds the
         # item -> user source, the exchange fetches / returns remote rows
         degs = synth_degrees(nu_all, cfg["mean_degree"], cfg["graph_seed"])
@@ -295,10 +304,10 @@ def main():
         step, _grad = make_gpu_group_exchange(eng, world, rank, bounds, gip, gix, ni, d, B,
                                               torch.device("cuda", local_rank))
         del gip, gix
-    elif world > 1:
+    elif sharded:
         step, _grad = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
                                        torch.device("cuda", local_rank))
-    if world > 1:
+    if sharded:
         def run(k):
             for _ in range(k):
                 step(B)
@@ -435,7 +444,7 @@ def main():
     if rank == 0:
         print(json.dumps(out))
         sys.stdout.flush()
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 
