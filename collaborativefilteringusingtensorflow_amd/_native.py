@@ -120,6 +120,7 @@ SIGNATURES = {
     "cf_ens_set_interactions": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
     "cf_ens_step": (ctypes.c_int, [_P, _PI32, _I32, _PD]),
     "cf_ens_take_loss": (ctypes.c_int, [_P, _PD]),
+    "cf_ens_step_w": (ctypes.c_int, [_P, _PI32, _PI32, _I32, _I32, _F, _I32, _PD]),
     "cf_ens_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
     "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
     "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),

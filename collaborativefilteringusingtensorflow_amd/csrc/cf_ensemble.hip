@@ -277,6 +277,150 @@ __global__ __launch_bounds__(kBlock) void ens_score_kernel(int K, int d, int64_t
     keys[(int64_t)c * n_items + it] = key;
 }
 
+// ---------------------------------------------------------------------------
+// W-negative variants (ensemble_.py:75-118, ensemble__.py:102-145): per pair
+// p, items x in {i, j_0..j_{W-1}}: r_x = sum_k w_k(x) s_k(x); loss
+// lam * sum_w -log sigmoid(r_i - r_jw) (+ the members' own BPR terms
+// sum_k sum_w -log sigmoid(s_k(i) - s_k(j_w)) when `singles`).  One 16-lane
+// group per pair; the K x (1+W) scores and weights live in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kEnsMaxW = 8;
+
+struct EnsWArgs {
+    int K, d, B, W, singles;
+    int64_t n_users, n_items;
+    float reg, lam;
+    const int32_t* __restrict__ pairs;   // [B, 2]
+    const int32_t* __restrict__ negs;    // [B, W]
+    const float* __restrict__ U;
+    const float* __restrict__ V;
+    const float* __restrict__ H;
+    float* __restrict__ GU;
+    float* __restrict__ GV;
+    float* __restrict__ GH;
+    double* __restrict__ loss_partial;   // [blocks]
+    double* __restrict__ loss_acc;
+};
+
+__global__ __launch_bounds__(kBlock) void ens_w_kernel(EnsWArgs a) {
+    constexpr int X1 = kEnsMaxW + 1;
+    __shared__ float s_s[kGroupsPerBlock][kEnsMaxK][X1];   // s_k(x), then dL/ds_k(x)
+    __shared__ float s_w[kGroupsPerBlock][kEnsMaxK][X1];   // w_k(x), then dL/de_k(x)
+    __shared__ double s_l[kGroupsPerBlock];
+    extern __shared__ float s_gh[];                        // [K, d]
+    for (int t = threadIdx.x; t < a.K * a.d; t += kBlock)
+        s_gh[t] = (blockIdx.x == 0) ? a.reg * a.H[t] : 0.f;   // + reg * H, once
+    __syncthreads();
+    const int gl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int p = blockIdx.x * kGroupsPerBlock + grp;
+    const int K = a.K, W = a.W, NX = 1 + a.W;
+    float sq = 0.f, lossf = 0.f;
+    if (p < a.B) {
+        const int64_t u = a.pairs[2 * p];
+        auto item = [&](int x) -> int64_t { return x == 0 ? a.pairs[2 * p + 1] : a.negs[(int64_t)p * W + x - 1]; };
+        // scores s_k(x) and attention logits, per member
+        for (int k = 0; k < K; ++k) {
+            const float* uk = a.U + ((int64_t)k * a.n_users + u) * a.d;
+            const float* hk = a.H + (int64_t)k * a.d;
+            for (int x = 0; x < NX; ++x) {
+                const float* vk = a.V + ((int64_t)k * a.n_items + item(x)) * a.d;
+                float sv = 0.f, ev = 0.f;
+                for (int e = gl; e < a.d; e += 16) {
+                    const float uu = uk[e], vv = vk[e];
+                    sv = fmaf(uu, vv, sv);
+                    ev = fmaf(uu * vv, hk[e], ev);
+                    sq = fmaf(vv, vv, sq);
+                    if (x == 0) sq = fmaf(uu, uu, sq);
+                }
+                sv = g16sum(sv);
+                ev = g16sum(ev);
+                if (gl == 0) {
+                    s_s[grp][k][x] = sv;
+                    s_w[grp][k][x] = expf(ev);   // exp(<u o v, h_k>), ensemble_.py:89-91
+                }
+            }
+        }
+        if (gl == 0) {
+            float r[X1], den[X1];
+            for (int x = 0; x < NX; ++x) {
+                den[x] = 0.f;
+                for (int k = 0; k < K; ++k) den[x] += s_w[grp][k][x];
+                r[x] = 0.f;
+                for (int k = 0; k < K; ++k) {
+                    s_w[grp][k][x] /= den[x];
+                    r[x] = fmaf(s_s[grp][k][x], s_w[grp][k][x], r[x]);
+                }
+            }
+            // dL/dr_x for the ensemble term
+            float gr[X1];
+            gr[0] = 0.f;
+            for (int w = 1; w < NX; ++w) {
+                const float z = r[0] - r[w];
+                lossf += a.lam * (-logf(1.f / (1.f + expf(-z))));
+                const float c = a.lam * (-1.f / (1.f + expf(z)));
+                gr[0] += c;
+                gr[w] = -c;
+            }
+            // singles: the members' own BPR terms (ensemble__.py:118-133)
+            float ds0[kEnsMaxK];
+            for (int k = 0; k < K; ++k) ds0[k] = 0.f;
+            for (int k = 0; k < K; ++k) {
+                const float si = s_s[grp][k][0];
+                for (int x = 0; x < NX; ++x) {
+                    const float wv = s_w[grp][k][x], sv = s_s[grp][k][x];
+                    float ds = gr[x] * wv;
+                    const float de = gr[x] * wv * (sv - r[x]);   // softmax backward
+                    if (a.singles && x > 0) {
+                        const float z = si - sv;
+                        lossf += -logf(1.f / (1.f + expf(-z)));
+                        const float c = -1.f / (1.f + expf(z));
+                        ds0[k] += c;
+                        ds -= c;
+                    }
+                    s_s[grp][k][x] = ds;   // now dL/ds_k(x) (the positive's singles part added below)
+                    s_w[grp][k][x] = de;   // now dL/de_k(x)
+                }
+            }
+            for (int k = 0; k < K; ++k) s_s[grp][k][0] += ds0[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // gradient rows: d(u o v_x) = ds + de * h_k
+        for (int k = 0; k < K; ++k) {
+            const int64_t ru = (int64_t)k * a.n_users + u;
+            const float* uk = a.U + ru * a.d;
+            const float* hk = a.H + (int64_t)k * a.d;
+            for (int e = gl; e < a.d; e += 16) {
+                const float uu = uk[e], h = hk[e];
+                float gu = a.reg * uu;
+                float gh = 0.f;
+                for (int x = 0; x < NX; ++x) {
+                    const int64_t rx = (int64_t)k * a.n_items + item(x);
+                    const float vv = a.V[rx * a.d + e];
+                    const float ds = s_s[grp][k][x], de = s_w[grp][k][x];
+                    const float gx = fmaf(de, h, ds);
+                    gu = fmaf(gx, vv, gu);
+                    unsafeAtomicAdd(a.GV + rx * a.d + e, fmaf(gx, uu, a.reg * vv));
+                    gh = fmaf(de, uu * vv, gh);
+                }
+                unsafeAtomicAdd(a.GU + ru * a.d + e, gu);
+                atomicAdd(&s_gh[k * a.d + e], gh);
+            }
+        }
+    }
+    const float t = g16sum(sq);
+    if (gl == 0) s_l[grp] = (double)lossf + 0.5 * (double)a.reg * (double)t;
+    __syncthreads();
+    for (int t2 = threadIdx.x; t2 < a.K * a.d; t2 += kBlock) unsafeAtomicAdd(a.GH + t2, s_gh[t2]);
+    if (threadIdx.x == 0) {
+        double acc = 0.0;
+        for (int g = 0; g < kGroupsPerBlock; ++g) acc += s_l[g];
+        if (blockIdx.x == 0)
+            for (int e = 0; e < a.K * a.d; ++e) acc += 0.5 * (double)a.reg * (double)a.H[e] * a.H[e];
+        a.loss_partial[blockIdx.x] = acc;
+        atomicAdd(a.loss_acc, acc);
+    }
+}
+
 }  // namespace cfk
 
 using namespace cfk;
@@ -518,6 +662,62 @@ int cf_ens_step(cf_ensemble* e, const int32_t* uij, int32_t B, double* loss_out)
         ENS_HIP(hipStreamSynchronize(e->stream));
         double t = 0.0;
         for (int q = 0; q < nl; ++q) t += e->h_loss[(size_t)q];
+        *loss_out = t;
+    }
+    return CF_OK;
+}
+
+int cf_ens_step_w(cf_ensemble* e, const int32_t* pairs, const int32_t* negs, int32_t W, int32_t B,
+                  float lam, int32_t singles, double* loss_out) {
+    if (!e || !pairs || !negs || B < 1) return cfi::set_error(CF_EINVAL, "bad arguments");
+    if (W < 1 || W > kEnsMaxW) return cfi::set_error(CF_EINVAL, "W must be 1..8");
+    for (int p = 0; p < B; ++p) {
+        bool ok = pairs[2 * p] >= 0 && pairs[2 * p] < e->n_users && pairs[2 * p + 1] >= 0 &&
+                  pairs[2 * p + 1] < e->n_items;
+        for (int w = 0; w < W; ++w) ok = ok && negs[(size_t)p * W + w] >= 0 && negs[(size_t)p * W + w] < e->n_items;
+        if (!ok) return cfi::set_error(CF_EINVAL, "pair " + std::to_string(p) + " out of range");
+    }
+    ENS_HIP(hipSetDevice(e->device));
+    const int K = e->K;
+    const int nb = (B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    const size_t need = (size_t)B * (2 + W);
+    if (need > (size_t)e->Bcap * 3) {   // reuse the uij buffer for [pairs | negs]
+        ENS_HIP(hipStreamSynchronize(e->stream));
+        efree(e->uij);
+        efree(e->scratch);
+        ENS_TRY(ealloc(&e->uij, need));
+        ENS_TRY(ealloc(&e->scratch, (size_t)8 * K * ((need + 2) / 3)));
+        e->Bcap = (int)((need + 2) / 3);
+    }
+    if (nb > e->loss_cap) {
+        ENS_HIP(hipStreamSynchronize(e->stream));
+        efree(e->loss_partial);
+        ENS_TRY(ealloc(&e->loss_partial, (size_t)nb));
+        e->loss_cap = nb;
+        e->h_loss.resize((size_t)nb);
+    }
+    ENS_HIP(hipMemcpyAsync(e->uij, pairs, (size_t)B * 8, hipMemcpyHostToDevice, e->stream));
+    ENS_HIP(hipMemcpyAsync(e->uij + 2 * (size_t)B, negs, (size_t)B * W * 4, hipMemcpyHostToDevice, e->stream));
+    EnsWArgs a{};
+    a.K = K; a.d = e->d; a.B = B; a.W = W; a.singles = singles ? 1 : 0;
+    a.n_users = e->n_users; a.n_items = e->n_items;
+    a.reg = e->reg; a.lam = lam;
+    a.pairs = e->uij; a.negs = e->uij + 2 * (size_t)B;
+    a.U = e->U; a.V = e->V; a.H = e->H;
+    a.GU = e->GU; a.GV = e->GV; a.GH = e->GH;
+    a.loss_partial = e->loss_partial;
+    a.loss_acc = e->loss_acc;
+    hipLaunchKernelGGL(ens_w_kernel, dim3(nb), dim3(kBlock), (size_t)K * e->d * 4, e->stream, a);
+    ENS_HIP(hipGetLastError());
+    ENS_TRY(dense_apply(e, e->U, e->AU, e->GU, (int64_t)K * e->n_users));
+    ENS_TRY(dense_apply(e, e->V, e->AV, e->GV, (int64_t)K * e->n_items));
+    ENS_TRY(dense_apply(e, e->H, e->AH, e->GH, K));
+    if (loss_out) {
+        ENS_HIP(hipMemcpyAsync(e->h_loss.data(), e->loss_partial, (size_t)nb * 8, hipMemcpyDeviceToHost,
+                               e->stream));
+        ENS_HIP(hipStreamSynchronize(e->stream));
+        double t = 0.0;
+        for (int q = 0; q < nb; ++q) t += e->h_loss[(size_t)q];
         *loss_out = t;
     }
     return CF_OK;

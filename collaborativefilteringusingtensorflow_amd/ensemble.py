@@ -97,6 +97,18 @@ class EnsembleEngine(object):
                                     ctypes.byref(loss) if return_loss else None), "cf_ens_step")
         return float(loss.value) if return_loss else None
 
+    def step_w(self, pairs, negs, lam=1.0, singles=False, return_loss=True):
+        """One step of the W-negative variants (cf_ens_step_w): pairs [B, 2],
+        negs [B, W]."""
+        pr = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+        B = pr.shape[0]
+        ng = np.ascontiguousarray(negs, dtype=np.int32).reshape(B, -1)
+        loss = ctypes.c_double(0.0)
+        N.check(self._L.cf_ens_step_w(self._h, _ptr(pr, ctypes.c_int32), _ptr(ng, ctypes.c_int32),
+                                      ng.shape[1], B, float(lam), 1 if singles else 0,
+                                      ctypes.byref(loss) if return_loss else None), "cf_ens_step_w")
+        return float(loss.value) if return_loss else None
+
     def take_loss(self):
         s = ctypes.c_double(0.0)
         N.check(self._L.cf_ens_take_loss(self._h, ctypes.byref(s)), "cf_ens_take_loss")
@@ -142,6 +154,9 @@ class Ensemble(object):
              if a is not None}
         self._init_tables = t or None
 
+    def _feed(self, eng, batch):
+        eng.step(batch, return_loss=False)   # [B, 3] (u, i, j), ensemble.py:204-205
+
     def _recommend(self, test_users):
         idx = self._engine.score_topk(np.asarray(test_users, dtype=np.int32), self._topN,
                                       exclude_train=True)
@@ -179,7 +194,7 @@ class Ensemble(object):
         for it in range(self._max_iter):
             t0 = time.time()
             for _ in range(n_batches):
-                eng.step(sampler.next_batch(), return_loss=False)
+                self._feed(eng, sampler.next_batch())
             aveloss = eng.take_loss() / max(n_batches, 1)
             scores = self._eval(yss_true, self._recommend(test_users))
             if self._verbose:
@@ -196,3 +211,16 @@ class Ensemble(object):
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+
+
+class EnsembleW(Ensemble):
+    """Shared host loop of the W-negative variants (ensemble_.py,
+    ensemble__.py): sampler_ranking batches (pairs [B, 2], negs [B, W]),
+    cf_ens_step_w with the variant's lam / singles."""
+    LAM_FROM_ARG = False
+    SINGLES = False
+
+    def _feed(self, eng, batch):
+        pairs, negs = batch
+        lam = self.ensemble_lambda if self.LAM_FROM_ARG else 1.0
+        eng.step_w(pairs, negs, lam=lam, singles=self.SINGLES, return_loss=False)

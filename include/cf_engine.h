@@ -391,6 +391,14 @@ int cf_ens_set_interactions(cf_ensemble* e, const int64_t* indptr, const int32_t
 /* one optimizer step on B host triplets [B,3] int32; loss_out (may be NULL,
  * else syncs) = the pre-update loss of the batch */
 int cf_ens_step(cf_ensemble* e, const int32_t* host_uij, int32_t B, double* loss_out);
+/* W-negative variants: pairs [B,2] + negs [B,W] (W <= 8)
+ * from sampler_ranking.  Loss per pair and negative, no [B, B] broadcast:
+ * lam * sum_w -log sigmoid(r_i - r_jw), r_x = sum_k w_k(x) s_k(x)
+ * (ensemble_.py:75-118, lam = 1, singles = 0); singles = 1 adds every
+ * member's own BPR terms sum_k sum_w -log sigmoid(s_k(i) - s_k(j_w)) with
+ * lam = ensemble_lambda (ensemble__.py:102-145).  Same reg and dense Adagrad. */
+int cf_ens_step_w(cf_ensemble* e, const int32_t* host_pairs, const int32_t* host_negs, int32_t W,
+                  int32_t B, float lam, int32_t singles, double* loss_out);
 /* sum of the step losses since the last call (syncs), then reset */
 int cf_ens_take_loss(cf_ensemble* e, double* sum_out);
 int cf_ens_score_topk(cf_ensemble* e, const int32_t* host_users, int32_t n, int32_t k,

@@ -382,6 +382,58 @@ def ens_step(U, V, H, AU, AV, AH, uij, reg, lr=0.1):
     return loss
 
 
+def ens_w_step(U, V, H, AU, AV, AH, pairs, negs, reg, lam=1.0, singles=False, lr=0.1):
+    """One step of the W-negative Ensemble variants, in place.
+
+    ensemble_.py:75-118 (lam = 1, singles off): r_x = sum_k w_k(x) s_k(x)
+    with the member softmax w over <U_k[u] o V_k[x], h_k>, loss
+    sum_{p,w} -log sigmoid(r_i - r_{j_w}) -- per pair, no [B, B] broadcast;
+    ensemble__.py:102-145 adds the members' own BPR terms
+    sum_k sum_{p,w} -log sigmoid(s_k(i) - s_k(j_w)) and weights the ensemble
+    term by lam (ensemble_lambda).  + reg (sum_k l2(U_k[u]) + l2(V_k[i]) +
+    l2(V_k[negs]) + l2(H)); dense Adagrad on U, V, H.  Returns the loss."""
+    dt = U.dtype.type
+    reg, lam = dt(reg), dt(lam)
+    pairs = np.asarray(pairs)
+    B = pairs.shape[0]
+    negs = np.asarray(negs).reshape(B, -1)
+    u, i = pairs[:, 0], pairs[:, 1]
+    X = np.concatenate([i[:, None], negs], 1)               # [B, 1+W] items
+    Uu = U[:, u]                                             # [K, B, d]
+    VX = V[:, X]                                             # [K, B, 1+W, d]
+    P = Uu[:, :, None, :] * VX
+    S = P.sum(-1)                                            # s_k(x)   [K, B, 1+W]
+    A = np.exp(np.einsum("kbxd,kd->kbx", P, H))
+    Wt = A / A.sum(0)                                        # w_k(x)
+    R = (Wt * S).sum(0)                                      # r_x      [B, 1+W]
+    z = R[:, :1] - R[:, 1:]                                  # [B, W]
+    loss = float(lam * np.sum(_neg_log_sigmoid(z)))
+    c = lam * _c_bpr(z).astype(U.dtype)
+    gR = np.concatenate([c.sum(1, keepdims=True), -c], 1)   # dL/dr_x
+    dS = gR[None] * Wt                                       # dL/ds_k through r
+    dE = gR[None] * Wt * (S - R[None])                       # softmax backward
+    if singles:
+        zs = S[:, :, :1] - S[:, :, 1:]                       # [K, B, W]
+        loss += float(np.sum(_neg_log_sigmoid(zs)))
+        cs = _c_bpr(zs).astype(U.dtype)
+        dS[:, :, 0] += cs.sum(2)
+        dS[:, :, 1:] -= cs
+    loss += float(reg * (_l2(Uu) + _l2(VX) + _l2(H)))
+    gX = dS[..., None] + dE[..., None] * H[:, None, None, :]  # dL/d(u o v_x)
+    GU, GV = np.zeros_like(U), np.zeros_like(V)
+    K = U.shape[0]
+    for k in range(K):
+        np.add.at(GU[k], u, (gX[k] * VX[k]).sum(1) + reg * Uu[k])
+        np.add.at(GV[k], X.reshape(-1), (gX[k] * Uu[k][:, None, :]).reshape(-1, U.shape[2])
+                  + reg * VX[k].reshape(-1, U.shape[2]))
+    GH = np.einsum("kbx,kbxd->kd", dE, P) + reg * H
+    lr = dt(lr)
+    for Xt, At, G in ((U, AU, GU), (V, AV, GV), (H, AH, GH)):
+        At += G * G
+        Xt -= lr * G / np.sqrt(At)
+    return loss
+
+
 def ens_predict(U, V, H, users):
     """ensemble.py:116-140: sum_k s_k exp(e_k) / sum_k exp(e_k) over all items."""
     Uu = U[:, np.asarray(users)]                     # [K, n, d]

@@ -124,3 +124,45 @@ def test_ensemble_train_loop(fold1):
     assert np.all(np.isfinite(scores))
     assert scores[0] > 0.05, scores
     en.close()
+
+
+@pytest.mark.parametrize("stream,K,d,lam,singles", [("rank_b100_w5", 5, 100, 1.0, False),
+                                                    ("rank_b100_w1", 2, 20, 1.0, False),
+                                                    ("rank_b100_w5", 3, 100, 0.1, True),
+                                                    ("rank_b50_w5", 8, 33, 0.5, True)])
+def test_ensemble_w_variants_match_oracle(streams, stream, K, d, lam, singles):
+    """ensemble_.py (singles off, lam 1) and ensemble__.py (members' BPR +
+    lam * ensemble) on the reference's captured sampler_ranking streams."""
+    st = get_stream(streams, stream)
+    e, U, V, H = make(K, 943, 1682, d, 0.1)
+    AU, AV, AH = (np.full_like(x, 0.1) for x in (U, V, H))
+    tot = 0.0
+    for s in range(8):
+        lg = e.step_w(st["pairs"][s], st["negs"][s], lam=lam, singles=singles)
+        lo = O.ens_w_step(U, V, H, AU, AV, AH, st["pairs"][s], st["negs"][s], 0.1, lam, singles)
+        assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
+        tot += lg
+    check_tables(e, U, V, H, AU, AV, AH)
+    assert abs(e.take_loss() - tot) <= 1e-6 * tot
+    e.close()
+
+
+@pytest.mark.parametrize("variant", ["ensemble_", "ensemble__"])
+def test_ensemble_w_drop_in_trains(fold1, variant):
+    import importlib
+    import scipy.sparse as sp
+    from collaborativefilteringusingtensorflow_amd.sampler_ranking import ExactSampler
+    mod = importlib.import_module("collaborativefilteringusingtensorflow_amd." + variant)
+    f = fold1
+    tra = sp.csr_matrix((np.ones(len(f["train_indices"])), f["train_indices"], f["train_indptr"]),
+                        shape=(943, 1682))
+    tst = sp.csr_matrix((np.ones(len(f["test_indices"])), f["test_indices"], f["test_indptr"]),
+                        shape=(943, 1682))
+    m = ['pre', 'recall', 'map', 'mrr', 'ndcg']
+    if variant == "ensemble_":
+        en = mod.Ensemble(943, 1682, 3, 10, 'cv', m, 0.1, 32, 100, max_iter=3, device=0, seed=2)
+    else:
+        en = mod.Ensemble(943, 1682, 3, 0.1, 10, 'cv', m, 0.1, 32, 100, max_iter=3, device=0, seed=2)
+    scores = en.train(1, tra, tst, ExactSampler(tra, n_neg=5, batch_size=100, seed=4))
+    assert np.all(np.isfinite(scores)) and scores[0] > 0.05, scores
+    en.close()

@@ -396,3 +396,68 @@ def test_c_oracle_multithread_matches_single(fold1, model, W, threads):
     assert abs(la - lb) <= 1e-5 * abs(la)
     for x, y in ((a.U, b.U), (a.V, b.V), (a.AU, b.AU), (a.AV, b.AV)):
         assert rel(y, x.astype(np.float64)) < 1e-5
+
+
+def literal_ens_w_loss(U, V, H, pairs, negs, reg, lam, singles):
+    """Torch transcription of ensemble_.py:58-118 (singles=False, lam=1) and
+    ensemble__.py:61-145 (singles=True): [B] positive ratings against [B, W]
+    negative ratings; ensemble__ adds each member's own BPR loss."""
+    p = torch.as_tensor(pairs, dtype=torch.long)
+    n = torch.as_tensor(negs, dtype=torch.long)
+    l2 = lambda x: 0.5 * (x * x).sum()
+    K = U.shape[0]
+    reg_loss = 0
+    for k in range(K):
+        reg_loss = reg_loss + l2(U[k][p[:, 0]]) + l2(V[k][p[:, 1]]) + l2(V[k][n])
+    reg_loss = reg_loss + l2(H)
+    parts, ai_base, aj_base = [], 0, 0
+    for k in range(K):
+        u, i, js = U[k][p[:, 0]], V[k][p[:, 1]], V[k][n]
+        ui = u * i
+        ujs = u[:, None, :] * js
+        ui_a = torch.exp(ui @ H[k][:, None]).sum(-1)                  # [B]
+        ujs_a = torch.exp((ujs * H[k][None, None, :]).sum(-1))        # [B, W]
+        parts.append((ui.sum(-1) * ui_a, ujs.sum(-1) * ujs_a))
+        ai_base, aj_base = ai_base + ui_a, aj_base + ujs_a
+    ui_r = sum(q[0] / ai_base for q in parts)
+    uj_r = sum(q[1] / aj_base for q in parts)
+    ens = (-torch.log(torch.sigmoid(ui_r[:, None] - uj_r))).sum()
+    if not singles:
+        return ens + reg * reg_loss
+    single = 0
+    for k in range(K):
+        u, i, js = U[k][p[:, 0]], V[k][p[:, 1]], V[k][n]
+        a = (u * i).sum(-1)
+        b = (u[:, None, :] * js).sum(-1)
+        single = single + (-torch.log(torch.sigmoid(a[:, None] - b))).sum()
+    return single + lam * ens + reg * reg_loss
+
+
+@pytest.mark.parametrize("K,W,reg,lam,singles", [(2, 5, 0.1, 1.0, False), (3, 1, 0.05, 1.0, False),
+                                                  (2, 5, 0.1, 0.1, True), (4, 3, 0.02, 0.5, True)])
+def test_ensemble_w_oracle_matches_literal_autograd(K, W, reg, lam, singles):
+    rng = np.random.RandomState(5 + K + W)
+    nu, ni, d, B = 50, 70, 8, 64
+    tabs = {"U": O.init_table(rng, (K, nu, d), dtype=np.float64),
+            "V": O.init_table(rng, (K, ni, d), dtype=np.float64),
+            "H": O.init_table(rng, (K, d), dtype=np.float64)}
+    ora = {k: v.copy() for k, v in tabs.items()}
+    oacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    tacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    for s in range(4):
+        pairs = np.stack([rng.randint(0, nu, B), rng.randint(0, ni, B)], 1)
+        negs = rng.randint(0, ni, (B, W))
+        negs[: B // 4, 0] = pairs[: B // 4, 1]                  # i among its own negatives
+        T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tabs.items()}
+        loss = literal_ens_w_loss(T["U"], T["V"], T["H"], pairs, negs, reg, lam, singles)
+        loss.backward()
+        for k, tt in T.items():
+            g = tt.grad.numpy()
+            tacc[k] = tacc[k] + g * g
+            tabs[k] = tt.detach().numpy() - 0.1 * g / np.sqrt(tacc[k])
+        lo = O.ens_w_step(ora["U"], ora["V"], ora["H"], oacc["U"], oacc["V"], oacc["H"], pairs, negs,
+                          reg, lam, singles)
+        assert abs(lo - float(loss.detach())) <= TOL * abs(float(loss.detach()))
+        for k in tabs:
+            assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
+            assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
