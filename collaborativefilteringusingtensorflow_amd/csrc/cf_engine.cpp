@@ -90,7 +90,8 @@ struct cf_engine {
     int hot_rep = 1;
     bool slots_ready = false;
     // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
-    // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches)
+    // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches);
+    // 2 = grad(s) + prep(s+1) fused, apply(s) alone
     int pipeline = 1;
 
     // batch: two buffer sets, so that the sampler of step s+1 runs on the side
@@ -168,6 +169,8 @@ struct cf_engine {
     // profiling
     bool prof = false;
     uint32_t prof_mask = 0xFFFFFFFFu;  // cf_set_option("profile_mask"): kernel ids timed
+    int prof_every = 1;                // cf_set_option("profile_every"): time every n-th launch
+    int64_t prof_seen[CF_K_COUNT] = {};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[CF_K_COUNT];
     std::vector<hipEvent_t> ev_pool;
 };
@@ -196,6 +199,7 @@ struct ProfScope {
     }
     ProfScope(cf_engine* e_, int k_, hipStream_t s_ = nullptr) : e(e_), k(k_), s(s_) {
         if (!e->prof || !((e->prof_mask >> k) & 1)) return;
+        if (e->prof_seen[k]++ % e->prof_every != 0) return;   // sampled launches only
         if (!s) s = e->stream;
         a = get(e);
         z = get(e);
@@ -517,11 +521,23 @@ int pending_clips(cf_engine* e) {
 
 int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
+    ApplyArgs p = apply_args(e, a, B, k, loss_acc);
+    if (next && e->pipeline == 2) {
+        // the draw + count of step s+1 rides in the gradient launch of step s
+        // (other buffer set), the duplicate apply runs alone
+        {
+            ProfScope ps(e, CF_K_GRAD_PREP);
+            CF_HIP(launch_grad(a, e->stream, next));
+        }
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+        if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
+        return pending_clips(e);
+    }
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
-    ApplyArgs p = apply_args(e, a, B, k, loss_acc);
     if (next) {
         ProfScope ps(e, CF_K_APPLY_PREP);
         CF_HIP(launch_apply_prep(p, *next, e->stream));
@@ -1478,12 +1494,17 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         e->prep_side = (int)value;
         return CF_OK;
     }
+    if (n == "profile_every") {
+        if (value < 1 || value > 1 << 20) return fail(CF_EINVAL, "profile_every must be >= 1");
+        e->prof_every = (int)value;
+        return CF_OK;
+    }
     if (n == "profile_mask") {
         e->prof_mask = (uint32_t)value;
         return CF_OK;
     }
     if (n == "pipeline") {
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "pipeline must be 0 or 1");
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "pipeline must be 0, 1 or 2");
         e->pipeline = (int)value;
         return CF_OK;
     }
@@ -1536,6 +1557,7 @@ int cf_profile_read(cf_engine* e, int32_t kid, double* total_ms, int64_t* launch
 int cf_profile_reset(cf_engine* e) {
     CF_TRY(check_engine(e));
     CF_HIP(hipStreamSynchronize(e->stream));
+    for (auto& n : e->prof_seen) n = 0;
     for (auto& v : e->ev) {
         for (auto& pr : v) {
             e->ev_pool.push_back(pr.first);

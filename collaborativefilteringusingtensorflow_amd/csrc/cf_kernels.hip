@@ -754,6 +754,14 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
 // so that the latency-bound draw fills the gaps of the gather.  np == 0 is the
 // plain gradient launch.
 __device__ __forceinline__ bool minor_block(int b, int nmajor, int nminor, int& idx) {
+#ifdef CF_GRAD_PREP_TAIL  // experiment: the draw blocks after every gradient block
+    if (b >= nmajor) {
+        idx = b - nmajor;
+        return true;
+    }
+    idx = b;
+    return false;
+#endif
     const int64_t tot = (int64_t)nmajor + nminor;
     const int lo = (int)(((int64_t)b * nminor) / tot);
     const int hi = (int)(((int64_t)(b + 1) * nminor) / tot);

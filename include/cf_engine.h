@@ -84,7 +84,7 @@ enum cf_kernel_id {
     CF_K_TOPK = 6,       /* masked per-user top-k                             */
     CF_K_SLOT = 7,       /* (retired: fixed per-row slot ranges need no pass)  */
     CF_K_APPLY_PREP = 8, /* apply of step s fused with the draw of step s+1    */
-    CF_K_GRAD_PREP = 9,  /* (retired pipeline 2)                               */
+    CF_K_GRAD_PREP = 9,  /* gradient of step s + draw of step s+1 (pipeline 2) */
     CF_K_APPLY_SLOT = 10,/* (retired pipeline 2)                               */
     CF_K_COUNT = 11
 };
@@ -323,11 +323,16 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                than the spread atomics save).
  *   "pipeline"   how cf_train_steps overlaps consecutive steps (same results):
  *                1 = the duplicate apply of step s with the draw + count of
- *                step s+1, two launches per step (default); 0 = one step at a
- *                time, three launches.
+ *                step s+1, two launches per step (default); 2 = the draw +
+ *                count of step s+1 inside step s's gradient launch, the apply
+ *                alone (measured 4.7 us/step slower at cfg2); 0 = one step at
+ *                a time, three launches.
  *   "profile_mask" bit k set = cf_profile_enable times kernel id k (default
  *                all): timing only the kernel of interest keeps the event
  *                pairs of the others out of a timed loop.
+ *   "profile_every" time only every n-th launch of each kernel id (default
+ *                1): an event pair per step costs the loop a few us, so a
+ *                timed loop samples its launches.
  */
 int cf_set_option(cf_engine* eng, const char* name, int64_t value);
 

@@ -44,8 +44,9 @@ TABLES = {"bpr": ("user", "item", "acc_user", "acc_item"),
 
 
 @pytest.mark.parametrize("opts", [{}, {"slot_max_user": 1}, {"pipeline": 0}, {"prep_stream": 1, "pipeline": 0},
-                                  {"slot_max": 2}],
-                         ids=["pipelined", "user-atomics", "stepwise", "side-stream", "slot2"])
+                                  {"slot_max": 2}, {"pipeline": 2}],
+                         ids=["pipelined", "user-atomics", "stepwise", "side-stream", "slot2",
+                              "draw-in-grad"])
 @pytest.mark.parametrize("model,d,W,G,B", [("bpr", 32, 1, 1, 100), ("bpr", 24, 5, 1, 250),
                                            ("gbpr", 16, 5, 1, 100), ("gbpr", 16, 2, 3, 100),
                                            ("cml", 20, 5, 1, 100), ("amf", 40, 5, 1, 100)])
