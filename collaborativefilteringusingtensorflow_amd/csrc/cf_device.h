@@ -78,6 +78,17 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+// SparseApplyAdagrad's step as TF1 computes it, grad * lr * rsqrt(accum)
+// (training_ops.cc ApplyAdagrad), with the hardware reciprocal square root
+// (1 ulp) instead of an IEEE divide + sqrt sequence
+__device__ __forceinline__ float adagrad_delta(float lr, float g, float acc) {
+    return g * lr * __builtin_amdgcn_rsqf(acc);
+}
+
+// 1 / (1 + e) with the hardware reciprocal (1 ulp): the logistic pieces of
+// the BPR loss and its derivative; e = inf gives 0 as the IEEE divide does
+__device__ __forceinline__ float rcp_1p(float e) { return __builtin_amdgcn_rcpf(1.f + e); }
+
 // Order-preserving map float -> uint32 (larger float => larger key).  Key 0
 // is reserved for "excluded" (train items under exclude_train).
 __device__ __forceinline__ uint32_t float_key(float f) {

@@ -182,7 +182,7 @@ __device__ __forceinline__ void gapply(float* __restrict__ X, float* __restrict_
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         acc[s] = fmaf(g[s], g[s], acc[s]);
-        x[s] = x0[s] - (lr * g[s]) / sqrtf(acc[s]);
+        x[s] = x0[s] - adagrad_delta(lr, g[s], acc[s]);
     }
     if (clip) {
         const float n = sqrtf(gdot<EPL>(x, x));
@@ -240,7 +240,7 @@ __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int co
     if (count == 1) {
         const float acc = fmaf(g, g, a.Ab[r]);
         a.Ab[r] = acc;
-        a.b[r] -= (a.lr * g) / sqrtf(acc);
+        a.b[r] -= adagrad_delta(a.lr, g, acc);
     } else {
         unsafeAtomicAdd(a.Gb + r, g);
     }
@@ -248,7 +248,7 @@ __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int co
 
 __device__ __forceinline__ float neg_log_sigmoid(float x) {
     // literal -log(sigmoid(x)) as in bprmf.py:70 / gbprmf.py:88
-    return -logf(1.f / (1.f + expf(-x)));
+    return -logf(rcp_1p(expf(-x)));
 }
 
 __device__ __forceinline__ float softplus(float x) {
@@ -507,7 +507,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             for (int w = 0; w < W; ++w) {
                 const int sl = J.get(a, p, w, gl);
                 const float x = ui - gdot<EPL>(uu, J.v[sl]);
-                float c = -1.f / (1.f + expf(x));
+                float c = -rcp_1p(expf(x));
                 if (MODEL == AMF) {
                     loss_g += softplus(-x);
                     if (a.adversarial) {
@@ -568,7 +568,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 const int j = J.j[sl];
                 const float bj = a.b[j];
                 const float x = ui - (gdot<EPL>(uu, J.v[sl]) + bj);
-                const float c = -1.f / (1.f + expf(x));
+                const float c = -rcp_1p(expf(x));
                 loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj * bj;
                 sc += c;
                 float gj[EPL];
@@ -630,7 +630,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             auto term = [&](int xa, int xb, float coef, float wt) {
                 const float z = coef * (sx[xa] - sx[xb]);
                 loss_g += wt * neg_log_sigmoid(z);
-                const float g = wt * coef * (-1.f / (1.f + expf(z)));
+                const float g = wt * coef * (-rcp_1p(expf(z)));
                 ds[xa] += g;
                 ds[xb] -= g;
             };
@@ -812,7 +812,7 @@ __device__ __forceinline__ void gapply_pre(float* __restrict__ X, float* __restr
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         acc[s] = fmaf(g[s], g[s], acc0[s]);
-        x[s] = x0[s] - (lr * g[s]) / sqrtf(acc[s]);
+        x[s] = x0[s] - adagrad_delta(lr, g[s], acc[s]);
     }
     if (clip) {
         const float n = sqrtf(gdot<EPL>(x, x));
@@ -921,7 +921,7 @@ struct PairRows {
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 const float x = ui - gdot<EPL>(uu, vj[w]);
-                float c = -1.f / (1.f + expf(x));
+                float c = -rcp_1p(expf(x));
                 if (MODEL == AMF) {
                     loss_g += softplus(-x);
                     if (a.adversarial) {
@@ -964,7 +964,7 @@ struct PairRows {
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 const float x = ui - (gdot<EPL>(uu, vj[w]) + bj[w]);
-                const float c = -1.f / (1.f + expf(x));
+                const float c = -rcp_1p(expf(x));
                 loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj[w] * bj[w];
                 sc += c;
                 float gj[EPL];
@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
             const float gb = a.Gb[r];
             const float ab = fmaf(gb, gb, a.Ab[r]);
             a.Ab[r] = ab;
-            a.b[r] -= (a.lr * gb) / sqrtf(ab);
+            a.b[r] -= adagrad_delta(a.lr, gb, ab);
             a.Gb[r] = 0.f;
         }
     }
@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
             if (g != 0.f) {
                 const float acc = fmaf(g, g, a.Ab[r]);
                 a.Ab[r] = acc;
-                a.b[r] -= (a.lr * g) / sqrtf(acc);
+                a.b[r] -= adagrad_delta(a.lr, g, acc);
                 a.Gb[r] = 0.f;
             }
         }
