@@ -523,6 +523,7 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
     ApplyArgs p = apply_args(e, a, B, k, loss_acc);
     if (next && e->pipeline == 2) {
+        p.n_partial = grad_blocks(a, true);   // the launch with draw blocks keeps 256-lane groups
         // the draw + count of step s+1 rides in the gradient launch of step s
         // (other buffer set), the duplicate apply runs alone
         {

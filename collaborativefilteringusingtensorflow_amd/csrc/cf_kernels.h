@@ -206,7 +206,7 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + cou
 // draws and counts the next step's batch (other buffer set)
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
 // blocks (= loss partials) of the grad launch for this step shape
-int grad_blocks(const StepArgs& a);
+int grad_blocks(const StepArgs& a, bool with_draw = false);
 int grad_blocks_max(int B);  // upper bound over every grad variant
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 // apply of step s and prep of step s+1 in one launch (device-sampler pipeline)

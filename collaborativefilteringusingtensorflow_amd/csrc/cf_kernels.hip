@@ -1057,9 +1057,9 @@ struct PairRows {
     }
 };
 
-template <int MODEL, int EPL, int WT, int P>
+template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock>
 __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
-    __shared__ double s_loss[kGroupsPerBlock];
+    __shared__ double s_loss[GPB];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
     float loss_g = 0.f;
@@ -1069,7 +1069,7 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     bool ok[P];
 #pragma unroll
     for (int k = 0; k < P; ++k) {
-        pp[k] = (block * P + k) * kGroupsPerBlock + grp;
+        pp[k] = (block * P + k) * GPB + grp;
         ok[k] = pp[k] < a.B;
     }
 #pragma unroll
@@ -1092,7 +1092,7 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     if (threadIdx.x == 0) {
         double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[k];
+        for (int k = 0; k < GPB; ++k) t += s_loss[k];
         a.loss_partial[block] = t;
     }
 }
@@ -1109,6 +1109,14 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
         prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
         grad_fast_body<MODEL, EPL, WT, P>(a, idx);
+}
+
+// the same gradient blocks at one wave per workgroup (no draw blocks): a
+// finer dispatch granule, so the last round of workgroups leaves less of the
+// chip idle (a step's gradient launch is only ~2.7 rounds of 256-lane blocks)
+template <int MODEL, int EPL, int WT, int P>
+__global__ __launch_bounds__(kWave) void grad_fast_wave_kernel(StepArgs a) {
+    grad_fast_body<MODEL, EPL, WT, P, kWave / kGL>(a, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1184,6 +1192,12 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     }
 }
 
+#ifndef CF_APPLY_DETECT_WAVES
+#define CF_APPLY_DETECT_WAVES 1   // 4 measured slower: ~46 owners per block, ~3 per group in series
+#endif
+// waves of an apply block that find owners (64 work items each)
+constexpr int kApplyDetectWaves = CF_APPLY_DETECT_WAVES;
+
 template <int EPL>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     __shared__ double s_red[kWavesPerBlock];
@@ -1191,27 +1205,38 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
     const int wv = threadIdx.x >> 6;
     const int gl = lane & (kGL - 1);
     if (block == 0 && a.loss_acc != nullptr) {
+        // fixed order; eight partials in flight per lane, not a chain of loads
         double t = 0.0;
-        for (int k = threadIdx.x; k < a.n_partial; k += kBlock) t += a.loss_partial[k];
+        for (int k0 = threadIdx.x; k0 < a.n_partial; k0 += 8 * kBlock) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int k = k0 + q * kBlock;
+                v[q] = k < a.n_partial ? a.loss_partial[k] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t += v[q];
+        }
         t = wave_sum_d(t);
         if (lane == 0) s_red[wv] = t;
         __syncthreads();
         if (threadIdx.x == 0) a.loss_acc[0] += (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
     }
-    // a block takes 64 work items at a time: wave 0 finds their owners (~18 %
-    // of the occurrences at cfg2), then the block's 16 groups apply them --
-    // about one row per group per chunk, so a row's dependent loads are not
-    // queued behind other rows'
-    __shared__ unsigned long long s_mask;
-    __shared__ int64_t s_row[kWave];
-    __shared__ int s_isU[kWave];
-    __shared__ int s_cnt[kWave];   // the owner's count, read once in the check
+    // a block takes kApplyDetectWaves x 64 work items at a time: those waves
+    // find their owners (~18 % of the occurrences at cfg2), then the block's
+    // 16 groups apply them round-robin
+    constexpr int NW = kApplyDetectWaves;
+    __shared__ unsigned long long s_mask[NW];
+    __shared__ int64_t s_row[NW * kWave];
+    __shared__ int s_isU[NW * kWave];
+    __shared__ int s_cnt[NW * kWave];   // the owner's count, read once in the check
     const int64_t nU = a.count_users ? a.nU : 0, nV = a.count_items ? a.nV : 0;
     const int64_t total = nU + nV + a.nS;
     const int group = threadIdx.x >> 4;
-    for (int64_t base = (int64_t)block * kWave; base < total; base += (int64_t)nblocks * kWave) {
-        if (wv == 0) {
-            const int64_t q = base + lane;
+    constexpr int64_t chunk = (int64_t)NW * kWave;
+    for (int64_t base = (int64_t)block * chunk; base < total; base += (int64_t)nblocks * chunk) {
+        if (wv < NW) {
+            const int64_t q = base + wv * kWave + lane;
             int64_t row = -1;
             int isU = 0, c = 0;
             if (q < nU) {
@@ -1239,19 +1264,28 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 }
             }
             const unsigned long long m = __ballot(row >= 0);
-            s_row[lane] = row;
-            s_isU[lane] = isU;
-            s_cnt[lane] = c;
-            if (lane == 0) s_mask = m;
+            s_row[wv * kWave + lane] = row;
+            s_isU[wv * kWave + lane] = isU;
+            s_cnt[wv * kWave + lane] = c;
+            if (lane == 0) s_mask[wv] = m;
         }
         __syncthreads();
-        unsigned long long m = s_mask;
-        // group g applies the owners of rank g, g + 16, ... among the set bits
-        for (int k = 0; k < group && m != 0ull; ++k) m &= m - 1ull;
-        while (m != 0ull) {  // group-uniform
-            const int src = __ffsll((long long)m) - 1;
+        // owners in (wave, lane) order; group g applies owners g, g + 16, ...
+        // -- the four groups of a wave take four different owners at once
+        for (int t = group;; t += kGroupsPerBlock) {
+            int rem = t, src = -1;
+            for (int w = 0; w < NW; ++w) {
+                unsigned long long m = s_mask[w];
+                const int c = __popcll(m);
+                if (rem < c) {
+                    for (int q = 0; q < rem; ++q) m &= m - 1ull;
+                    src = w * kWave + __ffsll((long long)m) - 1;
+                    break;
+                }
+                rem -= c;
+            }
+            if (src < 0) break;  // group-uniform
             apply_row<EPL>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
-            for (int k = 0; k < kGroupsPerBlock && m != 0ull; ++k) m &= m - 1ull;
         }
         __syncthreads();  // s_* reused by the next chunk
     }
@@ -1521,15 +1555,22 @@ static int fast_w(const StepArgs& a) {
     return ok && (a.W == 1 || a.W == 5) ? a.W : 0;
 }
 
-int grad_blocks(const StepArgs& a) {
+#ifndef CF_GRAD_WAVE_BLOCKS
+// 1: fast path without draw blocks in one-wave workgroups (measured no faster
+// at cfg2: 43.9 vs 44.2 us), 0: 256-lane workgroups
+#define CF_GRAD_WAVE_BLOCKS 0
+#endif
+
+int grad_blocks(const StepArgs& a, bool with_draw) {
     const int fw = fast_w(a);
     const int B = a.B;
-    const int ppb = fw == 1 ? CF_FAST_PAIRS_W1 * kGroupsPerBlock
-                  : fw == 5 ? CF_FAST_PAIRS_W5 * kGroupsPerBlock : kPairsPerBlock;
+    const int gpb = (CF_GRAD_WAVE_BLOCKS && !with_draw) ? kWave / kGL : kGroupsPerBlock;
+    const int ppb = fw == 1 ? CF_FAST_PAIRS_W1 * gpb
+                  : fw == 5 ? CF_FAST_PAIRS_W5 * gpb : kPairsPerBlock;
     return (B + ppb - 1) / ppb;
 }
 
-int grad_blocks_max(int B) { return (B + kGroupsPerBlock - 1) / kGroupsPerBlock; }
+int grad_blocks_max(int B) { return (B + kWave / kGL - 1) / (kWave / kGL); }
 
 hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
@@ -1562,6 +1603,18 @@ static hipError_t launch_grad_w(const StepArgs& a, const StepArgs* nx, hipStream
 
 template <int MODEL, int WT, int P>
 static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
+    if (CF_GRAD_WAVE_BLOCKS && prep_blocks(nx) == 0) {
+        // the grid must match grad_blocks(): P * 4 pairs per one-wave block
+        constexpr int gpb = kWave / kGL;
+        const dim3 grid((a.B + P * gpb - 1) / (P * gpb)), block(kWave);
+        switch (epl_for(a.d)) {
+            case 1: hipLaunchKernelGGL((grad_fast_wave_kernel<MODEL, 1, WT, P>), grid, block, 0, s, a); break;
+            case 2: hipLaunchKernelGGL((grad_fast_wave_kernel<MODEL, 2, WT, P>), grid, block, 0, s, a); break;
+            case 4: hipLaunchKernelGGL((grad_fast_wave_kernel<MODEL, 4, WT, P>), grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL((grad_fast_wave_kernel<MODEL, 8, WT, P>), grid, block, 0, s, a); break;
+        }
+        return hipGetLastError();
+    }
     // the grid must match grad_blocks(): P * kGroupsPerBlock pairs per block
     const int ng = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock), np = prep_blocks(nx);
     const StepArgs n = nx ? *nx : a;
@@ -1608,9 +1661,11 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
 }
 
 static int apply_grid(const ApplyArgs& a) {
-    // 64 work items (user occurrences, item occurrences, served rows) per block
+    // 64 work items (user occurrences, item occurrences, served rows) per
+    // detecting wave
     const int64_t items = (a.count_users ? a.nU : 0) + (a.count_items ? a.nV : 0) + a.nS;
-    int64_t blocks = (items + kWave - 1) / kWave;
+    const int64_t per = (int64_t)kApplyDetectWaves * kWave;
+    int64_t blocks = (items + per - 1) / per;
     if (blocks > 4096) blocks = 4096;  // grid-stride over the work items
     if (blocks < 1) blocks = 1;        // block 0 still reduces the loss
     return (int)blocks;
