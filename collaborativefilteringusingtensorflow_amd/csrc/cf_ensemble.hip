@@ -612,6 +612,8 @@ int cf_ens_set_interactions(cf_ensemble* e, const int64_t* indptr, const int32_t
 
 int cf_ens_step(cf_ensemble* e, const int32_t* uij, int32_t B, double* loss_out) {
     if (!e || !uij || B < 1) return cfi::set_error(CF_EINVAL, "bad arguments");
+    // the reference loss is B x B (ensemble.py:84-91): 64 x 64 tiles over it
+    if (B > (1 << 16)) return cfi::set_error(CF_EINVAL, "B must be <= 65536 (the loss is B x B)");
     for (int p = 0; p < B; ++p)
         if (uij[3 * p] < 0 || uij[3 * p] >= e->n_users || uij[3 * p + 1] < 0 ||
             uij[3 * p + 1] >= e->n_items || uij[3 * p + 2] < 0 || uij[3 * p + 2] >= e->n_items)
