@@ -111,6 +111,10 @@ SIGNATURES = {
     "cf_mt_sampler_next": (ctypes.c_int, [_P, _PI32, _PI32, _PI32]),
     "cf_mt_sampler_state": (ctypes.c_int, [_P, _PI64, _PI64]),
     "cf_mt_sampler_free": (ctypes.c_int, [_P]),
+    "cf_tuple_sampler_create": (ctypes.c_int, [_I32, _PI64, _PI32, _I64, _I64, _PI64, _PI32, _PD,
+                                                _I32, ctypes.c_uint32, ctypes.POINTER(_P)]),
+    "cf_tuple_sampler_next": (ctypes.c_int, [_P, _PI32, _PF]),
+    "cf_tuple_sampler_free": (ctypes.c_int, [_P]),
     "cf_ens_create": (ctypes.c_int, [_I64, _I64, _I32, _I32, _F, _F, _F, _I32, ctypes.POINTER(_P)]),
     "cf_ens_destroy": (ctypes.c_int, [_P]),
     "cf_ens_init_params": (ctypes.c_int, [_P, _F, _F, _I32, _U64]),

@@ -16,8 +16,13 @@ the engine's ``cf_step_plr``; the optimizer step itself is the gfx950 kernel.
   stored entries (cplr_u.py:194-197).
 * ``PRIGPSampler`` / ``UITJSampler``: the producer loops of
   src/samplers/sampler_prigp.py:24-52 and sampler_uitj_ranking.py:22-38 on a
-  seedable RandomState, without the thread and queue.
+  seedable RandomState, without the thread and queue -- run natively
+  (``cf_tuple_sampler_*``, csrc/cf_mt_sampler.cpp) on the same legacy MT19937
+  stream; ``native=False`` keeps the Python loops (same batches, ~50x slower).
 """
+import ctypes
+import os
+
 import numpy as np
 import scipy.sparse as sp
 
@@ -79,11 +84,66 @@ def normalise_rows(C):
     return sp.lil_matrix(C)
 
 
+class _NativeTupleSampler(object):
+    """cf_tuple_sampler over the train and coefficient CSRs."""
+
+    def __init__(self, kind, trasR, coefMat, batch_size, seed):
+        from . import _native as N
+        self._N = N
+        self._L = N.lib()
+        self.kind, self.batch_size = int(kind), int(batch_size)
+        R = sp.csr_matrix(trasR)
+        R.sort_indices()
+        C = sp.csr_matrix(coefMat, dtype=np.float64)
+        C.sort_indices()
+        self.n_users, self.n_items = R.shape
+        ip = np.ascontiguousarray(R.indptr, np.int64)
+        ix = np.ascontiguousarray(R.indices, np.int32)
+        cp = np.ascontiguousarray(C.indptr, np.int64)
+        cx = np.ascontiguousarray(C.indices, np.int32)
+        cv = np.ascontiguousarray(C.data, np.float64)
+        if seed is None:
+            seed = int.from_bytes(os.urandom(4), "little")
+        self._h = ctypes.c_void_p()
+        P = ctypes.POINTER
+        N.check(self._L.cf_tuple_sampler_create(
+            self.kind, ip.ctypes.data_as(P(ctypes.c_int64)), ix.ctypes.data_as(P(ctypes.c_int32)),
+            self.n_users, self.n_items, cp.ctypes.data_as(P(ctypes.c_int64)),
+            cx.ctypes.data_as(P(ctypes.c_int32)), cv.ctypes.data_as(P(ctypes.c_double)),
+            self.batch_size, int(seed) & 0xFFFFFFFF, ctypes.byref(self._h)), "cf_tuple_sampler_create")
+
+    def _draw(self):
+        B = self.batch_size
+        t = np.empty((B, 5 if self.kind == 0 else 4), np.int32)
+        c = np.empty((B, 2), np.float32) if self.kind == 1 else None
+        self._N.check(self._L.cf_tuple_sampler_next(
+            self._h, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            c.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) if c is not None else None),
+            "cf_tuple_sampler_next")
+        return t, c
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._L.cf_tuple_sampler_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class PRIGPSampler(object):
     """sampler_prigp.py: (u, i, j, t, k) tuples; t, k drawn from the user's
     coefficient items (the more-coefficient item first)."""
 
-    def __init__(self, trasR, coefMat, batch_size=100, seed=None):
+    def __new__(cls, trasR, coefMat, batch_size=100, seed=None, native=True):
+        if native and cls is PRIGPSampler:
+            return _NativePRIGP(trasR, coefMat, batch_size, seed)
+        return super(PRIGPSampler, cls).__new__(cls)
+
+    def __init__(self, trasR, coefMat, batch_size=100, seed=None, native=False):
         self.batch_size = int(batch_size)
         self.n_users, self.n_items = trasR.shape
         self.rng = np.random.RandomState(seed)
@@ -130,10 +190,23 @@ class PRIGPSampler(object):
         return batch
 
 
+class _NativePRIGP(_NativeTupleSampler):
+    def __init__(self, trasR, coefMat, batch_size=100, seed=None):
+        super(_NativePRIGP, self).__init__(0, trasR, coefMat, batch_size, seed)
+
+    def next_batch(self):
+        return self._draw()[0].astype(np.int64)
+
+
 class UITJSampler(object):
     """sampler_uitj_ranking.py: (u, i, t, j) tuples and (coef[u,i], coef[u,t])."""
 
-    def __init__(self, trasR, coefMat, batch_size=100, seed=None):
+    def __new__(cls, trasR, coefMat, batch_size=100, seed=None, native=True):
+        if native and cls is UITJSampler:
+            return _NativeUITJ(trasR, coefMat, batch_size, seed)
+        return super(UITJSampler, cls).__new__(cls)
+
+    def __init__(self, trasR, coefMat, batch_size=100, seed=None, native=False):
         self.batch_size = int(batch_size)
         self.n_users, self.n_items = trasR.shape
         self.rng = np.random.RandomState(seed)
@@ -166,3 +239,12 @@ class UITJSampler(object):
             out[r] = (u, i, t, j)
             coefs[r] = (self.coef[u].get(i, 0.0), self.coef[u].get(t, 0.0))
         return out, coefs
+
+
+class _NativeUITJ(_NativeTupleSampler):
+    def __init__(self, trasR, coefMat, batch_size=100, seed=None):
+        super(_NativeUITJ, self).__init__(1, trasR, coefMat, batch_size, seed)
+
+    def next_batch(self):
+        t, c = self._draw()
+        return t.astype(np.int64), c.astype(np.float64)

@@ -23,6 +23,7 @@
 // reference's queue is not reproduced: this is the stream the
 // producer computed.
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -240,6 +241,217 @@ int cf_mt_sampler_state(const cf_mt_sampler* s, int64_t* epoch_out, int64_t* bat
 }
 
 int cf_mt_sampler_free(cf_mt_sampler* s) {
+    delete s;
+    return CF_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Tuple samplers of the PRIGP / CPLR drop-ins (_tuple.py PRIGPSampler /
+// UITJSampler, which restate src/samplers/sampler_prigp.py:24-52 and
+// sampler_uitj_ranking.py:22-38 on a seeded RandomState): the same draws in
+// the same order on the same legacy MT19937 stream, so a native sampler and
+// its Python restatement yield identical batches for one seed.  The Python
+// loops bound the tuple models' drivers at ~0.2M tuples/s; these run the
+// identical stream natively.
+// ---------------------------------------------------------------------------
+namespace {
+
+// legacy RandomState.random_sample(): 53-bit double from two 32-bit draws
+double legacy_double(MT19937& g) {
+    const int32_t a = (int32_t)(g.next32() >> 5), b = (int32_t)(g.next32() >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+}  // namespace
+
+struct cf_tuple_sampler {
+    int kind = 0;  // 0 PRIGP (u,i,j,t,k), 1 CPLR (u,i,t,j) + coefs
+    int64_t n_users = 0, n_items = 0;
+    int B = 1;
+    std::vector<int64_t> indptr, cindptr, utptr;
+    std::vector<int32_t> indices, cindices, ut;    // train rows, coefficient rows, coef-only items
+    std::vector<double> cvalues;
+    std::vector<int32_t> nvals;                     // distinct coefficient values per user
+    std::vector<uint8_t> valid;                     // CPLR: user can be drawn
+    std::vector<int32_t> pairs;
+    int64_t nnz = 0, per_epoch = 0, batch = 0;
+    MT19937 g;
+    bool has_gauss = false;
+    double gauss = 0.0;
+
+    static bool in(const std::vector<int32_t>& v, int64_t b, int64_t e, int32_t x) {
+        return std::binary_search(v.begin() + b, v.begin() + e, x);
+    }
+    double randn() {  // legacy_gauss: polar Box-Muller, second value cached
+        if (has_gauss) {
+            has_gauss = false;
+            return gauss;
+        }
+        double x1, x2, r2;
+        do {
+            x1 = 2.0 * legacy_double(g) - 1.0;
+            x2 = 2.0 * legacy_double(g) - 1.0;
+            r2 = x1 * x1 + x2 * x2;
+        } while (r2 >= 1.0 || r2 == 0.0);
+        const double f = std::sqrt(-2.0 * std::log(r2) / r2);
+        gauss = f * x1;
+        has_gauss = true;
+        return f * x2;
+    }
+    double coef(int64_t u, int32_t x) const {
+        const auto b = cindices.begin() + cindptr[(size_t)u], e = cindices.begin() + cindptr[(size_t)u + 1];
+        const auto it = std::lower_bound(b, e, x);
+        return (it != e && *it == x) ? cvalues[(size_t)(it - cindices.begin())] : 0.0;
+    }
+};
+
+extern "C" {
+
+int cf_tuple_sampler_create(int32_t kind, const int64_t* indptr, const int32_t* indices,
+                            int64_t n_users, int64_t n_items, const int64_t* coef_indptr,
+                            const int32_t* coef_indices, const double* coef_values,
+                            int32_t batch_size, uint32_t seed, cf_tuple_sampler** out) {
+    if (!out || !indptr || !coef_indptr || n_users < 1 || n_items < 2 || kind < 0 || kind > 1 ||
+        batch_size < 1)
+        return cfi::set_error(CF_EINVAL, "bad arguments");
+    const int64_t nnz = indptr[n_users], cnnz = coef_indptr[n_users];
+    if (nnz < 1 || !indices || (cnnz > 0 && (!coef_indices || !coef_values)))
+        return cfi::set_error(CF_EINVAL, "no interactions / coefficients");
+    for (int pass = 0; pass < 2; ++pass) {
+        const int64_t* ip = pass ? coef_indptr : indptr;
+        const int32_t* ix = pass ? coef_indices : indices;
+        for (int64_t u = 0; u < n_users; ++u) {
+            if (ip[u + 1] < ip[u]) return cfi::set_error(CF_EINVAL, "indptr not monotone");
+            for (int64_t k = ip[u]; k < ip[u + 1]; ++k)
+                if (ix[k] < 0 || ix[k] >= n_items || (k > ip[u] && ix[k - 1] >= ix[k]))
+                    return cfi::set_error(CF_EINVAL, "CSR rows must hold sorted, unique, in-range ids");
+        }
+    }
+    cf_tuple_sampler* s = new cf_tuple_sampler();
+    s->kind = kind;
+    s->n_users = n_users;
+    s->n_items = n_items;
+    s->B = batch_size;
+    s->nnz = nnz;
+    s->indptr.assign(indptr, indptr + n_users + 1);
+    s->indices.assign(indices, indices + nnz);
+    s->cindptr.assign(coef_indptr, coef_indptr + n_users + 1);
+    s->cindices.assign(coef_indices, coef_indices + cnnz);
+    s->cvalues.assign(coef_values, coef_values + cnnz);
+    s->nvals.assign((size_t)n_users, 0);
+    for (int64_t u = 0; u < n_users; ++u) {  // len(set(values of row u))
+        std::vector<double> v(coef_values + coef_indptr[u], coef_values + coef_indptr[u + 1]);
+        std::sort(v.begin(), v.end());
+        s->nvals[(size_t)u] = (int32_t)(std::unique(v.begin(), v.end()) - v.begin());
+    }
+    if (kind == 0) {
+        if (batch_size > nnz) {
+            delete s;
+            return cfi::set_error(CF_EINVAL, "batch size exceeds the number of interactions");
+        }
+        s->per_epoch = nnz / batch_size;
+        s->pairs.resize((size_t)(2 * nnz));   // np.array(R.nonzero()).T
+        for (int64_t u = 0; u < n_users; ++u)
+            for (int64_t k = indptr[u]; k < indptr[u + 1]; ++k) {
+                s->pairs[(size_t)(2 * k)] = (int32_t)u;
+                s->pairs[(size_t)(2 * k + 1)] = indices[k];
+            }
+        s->batch = s->per_epoch;  // the first next() shuffles
+    } else {
+        // ut[u] = sorted(coef items of u that are not train items of u)
+        s->utptr.assign((size_t)n_users + 1, 0);
+        s->valid.assign((size_t)n_users, 0);
+        bool any = false;
+        for (int64_t u = 0; u < n_users; ++u) {
+            for (int64_t k = coef_indptr[u]; k < coef_indptr[u + 1]; ++k)
+                if (!cf_tuple_sampler::in(s->indices, indptr[u], indptr[u + 1], coef_indices[k]))
+                    s->ut.push_back(coef_indices[k]);
+            s->utptr[(size_t)u + 1] = (int64_t)s->ut.size();
+            const int64_t nui = indptr[u + 1] - indptr[u], nut = s->utptr[u + 1] - s->utptr[u];
+            s->valid[(size_t)u] = nui > 0 && nut > 0 && nui + nut < n_items;
+            any = any || s->valid[(size_t)u];
+        }
+        if (!any) {
+            delete s;
+            return cfi::set_error(CF_EINVAL, "no user has both train and coefficient-only items");
+        }
+    }
+    s->g.seed(seed);
+    *out = s;
+    return CF_OK;
+}
+
+int cf_tuple_sampler_next(cf_tuple_sampler* s, int32_t* tuples, float* coefs) {
+    if (!s || !tuples || (s->kind == 1 && !coefs)) return cfi::set_error(CF_EINVAL, "bad arguments");
+    const int B = s->B;
+    MT19937& g = s->g;
+    const int64_t ni = s->n_items;
+    if (s->kind == 0) {  // PRIGPSampler.next_batch
+        if (s->batch >= s->per_epoch) {
+            for (int64_t i = s->nnz - 1; i >= 1; --i) {  // rng.shuffle(self.pairs)
+                const int64_t j = (int64_t)random_interval(g, (uint64_t)i);
+                if (i == j) continue;
+                std::swap(s->pairs[(size_t)(2 * i)], s->pairs[(size_t)(2 * j)]);
+                std::swap(s->pairs[(size_t)(2 * i + 1)], s->pairs[(size_t)(2 * j + 1)]);
+            }
+            s->batch = 0;
+        }
+        const int32_t* src = s->pairs.data() + (size_t)(2 * s->batch * (int64_t)B);
+        for (int p = 0; p < B; ++p) {
+            tuples[5 * p] = src[2 * p];
+            tuples[5 * p + 1] = src[2 * p + 1];
+        }
+        for (int p = 0; p < B; ++p) tuples[5 * p + 2] = (int32_t)randint(g, 0, ni);  // randint(0, n, B)
+        s->batch += 1;
+        for (int p = 0; p < B; ++p) {
+            const int64_t u = tuples[5 * p];
+            const int32_t i = tuples[5 * p + 1];
+            int32_t j = tuples[5 * p + 2];
+            while (cf_tuple_sampler::in(s->indices, s->indptr[u], s->indptr[u + 1], j))
+                j = (int32_t)randint(g, 0, ni);
+            int32_t t = i, k = j;
+            const int64_t cb = s->cindptr[(size_t)u], ce = s->cindptr[(size_t)u + 1];
+            const int nv = s->nvals[(size_t)u];
+            if (nv > 0) {
+                const int64_t len = ce - cb;
+                t = s->cindices[(size_t)(cb + randint(g, 0, len))];
+                k = (int32_t)randint(g, 0, ni);
+                while (cf_tuple_sampler::in(s->cindices, cb, ce, k)) k = (int32_t)randint(g, 0, ni);
+                if (nv > 1 && s->randn() < (double)len / (double)ni) {
+                    k = s->cindices[(size_t)(cb + randint(g, 0, len))];
+                    while (s->coef(u, t) == s->coef(u, k)) k = s->cindices[(size_t)(cb + randint(g, 0, len))];
+                    if (s->coef(u, t) < s->coef(u, k)) std::swap(t, k);
+                }
+            }
+            tuples[5 * p + 2] = j;
+            tuples[5 * p + 3] = t;
+            tuples[5 * p + 4] = k;
+        }
+        return CF_OK;
+    }
+    for (int p = 0; p < B; ++p) {  // UITJSampler.next_batch
+        int64_t u = randint(g, 0, s->n_users);
+        while (!s->valid[(size_t)u]) u = randint(g, 0, s->n_users);
+        const int64_t ib = s->indptr[(size_t)u], ie = s->indptr[(size_t)u + 1];
+        const int64_t tb = s->utptr[(size_t)u], te = s->utptr[(size_t)u + 1];
+        const int32_t i = s->indices[(size_t)(ib + randint(g, 0, ie - ib))];
+        const int32_t t = s->ut[(size_t)(tb + randint(g, 0, te - tb))];
+        int32_t j = (int32_t)randint(g, 0, ni);
+        while (cf_tuple_sampler::in(s->indices, ib, ie, j) || cf_tuple_sampler::in(s->ut, tb, te, j))
+            j = (int32_t)randint(g, 0, ni);
+        tuples[4 * p] = (int32_t)u;
+        tuples[4 * p + 1] = i;
+        tuples[4 * p + 2] = t;
+        tuples[4 * p + 3] = j;
+        coefs[2 * p] = (float)s->coef(u, i);
+        coefs[2 * p + 1] = (float)s->coef(u, t);
+    }
+    return CF_OK;
+}
+
+int cf_tuple_sampler_free(cf_tuple_sampler* s) {
     delete s;
     return CF_OK;
 }

@@ -373,6 +373,20 @@ int cf_mt_sampler_next(cf_mt_sampler* s, int32_t* pairs /*[B,2]*/, int32_t* negs
 int cf_mt_sampler_state(const cf_mt_sampler* s, int64_t* epoch_out, int64_t* batch_out);
 int cf_mt_sampler_free(cf_mt_sampler* s);
 
+/* ---- tuple samplers of the PRIGP / CPLR drop-ins (host) ------------------------
+ * kind 0: PRIGP (u,i,j,t,k) tuples [B,5] (sampler_prigp.py:24-52); kind 1:
+ * CPLR (u,i,t,j) tuples [B,4] + coefs [B,2] (sampler_uitj_ranking.py:22-38).
+ * Train CSR (sorted rows) + coefficient CSR (sorted rows, float64 values).
+ * The same draws, in the same order, on the same legacy MT19937 stream as
+ * the Python restatements in _tuple.py for RandomState(seed). */
+typedef struct cf_tuple_sampler cf_tuple_sampler;
+int cf_tuple_sampler_create(int32_t kind, const int64_t* indptr, const int32_t* indices,
+                            int64_t n_users, int64_t n_items, const int64_t* coef_indptr,
+                            const int32_t* coef_indices, const double* coef_values,
+                            int32_t batch_size, uint32_t seed, cf_tuple_sampler** out);
+int cf_tuple_sampler_next(cf_tuple_sampler* s, int32_t* tuples, float* coefs /* CPLR | NULL */);
+int cf_tuple_sampler_free(cf_tuple_sampler* s);
+
 /* ---- attention-weighted MF ensemble ----------------------
  * src/models/pl/models/ensemble.py: K members U[K,n_users,d], V[K,n_items,d],
  * H[K,d] (all truncated-normal), trained on sampler_uij_ranking (u,i,j)

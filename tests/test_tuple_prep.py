@@ -76,11 +76,12 @@ def test_tuple_preprocessing_matches_literal_reference(cplr, topK):
         np.testing.assert_allclose(T.normalise_rows(C).toarray(), Cn_ref.toarray(), rtol=1e-12)
 
 
-def test_prigp_sampler_invariants():
+@pytest.mark.parametrize("native", [True, False])
+def test_prigp_sampler_invariants(native):
     R = random_R(5)
     S = T.top_k_rows(T.user_similarity(R), 5)
     C = T.coefficients(S, R, weighted=False)
-    s = T.PRIGPSampler(R, C, batch_size=50, seed=3)
+    s = T.PRIGPSampler(R, C, batch_size=50, seed=3, native=native)
     Cd = C.toarray()
     for _ in range(30):
         b = s.next_batch()
@@ -94,10 +95,11 @@ def test_prigp_sampler_invariants():
                 assert Cd[u, k] == 0 or Cd[u, t] > Cd[u, k]
 
 
-def test_uitj_sampler_invariants():
+@pytest.mark.parametrize("native", [True, False])
+def test_uitj_sampler_invariants(native):
     R = random_R(6)
     C = T.normalise_rows(T.coefficients(T.top_k_rows(T.user_similarity(R), 200, True), R, True))
-    s = T.UITJSampler(R, C, batch_size=40, seed=4)
+    s = T.UITJSampler(R, C, batch_size=40, seed=4, native=native)
     Cd = C.toarray()
     for _ in range(30):
         tup, coefs = s.next_batch()
@@ -105,4 +107,26 @@ def test_uitj_sampler_invariants():
         for (u, i, t, j), (ci, ct) in zip(tup, coefs):
             assert R[u, i] != 0 and R[u, t] == 0 and Cd[u, t] != 0
             assert R[u, j] == 0 and Cd[u, j] == 0
-            assert ci == Cd[u, i] and ct == Cd[u, t]
+            assert np.float32(ci) == np.float32(Cd[u, i]) and np.float32(ct) == np.float32(Cd[u, t])
+
+
+@pytest.mark.parametrize("seed", [0, 3, 12345])
+def test_native_tuple_samplers_reproduce_the_python_stream(seed):
+    """cf_tuple_sampler draws exactly what the Python restatements draw from
+    RandomState(seed): same shuffles, randint rejections and randn calls,
+    across epoch boundaries."""
+    R = random_R(7)
+    S = T.user_similarity(R)
+    Cp = T.coefficients(T.top_k_rows(S.copy(), 5), R, weighted=False)
+    py = T.PRIGPSampler(R, Cp, batch_size=64, seed=seed, native=False)
+    nat = T.PRIGPSampler(R, Cp, batch_size=64, seed=seed)
+    nb = 3 * (R.nnz // 64) + 2                     # three epochs and then some
+    for _ in range(nb):
+        np.testing.assert_array_equal(nat.next_batch(), py.next_batch())
+    Cc = T.normalise_rows(T.coefficients(T.top_k_rows(S.copy(), 50, True), R, True))
+    py = T.UITJSampler(R, Cc, batch_size=80, seed=seed, native=False)
+    nat = T.UITJSampler(R, Cc, batch_size=80, seed=seed)
+    for _ in range(40):
+        (a, ca), (b, cb) = nat.next_batch(), py.next_batch()
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(ca.astype(np.float32), cb.astype(np.float32))
