@@ -18,7 +18,7 @@ the engine's ``cf_step_plr``; the optimizer step itself is the gfx950 kernel.
   src/samplers/sampler_prigp.py:24-52 and sampler_uitj_ranking.py:22-38 on a
   seedable RandomState, without the thread and queue -- run natively
   (``cf_tuple_sampler_*``, csrc/cf_mt_sampler.cpp) on the same legacy MT19937
-  stream; ``native=False`` keeps the Python loops (same batches, ~50x slower).
+  stream; ``native=False`` keeps the Python loops (same batches, ~20x slower).
 """
 import ctypes
 import os

@@ -111,8 +111,8 @@ def tuple_rates(tra):
         out[name] = {"d": 100, "B": 1000, "tuples_per_s": steps * 1000 / dt,
                      "host_sampler_tuples_per_s": n * 1000 / host_dt,
                      "preprocess_s": prep,
-                     "note": "engine step rate on pre-drawn tuples; the python tuple sampler "
-                             "(the reference's loops) is the end-to-end bound"}
+                     "note": "engine step rate on pre-drawn tuples; host_sampler = the native "
+                             "tuple sampler (cf_tuple_sampler, the Python loops' exact stream)"}
         e.close()
     return out
 
