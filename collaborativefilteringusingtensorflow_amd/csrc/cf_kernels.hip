@@ -1150,7 +1150,10 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     {
         const float* S = isU ? a.slotU : a.slotV;
         const int64_t s0 = r * (int64_t)cap;
-        constexpr int NF = 4;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
+#ifndef CF_APPLY_NF
+#define CF_APPLY_NF 4
+#endif
+        constexpr int NF = CF_APPLY_NF;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
         for (int t0 = 0; t0 < ns; t0 += NF) {
             float h[NF][EPL];
 #pragma unroll
