@@ -1198,23 +1198,33 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
 #ifndef CF_APPLY_DETECT_WAVES
 #define CF_APPLY_DETECT_WAVES 1   // 4 measured slower: ~46 owners per block, ~3 per group in series
 #endif
-// waves of an apply block that find owners (64 work items each)
+// waves of an apply block that find owners (kApplyChunk work items each)
 constexpr int kApplyDetectWaves = CF_APPLY_DETECT_WAVES;
+#ifndef CF_APPLY_CHUNK
+// work items per detecting wave (<= 64).  A/B at cfg2: 64 best; 32 and 16
+// double / quadruple the apply blocks and delay the fused draw (34 -> 42 / 50
+// us); one-wave apply blocks (CF_APPLY_WAVE_BLOCKS) serialise ~3 owners per
+// group (standalone apply 24 -> 45 us)
+#define CF_APPLY_CHUNK 64
+#endif
+constexpr int kApplyChunk = CF_APPLY_CHUNK;
 
-template <int EPL>
+// BS = workgroup size (256, or 64 for one-wave apply blocks)
+template <int EPL, int BS = kBlock>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
-    __shared__ double s_red[kWavesPerBlock];
+    constexpr int NWV = BS / kWave, NGR = BS / kGL;
+    __shared__ double s_red[NWV];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
     const int gl = lane & (kGL - 1);
     if (block == 0 && a.loss_acc != nullptr) {
         // fixed order; eight partials in flight per lane, not a chain of loads
         double t = 0.0;
-        for (int k0 = threadIdx.x; k0 < a.n_partial; k0 += 8 * kBlock) {
+        for (int k0 = threadIdx.x; k0 < a.n_partial; k0 += 8 * BS) {
             double v[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
-                const int k = k0 + q * kBlock;
+                const int k = k0 + q * BS;
                 v[q] = k < a.n_partial ? a.loss_partial[k] : 0.0;
             }
 #pragma unroll
@@ -1223,12 +1233,16 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         t = wave_sum_d(t);
         if (lane == 0) s_red[wv] = t;
         __syncthreads();
-        if (threadIdx.x == 0) a.loss_acc[0] += (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
+        if (threadIdx.x == 0) {
+            double tt = 0.0;
+            for (int w = 0; w < NWV; ++w) tt += s_red[w];
+            a.loss_acc[0] += tt;
+        }
     }
     // a block takes kApplyDetectWaves x 64 work items at a time: those waves
     // find their owners (~18 % of the occurrences at cfg2), then the block's
     // 16 groups apply them round-robin
-    constexpr int NW = kApplyDetectWaves;
+    constexpr int NW = kApplyDetectWaves < NWV ? kApplyDetectWaves : NWV;
     __shared__ unsigned long long s_mask[NW];
     __shared__ int64_t s_row[NW * kWave];
     __shared__ int s_isU[NW * kWave];
@@ -1236,10 +1250,10 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
     const int64_t nU = a.count_users ? a.nU : 0, nV = a.count_items ? a.nV : 0;
     const int64_t total = nU + nV + a.nS;
     const int group = threadIdx.x >> 4;
-    constexpr int64_t chunk = (int64_t)NW * kWave;
+    constexpr int64_t chunk = (int64_t)NW * kApplyChunk;
     for (int64_t base = (int64_t)block * chunk; base < total; base += (int64_t)nblocks * chunk) {
         if (wv < NW) {
-            const int64_t q = base + wv * kWave + lane;
+            const int64_t q = lane < kApplyChunk ? base + wv * kApplyChunk + lane : total;
             int64_t row = -1;
             int isU = 0, c = 0;
             if (q < nU) {
@@ -1275,7 +1289,7 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
         __syncthreads();
         // owners in (wave, lane) order; group g applies owners g, g + 16, ...
         // -- the four groups of a wave take four different owners at once
-        for (int t = group;; t += kGroupsPerBlock) {
+        for (int t = group;; t += NGR) {
             int rem = t, src = -1;
             for (int w = 0; w < NW; ++w) {
                 unsigned long long m = s_mask[w];
@@ -1297,6 +1311,12 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
 template <int EPL>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
     apply_body<EPL>(a, blockIdx.x, gridDim.x);
+}
+
+// one-wave apply blocks: the detecting wave's own four groups apply its owners
+template <int EPL>
+__global__ __launch_bounds__(kWave) void apply_wave_kernel(ApplyArgs a) {
+    apply_body<EPL, kWave>(a, blockIdx.x, gridDim.x);
 }
 
 // horizontal fusion on the device-sampler path: apply of step s (blocks
@@ -1667,14 +1687,29 @@ static int apply_grid(const ApplyArgs& a) {
     // 64 work items (user occurrences, item occurrences, served rows) per
     // detecting wave
     const int64_t items = (a.count_users ? a.nU : 0) + (a.count_items ? a.nV : 0) + a.nS;
-    const int64_t per = (int64_t)kApplyDetectWaves * kWave;
+    const int64_t per = (int64_t)kApplyDetectWaves * kApplyChunk;
     int64_t blocks = (items + per - 1) / per;
-    if (blocks > 4096) blocks = 4096;  // grid-stride over the work items
+    if (blocks > 16384) blocks = 16384;  // grid-stride over the work items
     if (blocks < 1) blocks = 1;        // block 0 still reduces the loss
     return (int)blocks;
 }
 
+#ifndef CF_APPLY_WAVE_BLOCKS
+#define CF_APPLY_WAVE_BLOCKS 0
+#endif
+
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
+    if (CF_APPLY_WAVE_BLOCKS) {
+        const dim3 grid(apply_grid(a)), block(kWave);
+        switch (epl_for(a.d)) {
+            case 1: hipLaunchKernelGGL(apply_wave_kernel<1>, grid, block, 0, s, a); break;
+            case 2: hipLaunchKernelGGL(apply_wave_kernel<2>, grid, block, 0, s, a); break;
+            case 4: hipLaunchKernelGGL(apply_wave_kernel<4>, grid, block, 0, s, a); break;
+            case 8: hipLaunchKernelGGL(apply_wave_kernel<8>, grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL(apply_wave_kernel<16>, grid, block, 0, s, a); break;
+        }
+        return hipGetLastError();
+    }
     const dim3 grid(apply_grid(a)), block(kBlock);
     switch (epl_for(a.d)) {
         case 1: hipLaunchKernelGGL(apply_kernel<1>, grid, block, 0, s, a); break;
