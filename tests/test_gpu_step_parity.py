@@ -269,3 +269,56 @@ def test_side_stream_prep_matches_oracle(fold1, streams, opts):
     out = run_bpr_like("bpr", fold1, get_stream(streams, "rank_b100_w5"), 32, 0.05, K=40)
     for t, (g, o) in out.items():
         assert rel(g, o) <= RTOL, (t, rel(g, o))
+
+
+@pytest.mark.parametrize("model,d,W,G,B", [
+    ("bpr", 256, 1, 1, 1),      # widest rows, a one-pair batch
+    ("bpr", 8, 64, 1, 37),      # the most negatives per pair, ragged batch
+    ("amf", 256, 5, 1, 130),
+    ("cml", 128, 16, 1, 50),    # CML's negative cap
+    ("gbpr", 16, 2, 16, 20),    # the largest group
+    ("gbpr", 33, 1, 1, 3),      # d not a multiple of the 16-lane group
+])
+def test_extreme_shapes_match_oracle(fold1, model, d, W, G, B):
+    """The ABI's limits (n_factors 256, n_neg 64 (CML 16), gsize 16) and
+    ragged / single-pair batches, against the float64 oracle."""
+    rng = np.random.RandomState(d + W + G + B)
+    nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    U, V, b = init_tables(fold1, d, 17, truncated=(model != "cml"), bias=(model == "gbpr"))
+    kw = dict(reg=0.03)
+    if model == "gbpr":
+        kw["rho"] = 0.4
+    if model == "cml":
+        kw = dict(margin=1.0, reg_cov=0.5, use_rank_weight=True, clip_norm=1.0)
+    e = make_engine(model, fold1, d, W, G=G, **kw)
+    e.set_table("user", U)
+    e.set_table("item", V)
+    if b is not None:
+        e.set_table("bias", b)
+    U64, V64 = U.astype(np.float64), V.astype(np.float64)
+    b64 = b.astype(np.float64) if b is not None else None
+    AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
+    Ab = np.full_like(b64, 0.1) if b is not None else None
+    users = np.nonzero(np.diff(ip))[0]
+    for s in range(5):
+        u = rng.choice(users, B)
+        pos = [ix[ip[x] + rng.randint(ip[x + 1] - ip[x])] for x in u]
+        pairs = np.stack([u, pos], 1).astype(np.int32)
+        negs = rng.randint(0, ni, (B, W)).astype(np.int32)
+        groups = rng.randint(0, nu, (B, G)).astype(np.int32) if model == "gbpr" else None
+        lg = e.step(pairs, negs, groups)
+        if model == "bpr":
+            lo = O.bpr_step(U64, V64, AU, AV, pairs, negs, 0.03)
+        elif model == "amf":
+            lo = O.amf_step(U64, V64, AU, AV, pairs, negs, 0.03, False)
+        elif model == "gbpr":
+            lo = O.gbpr_step(U64, V64, b64, AU, AV, Ab, pairs, negs, groups, 0.4, 0.03)
+        else:
+            lo = O.cml_step(U64, V64, AU, AV, pairs, negs, 1.0, 0.5, 1.0, use_rank_weight=True)
+        assert abs(lg - lo) <= RTOL * abs(lo) + 1e-6, (s, lg, lo)
+    for t, o in (("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV)):
+        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+    if b is not None:
+        assert rel(e.get_table("bias"), b64) <= RTOL
+    e.close()
