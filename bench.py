@@ -41,8 +41,12 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 CONFIGS = {
     # configs[1] of BASELINE.json
+    # B = 2^19 pairs per GPU per step: the multi-GPU step all-reduces the dense
+    # 25.6 MB item gradient once per step whatever B is, so B sets how many
+    # triplets each exchanged byte carries; the 2^16 line of earlier
+    # profiles is `--batch 65536`
     "cfg2": dict(model="bpr", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
-                 graph_seed=20261015, d=64, W=1, G=1, B=65536, reg=0.02, truncated=True,
+                 graph_seed=20261015, d=64, W=1, G=1, B=524288, reg=0.02, truncated=True,
                  desc="BPR-MF synthetic 1M users x 100K items, d=64"),
     # configs[2]: CML on the same graph
     "cfg3": dict(model="cml", n_users=1_000_000, n_items=100_000, mean_degree=50.0, zipf=0.8,
@@ -223,6 +227,8 @@ def main():
                     help="cf_set_option pipeline: 1 apply(s)+draw(s+1) (default); 0 stepwise")
     ap.add_argument("--slot-max", type=int, default=0,
                     help="cf_set_option slot_max (0 = engine default)")
+    ap.add_argument("--item-reduce", type=int, default=-1,
+                    help="multi-rank item path (cf_set_option item_reduce 0/1/2; -1 = engine default)")
     ap.add_argument("--n-users", type=int, default=0, help="override the config's users (rehearsals)")
     ap.add_argument("--n-items", type=int, default=0, help="override the config's items (rehearsals)")
     ap.add_argument("--hot-replicas", type=int, default=0,
@@ -230,6 +236,11 @@ def main():
     ap.add_argument("--zipf", type=float, default=-1.0,
                     help="override the item popularity exponent (experiments; 0 = uniform)")
     args = ap.parse_args()
+    # the JSON line is the only thing on stdout: RCCL / HIP print banners
+    # there from native code, so fd 1 points at stderr until the end
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["B"] = args.batch
@@ -288,6 +299,8 @@ def main():
     eng.set_option("pipeline", args.pipeline)
     if args.hot_replicas:
         eng.set_option("hot_replicas", args.hot_replicas)
+    if args.item_reduce >= 0:
+        eng.set_option("item_reduce", args.item_reduce)
     if args.slot_max:
         eng.set_option("slot_max", args.slot_max)
     eng.set_interactions(indptr, indices)
@@ -359,7 +372,7 @@ def main():
         run(nb)
         sync()
         eng.profile(False)
-        for kname in ("sample", "slot", "step", "grad_prep", "apply", "apply_prep", "apply_slot",
+        for kname in ("sample", "slot", "step", "grad_prep", "apply", "apply_prep", "apply_slot", "item_reduce",
                       "apply_dense", "clip"):
             ms, n = eng.profile_read(kname)
             if n:
@@ -378,7 +391,7 @@ def main():
     mean_row = float((deg * deg).sum() / max(deg.sum(), 1.0))
     db = draw_bytes_per_pair(W, Gm, mean_row) * B if dom == "grad_prep" else 0.0
     achieved = (gb + db) / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
-    traffic = load_pmc(args.config, world)
+    traffic = load_pmc("%s_b%d" % (args.config, B), world)
     if dom == "grad_prep":
         kdesc = ("grad_fast_kernel: gather + loss + grads + singleton-row Adagrad of step s, "
                  "fused with the device draw + count of step s+1")
@@ -448,8 +461,8 @@ def main():
             out["cpu_baseline"] = None
     eng.close()
     if rank == 0:
-        print(json.dumps(out))
-        sys.stdout.flush()
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
     if sharded:
         dist.barrier()
         dist.destroy_process_group()

@@ -164,6 +164,7 @@ struct cf_engine {
 
     int topk_path = 0;  // cf_set_option("topk_path")
     int grad_path = 0;  // cf_set_option("grad_path")
+    int item_reduce = 1;  // cf_set_option("item_reduce"): dense mode counts item rows
     int prep_side = 0;  // cf_set_option("prep_stream"): 1 = side stream (overlap), 0 = main
 
     // profiling
@@ -225,8 +226,10 @@ int ensure_slots(cf_engine* e) {
     dfree(e->slotV);
     dfree(e->GVrep);
     CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
-    if (!c.dense_item_apply) {
+    if (!c.dense_item_apply || e->item_reduce == 1) {
         CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+    }
+    if (!c.dense_item_apply) {
         if (e->hot_rep > 1) {
             const size_t n = (size_t)(e->hot_rep - 1) * c.n_items * c.n_factors;
             CF_TRY(dalloc(&e->GVrep, n));
@@ -303,7 +306,9 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.repV = e->GVrep ? e->hot_rep - 1 : 0;
     a.loss_partial = e->loss_partial;
     a.count_users = 1;
-    a.count_items = c.dense_item_apply ? 0 : 1;
+    a.count_items = (!c.dense_item_apply || e->item_reduce) ? 1 : 0;
+    a.items_grad_only = (c.dense_item_apply && e->item_reduce) ? 1 : 0;
+    if (c.dense_item_apply && e->item_reduce == 2) a.capV = 0;  // duplicates: float atomics
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
     a.plr_kind = c.plr_kind;
@@ -482,6 +487,8 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.n_items = c.n_items;
     p.count_users = a.count_users;
     p.count_items = a.count_items;
+    p.items_grad_only = a.items_grad_only;
+    if (a.items_grad_only && a.capV == 0) p.count_items = 0;  // item_reduce 2: nothing to reduce
     p.occU = e->occU_[k];
     p.rankU = e->rankU_[k];
     p.nU = (int64_t)B * users_per_pair(c);
@@ -1172,6 +1179,14 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
+    if (a.items_grad_only && a.capV > 0) {
+        // duplicated item rows: slot rows summed into the bound buffer now, so
+        // it holds this rank's complete item gradient when the all-reduce starts
+        ApplyArgs p = apply_args(e, a, B, k, nullptr);
+        p.count_users = 0;
+        ProfScope ps(e, CF_K_ITEM_REDUCE);
+        CF_HIP(launch_apply(p, e->stream));
+    }
     e->lg_args = a;
     e->lg_set = k;
     e->lg_B = B;
@@ -1185,6 +1200,7 @@ int cf_step_local_apply(cf_engine* e, int32_t next_B) {
     if (next_B < 0) return fail(CF_EINVAL, "next_B must be >= 0");
     const int k = e->lg_set;
     ApplyArgs p = apply_args(e, e->lg_args, e->lg_B, k, e->loss);
+    if (p.items_grad_only) p.count_items = 0;  // reduced in cf_step_local_grad
     e->lg_stage = 0;
     if (next_B > 0 && next_B <= e->Bcap && e->prep_side == 0) {
         // draw + count the next batch in the same launch (other buffer set)
@@ -1523,6 +1539,15 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
         e->hot_rep = (int)value;
+        e->slots_ready = false;
+        return CF_OK;
+    }
+    if (n == "item_reduce") {
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "item_reduce must be 0, 1 or 2");
+        if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        e->item_reduce = (int)value;
         e->slots_ready = false;
         return CF_OK;
     }

@@ -53,6 +53,8 @@ struct StepArgs {
     int sample;          // 1: draw batch on device; 0: batch already in occ*
     int count_users;     // count user-row occurrences (sparse user apply)
     int count_items;     // count item-row occurrences (sparse item apply)
+    int items_grad_only; // multi-rank item reduce: item rows get their summed
+                         // gradient in GV (no Adagrad here; cf_step_items after the all-reduce)
     uint64_t slot_base;  // position of this batch inside the epoch shuffle
     uint64_t rng_key;    // per-epoch draw key
     PermKey perm;
@@ -118,6 +120,7 @@ struct ApplyArgs {
     int repV;
     int64_t n_items;
     int count_users, count_items;
+    int items_grad_only; // item owners store the summed gradient row into GV
     // work items: the batch's occurrences (+ the served rows of the group
     // exchange); the owner of a duplicated row applies it
     const int32_t* __restrict__ occU;

@@ -226,18 +226,24 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
                                         const float (&x0)[EPL], const float (&g)[EPL],
                                         const StepArgs& a) {
     if (count == 1) {
-        gapply<EPL>(X, A, r, d, gl, x0, g, a.lr, a.clip != 0, a.clip_norm);
+        if (a.items_grad_only && X == a.V)
+            gstore<EPL>(G, r, d, gl, g);  // sole writer of the zeroed dense row
+        else
+            gapply<EPL>(X, A, r, d, gl, x0, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) cnt[r] = 0;
     } else if (slot >= 0) {
         gstore<EPL>(S, slot, d, gl, g);
     } else {
         gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
+        // item_reduce 2 (no reduce launch): the atomic path resets the count
+        // itself; a count read as 0 by a later occurrence still means atomics
+        if (a.items_grad_only && a.capV == 0 && X == a.V && gl == 0) cnt[r] = 0;
     }
 }
 
 __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g) {
     // GBPR item bias: one scalar row
-    if (count == 1) {
+    if (count == 1 && !a.items_grad_only) {
         const float acc = fmaf(g, g, a.Ab[r]);
         a.Ab[r] = acc;
         a.b[r] -= adagrad_delta(a.lr, g, acc);
@@ -833,9 +839,13 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
                                             const float (&g)[EPL], const StepArgs& a) {
     // CF_EXP_* are bench-only attribution builds (wrong results by design)
     if (count == 1) {
+        if (a.items_grad_only && X == a.V) {
+            gstore<EPL>(G, r, d, gl, g);  // sole writer of the zeroed dense row
+        } else {
 #ifndef CF_EXP_NO_SINGLE
-        gapply_pre<EPL>(X, A, r, d, gl, x0, acc0, g, a.lr, a.clip != 0, a.clip_norm);
+            gapply_pre<EPL>(X, A, r, d, gl, x0, acc0, g, a.lr, a.clip != 0, a.clip_norm);
 #endif
+        }
         if (gl == 0) cnt[r] = 0;
     } else if (slot >= 0) {
         gstore<EPL>(S, slot, d, gl, g);
@@ -843,6 +853,7 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
 #ifndef CF_EXP_NO_ATOMIC
         gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
 #endif
+        if (a.items_grad_only && a.capV == 0 && X == a.V && gl == 0) cnt[r] = 0;  // see gfinish
     }
 }
 
@@ -903,9 +914,10 @@ struct PairRows {
 #pragma unroll
         for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
-        gload_acc<EPL>(a.AV, i, a.d, gl, ci == 1, ai);
+        const bool item_acc = !a.items_grad_only;
+        gload_acc<EPL>(a.AV, i, a.d, gl, item_acc && ci == 1, ai);
 #pragma unroll
-        for (int w = 0; w < WT; ++w) gload_acc<EPL>(a.AV, j[w], a.d, gl, cj[w] == 1, aj[w]);
+        for (int w = 0; w < WT; ++w) gload_acc<EPL>(a.AV, j[w], a.d, gl, item_acc && cj[w] == 1, aj[w]);
 #pragma unroll
         for (int k = 0; k < NG; ++k) gload_acc<EPL>(a.AU, g[k], a.d, gl, cg[k] == 1, ag[k]);
     }
@@ -1137,9 +1149,14 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     float* A = isU ? a.AU : a.AV;
     float* G = isU ? a.GU : a.GV;
     const int cap = isU ? a.capU : a.capV;
+    // multi-rank item reduce: the row's summed gradient goes to GV for the
+    // all-reduce; the table and accumulator are left to cf_step_items
+    const bool reduce_only = !isU && a.items_grad_only;
     float x[EPL], acc[EPL], g[EPL];
-    gload<EPL>(X, r, a.d, gl, x);
-    gload_acc<EPL>(A, r, a.d, gl, true, acc);
+    if (!reduce_only) {
+        gload<EPL>(X, r, a.d, gl, x);
+        gload_acc<EPL>(A, r, a.d, gl, true, acc);
+    }
     // c = the row's count word: occurrences, plus kRemoteFlag for a row the
     // group exchange served (all its contributions went to G)
     const int flagged = c & kRemoteFlag;
@@ -1173,7 +1190,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
         gload<EPL>(G, r, a.d, gl, h);
 #pragma unroll
         for (int s = 0; s < EPL; ++s) g[s] += h[s];
-        row_zero<EPL>(G + r * a.d, a.d, gl);
+        if (!reduce_only) row_zero<EPL>(G + r * a.d, a.d, gl);
         for (int k = 0; k < nrep; ++k) {
             float* Gk = a.GVrep + (int64_t)k * a.n_items * a.d;
             gload<EPL>(Gk, r, a.d, gl, h);
@@ -1181,6 +1198,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
             for (int s = 0; s < EPL; ++s) g[s] += h[s];
             row_zero<EPL>(Gk + r * a.d, a.d, gl);
         }
+    }
+    if (reduce_only) {
+        row_st<EPL>(G + r * (int64_t)a.d, a.d, gl, g);
+        if (gl == 0) cnt[r] = 0;
+        return;
     }
     gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
     if (gl == 0) {

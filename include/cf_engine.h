@@ -86,7 +86,9 @@ enum cf_kernel_id {
     CF_K_APPLY_PREP = 8, /* apply of step s fused with the draw of step s+1    */
     CF_K_GRAD_PREP = 9,  /* gradient of step s + draw of step s+1 (pipeline 2) */
     CF_K_APPLY_SLOT = 10,/* (retired pipeline 2)                               */
-    CF_K_COUNT = 11
+    CF_K_ITEM_REDUCE = 11,/* multi-rank: duplicated item rows' summed gradient
+                            into the bound buffer, before the all-reduce    */
+    CF_K_COUNT = 12
 };
 
 /*
@@ -327,6 +329,16 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                count of step s+1 inside step s's gradient launch, the apply
  *                alone (measured 4.7 us/step slower at cfg2); 0 = one step at
  *                a time, three launches.
+ *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
+ *                item occurrences are counted like user ones, a row seen
+ *                once stores its gradient row into the bound buffer, a
+ *                duplicated row stores slot rows summed by a short reduce
+ *                launch in cf_step_local_grad (default; plain stores instead
+ *                of one float atomic per element and occurrence); 2 = rows
+ *                seen once store, every occurrence of a duplicated row adds
+ *                with float atomics (no reduce launch); 0 = every item
+ *                occurrence adds into the buffer with float atomics.
+ *                Same sums either way (fp32 summation order differs).
  *   "profile_mask" bit k set = cf_profile_enable times kernel id k (default
  *                all): timing only the kernel of interest keeps the event
  *                pairs of the others out of a timed loop.

@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, model, q):
+def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -42,6 +42,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, q):
     kw = dict(reg=0.05) if model == "bpr" else dict(margin=1.0, reg_cov=1.0, clip_norm=1.0)
     e = Engine(model, u1 - u0, 1682, U0.shape[1], n_neg=W, dense_item_apply=True,
                seed=10 + rank, **kw)
+    e.set_option("item_reduce", item_reduce)
     e.set_interactions(lip, lix)
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
@@ -58,8 +59,9 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("item_reduce", [1, 2, 0], ids=["reduce", "store-singletons", "atomic"])
 @pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
-def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream):
+def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream, item_reduce):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(8)
     d = 24
@@ -69,7 +71,7 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, item_reduce, q))
              for r in range(2)]
     for p in procs:
         p.start()

@@ -95,8 +95,19 @@ def test_bpr_steps_match_oracle(fold1, streams, name, d, reg):
         assert rel(g, o) <= RTOL, (t, rel(g, o))
 
 
-def test_bpr_dense_item_apply_matches(fold1, streams):
-    out = run_bpr_like("bpr", fold1, get_stream(streams, "rank_b100_w1"), 32, 0.1, K=20, dense=True)
+@pytest.mark.parametrize("opts", [{"item_reduce": 0}, {"item_reduce": 1},
+                                  {"item_reduce": 1, "slot_max": 2}, {"item_reduce": 2}],
+                         ids=["atomic", "reduce", "reduce-hot", "store-singletons"])
+@pytest.mark.parametrize("stream", ["rank_b100_w1", "rank_b100_w5"])
+def test_bpr_dense_item_apply_matches(fold1, streams, opts, stream):
+    """The multi-rank item path (dense_item_apply) on one rank: float atomics
+    for every item occurrence, or the item reduce (singleton rows stored,
+    duplicated rows through slot rows; slot_max 2 sends hot rows to atomics)."""
+    _OPTS.update(opts)
+    try:
+        out = run_bpr_like("bpr", fold1, get_stream(streams, stream), 32, 0.1, K=20, dense=True)
+    finally:
+        _OPTS.clear()
     for t, (g, o) in out.items():
         assert rel(g, o) <= RTOL, (t, rel(g, o))
 
