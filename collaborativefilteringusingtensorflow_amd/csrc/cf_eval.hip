@@ -313,6 +313,7 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
         Us[r * S + kk] = (r < nu && kk < d) ? a.U[(int64_t)a.users[u0 + r] * d + kk] : 0.f;
     }
     int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
+    int64_t nxt = INT64_MAX;                 // the train item at the cursor, kept in a register
     if (tid < kFusedUsers) {
         thr[tid] = 0ull;
         cnt[tid] = 0;
@@ -320,8 +321,15 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
             const int u = a.users[u0 + tid];
             cur = a.indptr[u];
             end = a.indptr[u + 1];
+            if (cur < end) nxt = a.indices[cur];
         }
     }
+    // the next item tile is loaded into registers during this tile's MFMA and
+    // candidate phases and written to LDS after them (d % 4 == 0)
+    const bool vec = (d & 3) == 0;
+    const int q4 = Dp >> 2;
+    constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + kBlock - 1) / kBlock;
+    float4 pre[kPre];
     __syncthreads();
     if (MODEL == CML && tid < kFusedUsers) {
         float sqn = 0.f;
@@ -329,18 +337,33 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
         unorm[tid] = sqn;
     }
 
+    auto load_tile = [&](int64_t jt) {   // 16-B loads; rows are 16-B aligned when d % 4 == 0
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) {
+            const int t = tid + q * kBlock;
+            const int r = t / q4, kk = (t - r * q4) * 4;
+            const int64_t j = jt + r;
+            pre[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t < kFusedItems * q4 && j < a.n_items && kk < d)
+                pre[q] = *reinterpret_cast<const float4*>(a.V + j * d + kk);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) {
+            const int t = tid + q * kBlock;
+            const int r = t / q4, kk = (t - r * q4) * 4;
+            if (t < kFusedItems * q4) *reinterpret_cast<float4*>(Vs + r * S + kk) = pre[q];
+        }
+    };
+    if (vec) {
+        load_tile(0);
+        store_tile();
+    }
+
     for (int64_t j0 = 0; j0 < a.n_items; j0 += kFusedItems) {
-        // ---- stage the item tile, its bias, the train mask ---------------------
-        if ((d & 3) == 0) {   // 16-B loads; rows are 16-B aligned when d % 4 == 0
-            const int q4 = Dp >> 2;
-            for (int t = tid; t < kFusedItems * q4; t += kBlock) {
-                const int r = t / q4, kk = (t - r * q4) * 4;
-                const int64_t j = j0 + r;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (j < a.n_items && kk < d) v = *reinterpret_cast<const float4*>(a.V + j * d + kk);
-                *reinterpret_cast<float4*>(Vs + r * S + kk) = v;
-            }
-        } else {
+        // ---- stage the item tile (unless prefetched), its bias, the train mask --
+        if (!vec) {
             for (int t = tid; t < kFusedItems * Dp; t += kBlock) {
                 const int r = t / Dp, kk = t - r * Dp;
                 const int64_t j = j0 + r;
@@ -351,13 +374,16 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
         if (tid < kFusedUsers) {
             unsigned long long m = 0ull;
-            while (cur < end && (int64_t)a.indices[cur] < j0 + kFusedItems) {
-                m |= 1ull << (int)((int64_t)a.indices[cur] - j0);
+            while (nxt < j0 + kFusedItems) {   // sorted row: no load unless an item is consumed
+                m |= 1ull << (int)(nxt - j0);
                 ++cur;
+                nxt = cur < end ? (int64_t)a.indices[cur] : INT64_MAX;
             }
             mask[tid] = m;
         }
         __syncthreads();
+        const bool more = vec && j0 + kFusedItems < a.n_items;
+        if (more) load_tile(j0 + kFusedItems);
         // ---- 32 x 32 tile per wave on the matrix cores --------------------------
         floatx16 acc;
 #pragma unroll
@@ -395,6 +421,7 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
             }
         }
         __syncthreads();
+        if (more) store_tile();   // every wave is past its MFMA reads of this tile
         // ---- shrink lists that could overflow at the next step ---------------------
         for (int R = wv; R < nu; R += kWavesPerBlock)
             if (cnt[R] > kFusedCap - kFusedItems)
