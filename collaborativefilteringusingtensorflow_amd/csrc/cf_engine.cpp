@@ -1435,7 +1435,7 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     CF_HIP(hipStreamSynchronize(e->side));
     const bool fused_ok = k <= kFusedMaxK && c.n_factors <= kFusedMaxD;
     if (e->topk_path == 2 && !fused_ok)
-        return fail(CF_EINVAL, "fused top-k needs k <= 32 and n_factors <= 128");
+        return fail(CF_EINVAL, "fused top-k needs k <= 28 and n_factors <= 128");
     if (fused_ok && e->topk_path != 1)
         return score_topk_fused(e, users, n, k, exclude_train, idx_out, val_out);
     const size_t row_bytes = (size_t)c.n_items * 4;

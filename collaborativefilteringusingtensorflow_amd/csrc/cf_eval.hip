@@ -235,7 +235,6 @@ __global__ __launch_bounds__(kBlock) void topk_kernel(TopkArgs a) {
 // k entries (and raises the threshold) whenever fewer than 64 slots remain.
 // ---------------------------------------------------------------------------
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int kFS = kFusedMaxD + 4;   // LDS row stride upper bound (floats)
 
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
     const int lo = __shfl_xor((int)(v & 0xFFFFFFFFull), m, 64);
@@ -288,10 +287,17 @@ __device__ int wave_compact(unsigned long long* __restrict__ buf, int* cnt,
     return m;
 }
 
+// V tile in LDS: 64 rows x 128 floats, no padding; the 16-B chunk q of row r
+// sits at chunk q ^ (r & 31), so the 16 lanes of a ds_read_b128 phase (rows
+// c .. c+15 at one k offset) land on 16 different chunks: conflict-free.
+__device__ __forceinline__ int vs_off(int r, int kk) {
+    return r * kFusedMaxD + ((((kk >> 2) ^ (r & 31)) << 2) | (kk & 3));
+}
+
 template <int MODEL>
-__global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
-    __shared__ __attribute__((aligned(16))) float Us[kFusedUsers * kFS];
-    __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFS];
+__global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) {
+    // ~80 KB of LDS: two blocks per CU.  The user operands live in registers.
+    __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFusedMaxD];
     __shared__ unsigned long long buf[kFusedUsers * kFusedCap];
     __shared__ unsigned long long thr[kFusedUsers];
     __shared__ unsigned long long mask[kFusedUsers];
@@ -304,13 +310,28 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
     const int wv = tid >> 6;
     const int wr = wv >> 1, wc = wv & 1;     // 32-row user block, 32-col item block
     const int h = lane >> 5, c = lane & 31;
-    const int d = a.d, Dp = a.Dp, Dh = a.Dh, S = a.Dp + 4;
+    const int d = a.d, Dp = a.Dp, Dh = a.Dh;
     const int u0 = blockIdx.x * kFusedUsers;
     const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
 
-    for (int t = tid; t < kFusedUsers * Dp; t += kBlock) {
-        const int r = t / Dp, kk = t - r * Dp;
-        Us[r * S + kk] = (r < nu && kk < d) ? a.U[(int64_t)a.users[u0 + r] * d + kk] : 0.f;
+    // A operand of lane (c, h): U[row wr*32 + c][h*Dh, (h+1)*Dh), zero-padded
+    constexpr int kAH = kFusedMaxD / 2;
+    float ua[kAH];
+    {
+        const int r = wr * 32 + c;
+        const float* urow = a.U + (int64_t)a.users[u0 + (r < nu ? r : 0)] * d;
+#pragma unroll
+        for (int t = 0; t < kAH; ++t) {
+            const int kk = h * Dh + t;
+            ua[t] = (r < nu && t < Dh && kk < d) ? urow[kk] : 0.f;
+        }
+        if (MODEL == CML) {
+            float sq = 0.f;
+#pragma unroll
+            for (int t = 0; t < kAH; ++t) sq = fmaf(ua[t], ua[t], sq);
+            sq += __shfl_xor(sq, 32, 64);
+            if (wc == 0 && h == 0) unorm[r] = sq;   // |u|^2 of row r
+        }
     }
     int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
     int64_t nxt = INT64_MAX;                 // the train item at the cursor, kept in a register
@@ -330,13 +351,6 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
     const int q4 = Dp >> 2;
     constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + kBlock - 1) / kBlock;
     float4 pre[kPre];
-    __syncthreads();
-    if (MODEL == CML && tid < kFusedUsers) {
-        float sqn = 0.f;
-        for (int kk = 0; kk < d; ++kk) sqn = fmaf(Us[tid * S + kk], Us[tid * S + kk], sqn);
-        unorm[tid] = sqn;
-    }
-
     auto load_tile = [&](int64_t jt) {   // 16-B loads; rows are 16-B aligned when d % 4 == 0
 #pragma unroll
         for (int q = 0; q < kPre; ++q) {
@@ -353,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
         for (int q = 0; q < kPre; ++q) {
             const int t = tid + q * kBlock;
             const int r = t / q4, kk = (t - r * q4) * 4;
-            if (t < kFusedItems * q4) *reinterpret_cast<float4*>(Vs + r * S + kk) = pre[q];
+            if (t < kFusedItems * q4) *reinterpret_cast<float4*>(Vs + vs_off(r, kk)) = pre[q];
         }
     };
     if (vec) {
@@ -367,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
             for (int t = tid; t < kFusedItems * Dp; t += kBlock) {
                 const int r = t / Dp, kk = t - r * Dp;
                 const int64_t j = j0 + r;
-                Vs[r * S + kk] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
+                Vs[vs_off(r, kk)] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
             }
         }
         if (MODEL == GBPR && tid < kFusedItems)
@@ -389,16 +403,17 @@ __global__ __launch_bounds__(kBlock) void fused_topk_kernel(FusedTopkArgs a) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
         float vsq = 0.f;
-        const float* ap = Us + (wr * 32 + c) * S + h * Dh;
-        const float* bp = Vs + (wc * 32 + c) * S + h * Dh;
-        for (int t0 = 0; t0 < Dh; t0 += 4) {
-            const float4 a4 = *reinterpret_cast<const float4*>(ap + t0);
-            const float4 b4 = *reinterpret_cast<const float4*>(bp + t0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, b4.x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, b4.y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, b4.z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, b4.w, acc, 0, 0, 0);
-            if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+        const int br = wc * 32 + c;              // B operand row (item) of this lane
+#pragma unroll
+        for (int t0 = 0; t0 < kAH; t0 += 4) {
+            if (t0 < Dh) {   // block-uniform
+                const float4 b4 = *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0));
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
+                if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+            }
         }
         float vnorm = 0.f;
         if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2

@@ -171,12 +171,12 @@ struct ScoreArgs {
     const int32_t* __restrict__ indices;
 };
 
-// fused scoring GEMM (fp32 MFMA) + streaming per-user top-k, d <= 128, k <= 32
+// fused scoring GEMM (fp32 MFMA) + streaming per-user top-k, d <= 128, k <= 28
 constexpr int kFusedUsers = 64;
 constexpr int kFusedItems = 64;
 constexpr int kFusedMaxD = 128;
-constexpr int kFusedMaxK = 32;
-constexpr int kFusedCap = 128;   // candidate slots per user
+constexpr int kFusedCap = 92;    // candidate slots per user (LDS for two blocks per CU)
+constexpr int kFusedMaxK = kFusedCap - kFusedItems;   // a compacted list + one tile's 64 fit
 
 struct FusedTopkArgs {
     int model;

@@ -302,7 +302,7 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
 
 /*
  * Engine options (name, value):
- *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 32 and d <= 128, else
+ *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 28 and d <= 128, else
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
  *   "grad_path"  0 = auto (phased gradient kernel for W in {1,5}, d <= 128,
