@@ -304,6 +304,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
     __shared__ int cnt[kFusedUsers];
     __shared__ float unorm[kFusedUsers];
     __shared__ float bt[kFusedItems];
+    __shared__ int thr_ver;                  // bumped whenever a compaction raised thresholds
 
     const int tid = threadIdx.x;
     const int lane = lane_id();
@@ -312,6 +313,12 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
     const int h = lane >> 5, c = lane & 31;
     const int d = a.d, Dp = a.Dp, Dh = a.Dh;
     const int u0 = blockIdx.x * kFusedUsers;
+    if (tid == 0) thr_ver = 0;
+    // the score words of the thresholds of this lane's 16 output rows, kept in
+    // registers: a score whose key word is below its row's cannot enter the
+    // list, so most scores are rejected without touching LDS
+    uint32_t thi[16];
+    int thi_ver = -1;
     const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
 
     // A operand of lane (c, h): U[row wr*32 + c][h*Dh, (h+1)*Dh), zero-padded
@@ -404,30 +411,59 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
         float vsq = 0.f;
         const int br = wc * 32 + c;              // B operand row (item) of this lane
+#ifdef CF_FUSED_2ACC   // experiment: two independent MFMA chains, summed at the end
+        floatx16 acc2;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
+#endif
+#ifndef CF_FUSED_EXP_NOMFMA   // attribution builds (wrong results by design)
 #pragma unroll
         for (int t0 = 0; t0 < kAH; t0 += 4) {
             if (t0 < Dh) {   // block-uniform
                 const float4 b4 = *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0));
+#ifdef CF_FUSED_2ACC
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
+                acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc2, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
+                acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc2, 0, 0, 0);
+#else
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
+#endif
                 if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
             }
         }
+#endif
+#ifdef CF_FUSED_2ACC
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+#endif
         float vnorm = 0.f;
         if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
         // ---- candidates above each user's threshold -------------------------------
         const int jl = wc * 32 + c;
         const int64_t J = j0 + jl;
+#ifndef CF_FUSED_EXP_NOCAND
+        if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
+            thi_ver = thr_ver;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                thi[q] = R < nu ? (uint32_t)(thr[R] >> 32) : 0xFFFFFFFFu;
+            }
+        }
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-            if (R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
-                float s = acc[q];
-                if (MODEL == GBPR) s += bt[jl];
-                if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];   // -|u - v|^2
-                const unsigned long long key = ((unsigned long long)float_key(s) << 32) |
+            float s = acc[q];
+            if (MODEL == GBPR) s += bt[jl];
+            if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];   // -|u - v|^2
+            const uint32_t fk = float_key(s);
+            // key > thr[R] implies fk >= thi[q]: a pure prefilter
+            if (fk >= thi[q] && R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
+                const unsigned long long key = ((unsigned long long)fk << 32) |
                                                (0xFFFFFFFFull - (unsigned long long)J);
                 if (key > thr[R]) {
                     const int pos = atomicAdd(&cnt[R], 1);
@@ -435,12 +471,17 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                 }
             }
         }
+#else
+        if (acc[0] == 12345.f && J == 7) cnt[0] = 1;   // keep the MFMA result live
+#endif
         __syncthreads();
         if (more) store_tile();   // every wave is past its MFMA reads of this tile
         // ---- shrink lists that could overflow at the next step ---------------------
         for (int R = wv; R < nu; R += kWavesPerBlock)
-            if (cnt[R] > kFusedCap - kFusedItems)
+            if (cnt[R] > kFusedCap - kFusedItems) {
                 wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+                if (lane == 0) atomicAdd(&thr_ver, 1);
+            }
         __syncthreads();
     }
     // ---- final sort and output -------------------------------------------------------
