@@ -403,7 +403,11 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
             mask[tid] = m;
         }
         __syncthreads();
+#ifdef CF_FUSED_EXP_NOLOAD   // attribution: no tile streaming (stale tile)
+        const bool more = false;
+#else
         const bool more = vec && j0 + kFusedItems < a.n_items;
+#endif
         if (more) load_tile(j0 + kFusedItems);
         // ---- 32 x 32 tile per wave on the matrix cores --------------------------
         floatx16 acc;
@@ -477,11 +481,23 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         __syncthreads();
         if (more) store_tile();   // every wave is past its MFMA reads of this tile
         // ---- shrink lists that could overflow at the next step ---------------------
-        for (int R = wv; R < nu; R += kWavesPerBlock)
-            if (cnt[R] > kFusedCap - kFusedItems) {
-                wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        // the wave's 16 rows (wv, wv + 4, ..) are checked with one LDS read and
+        // a ballot, not 16 dependent reads
+        {
+            constexpr int kRowsPerWave = kFusedUsers / kWavesPerBlock;
+            const int Rl = wv + kWavesPerBlock * lane;
+            unsigned long long need = __ballot(lane < kRowsPerWave && Rl < nu &&
+                                               cnt[lane < kRowsPerWave ? Rl : 0] > kFusedCap - kFusedItems);
+            if (need != 0ull) {
                 if (lane == 0) atomicAdd(&thr_ver, 1);
+                while (need != 0ull) {
+                    const int l = __ffsll((long long)need) - 1;
+                    need &= need - 1ull;
+                    const int R = wv + kWavesPerBlock * l;
+                    wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+                }
             }
+        }
         __syncthreads();
     }
     // ---- final sort and output -------------------------------------------------------
