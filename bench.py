@@ -229,6 +229,8 @@ def main():
                     help="cf_set_option slot_max (0 = engine default)")
     ap.add_argument("--item-reduce", type=int, default=-1,
                     help="multi-rank item path (cf_set_option item_reduce 0/1/2; -1 = engine default)")
+    ap.add_argument("--neg-check", type=int, default=-1,
+                    help="negative rejection (cf_set_option neg_check: 1 Pos(u) set, 0 CSR row scan; -1 default)")
     ap.add_argument("--n-users", type=int, default=0, help="override the config's users (rehearsals)")
     ap.add_argument("--n-items", type=int, default=0, help="override the config's items (rehearsals)")
     ap.add_argument("--hot-replicas", type=int, default=0,
@@ -299,6 +301,8 @@ def main():
     eng.set_option("pipeline", args.pipeline)
     if args.hot_replicas:
         eng.set_option("hot_replicas", args.hot_replicas)
+    if args.neg_check >= 0:
+        eng.set_option("neg_check", args.neg_check)
     if args.item_reduce >= 0:
         eng.set_option("item_reduce", args.item_reduce)
     if args.slot_max:

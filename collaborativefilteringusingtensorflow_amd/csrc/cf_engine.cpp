@@ -67,6 +67,10 @@ struct cf_engine {
     int64_t* indptr = nullptr;
     int32_t* indices = nullptr;
     int4* pairs = nullptr;   // (u, i, row start, row length) per interaction
+    unsigned long long* pos_set = nullptr;  // Pos(u) membership set of (u << 32 | i) keys
+    uint64_t pos_mask = 0;
+    int neg_check = 0;       // cf_set_option("neg_check"): 1 = Pos(u) set, 0 = CSR row scan
+    int64_t nnz_set = 0;     // interactions the set was built from
     int64_t* indptr_t = nullptr;
     int32_t* indices_t = nullptr;
     std::vector<int64_t> h_indptr;
@@ -286,6 +290,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.indices = e->indices;
     a.indptr_t = e->indptr_t;
     a.indices_t = e->indices_t;
+    a.pos_set = e->neg_check ? e->pos_set : nullptr;
+    a.pos_mask = e->pos_mask;
     a.U = e->U; a.AU = e->AU; a.GU = e->GU;
     a.V = e->V; a.AV = e->AV; a.GV = e->GV;
     a.b = e->b; a.Ab = e->Ab; a.Gb = e->Gb;
@@ -856,6 +862,7 @@ int cf_destroy(cf_engine* e) {
         }
     for (auto x : e->ev_pool) (void)hipEventDestroy(x);
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
+    dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
     for (int k = 0; k < 2; ++k) {
@@ -900,6 +907,18 @@ int cf_synchronize(cf_engine* e) {
     return CF_OK;
 }
 
+// the Pos(u) set of the current interactions (neg_check = 1), built on demand
+int build_pos_set(cf_engine* e) {
+    dfree(e->pos_set);
+    const int64_t nnz = e->nnz_set;
+    uint64_t cap = 1024;   // load factor <= 1/2
+    while (cap < 2 * (uint64_t)nnz) cap <<= 1;
+    CF_TRY(dalloc(&e->pos_set, (size_t)cap));
+    e->pos_mask = cap - 1;
+    CF_HIP(launch_build_pos_set(e->pairs, nnz, e->pos_set, e->pos_mask, e->stream));
+    return CF_OK;
+}
+
 int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indices, int64_t nnz) {
     CF_TRY(check_engine(e));
     CF_TRY(discard_pending(e));
@@ -921,12 +940,15 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
         }
     }
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
+    dfree(e->pos_set);
     CF_TRY(dalloc(&e->indptr, (size_t)c.n_users + 1));
     CF_TRY(dalloc(&e->indices, (size_t)nnz));
     CF_TRY(dalloc(&e->pairs, (size_t)nnz));
     CF_HIP(hipMemcpyAsync(e->indptr, indptr, ((size_t)c.n_users + 1) * 8, hipMemcpyHostToDevice, e->stream));
     CF_HIP(hipMemcpyAsync(e->indices, indices, (size_t)nnz * 4, hipMemcpyHostToDevice, e->stream));
     CF_HIP(launch_build_pairs(e->indptr, e->indices, c.n_users, e->pairs, e->stream));
+    e->nnz_set = nnz;
+    if (e->neg_check) CF_TRY(build_pos_set(e));
     if (c.model == CF_GBPR && !e->group_source_global) {
         // item -> users transpose (item_posUserList, sampler_gbpr.py:15)
         std::vector<int64_t> tp((size_t)c.n_items + 1, 0);
@@ -1540,6 +1562,13 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_HIP(hipStreamSynchronize(e->stream));
         e->hot_rep = (int)value;
         e->slots_ready = false;
+        return CF_OK;
+    }
+    if (n == "neg_check") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "neg_check must be 0 or 1");
+        CF_TRY(discard_pending(e));
+        e->neg_check = (int)value;
+        if (value == 1 && e->pairs && !e->pos_set) CF_TRY(build_pos_set(e));
         return CF_OK;
     }
     if (n == "item_reduce") {

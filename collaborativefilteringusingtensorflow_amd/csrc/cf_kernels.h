@@ -64,6 +64,10 @@ struct StepArgs {
     const int32_t* __restrict__ indices;    // [nnz] sorted per user
     const int64_t* __restrict__ indptr_t;   // [n_items+1] (GBPR)
     const int32_t* __restrict__ indices_t;  // [nnz] users of each item
+    // Pos(u) membership for the negative draw: open-addressed set of
+    // (u << 32 | i) keys, linear probing (null: scan the user's CSR row)
+    const unsigned long long* __restrict__ pos_set;
+    uint64_t pos_mask;                      // capacity - 1 (power of two)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
     float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
@@ -240,6 +244,8 @@ struct PackArgs {
     int32_t* occU; int32_t* occV; int32_t* bad;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
+hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
+                                uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,
                               int4* pairs, hipStream_t s);
 hipError_t launch_score(const ScoreArgs& a, hipStream_t s);

@@ -283,6 +283,25 @@ __device__ __forceinline__ uint32_t gor8(uint32_t v) {
     return v;
 }
 
+constexpr unsigned long long kPosEmpty = ~0ull;
+
+__device__ __forceinline__ uint64_t pos_slot(unsigned long long key, uint64_t mask) {
+    return mix64(key) & mask;
+}
+
+// j in Pos(u)?  Expected ~1.5 probes at load factor <= 1/2, mostly in one
+// 64-B sector (linear probing)
+__device__ __forceinline__ bool is_positive(const StepArgs& a, int u, int32_t j) {
+    const unsigned long long key = ((unsigned long long)(uint32_t)u << 32) | (uint32_t)j;
+    uint64_t s = pos_slot(key, a.pos_mask);
+    while (true) {
+        const unsigned long long t = a.pos_set[s];
+        if (t == key) return true;
+        if (t == kPosEmpty) return false;
+        s = (s + 1) & a.pos_mask;
+    }
+}
+
 template <int MODEL>
 __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
     constexpr int PGL = kPrepGL;
@@ -315,7 +334,18 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         const int nw = (W - w0 < PGL) ? (W - w0) : PGL;
         const int w = w0 + gl;
         int32_t j = -1;
-        if (a.sample) {
+        if (a.sample && a.pos_set != nullptr) {
+            // negItems = randint(0, n_items), redrawn while j in Pos(u)
+            // (sampler_ranking.py:30-36): negative w takes the first attempt
+            // k = 0, 1, .. of draw(key, (w << 32) + k) outside Pos(u) -- the
+            // same sequence as the row scan below, one set probe per attempt
+            if (gl < nw) {
+                uint64_t ctr = (uint64_t)w << 32;
+                j = draw_item(key, ctr++, a.n_items);
+                while (is_positive(a, u, j)) j = draw_item(key, ctr++, a.n_items);
+                a.occV[B + p * W + w] = j;
+            }
+        } else if (a.sample) {
             // negItems = randint(0, n_items), redrawn while j in Pos(u)
             // (sampler_ranking.py:30-36).  Negative w takes the first
             // candidate of the sequence draw(key, (w << 32) + k), k = 0, 1, ..
@@ -1448,6 +1478,23 @@ __global__ void fill_kernel(float* __restrict__ X, int64_t n, float v) {
     for (int64_t k = t0; k < n; k += nt) X[k] = v;
 }
 
+// the Pos(u) set: one insert per interaction (64-bit CAS, linear probing)
+__global__ void build_pos_set_kernel(const int4* __restrict__ pairs, int64_t nnz,
+                                     unsigned long long* __restrict__ set, uint64_t mask) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t k = t0; k < nnz; k += nt) {
+        const int4 pr = pairs[k];
+        const unsigned long long key = ((unsigned long long)(uint32_t)pr.x << 32) | (uint32_t)pr.y;
+        uint64_t s = pos_slot(key, mask);
+        while (true) {
+            const unsigned long long prev = atomicCAS(set + s, kPosEmpty, key);
+            if (prev == kPosEmpty || prev == key) break;
+            s = (s + 1) & mask;
+        }
+    }
+}
+
 __global__ void build_pairs_kernel(const int64_t* __restrict__ indptr,
                                    const int32_t* __restrict__ indices, int64_t n_users,
                                    int4* __restrict__ pairs) {
@@ -1812,6 +1859,16 @@ hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int
 hipError_t launch_fill(float* X, int64_t n, float v, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, X, n, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
+                                uint64_t mask, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(set, 0xFF, (mask + 1) * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    if (nnz <= 0) return hipSuccess;
+    hipLaunchKernelGGL(build_pos_set_kernel, dim3(grid_for(nnz)), dim3(kBlock), 0, s, pairs, nnz, set,
+                       mask);
     return hipGetLastError();
 }
 

@@ -329,6 +329,13 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                count of step s+1 inside step s's gradient launch, the apply
  *                alone (measured 4.7 us/step slower at cfg2); 0 = one step at
  *                a time, three launches.
+ *   "neg_check"  how the device draw rejects a negative candidate in Pos(u):
+ *                1 = probe an open-addressed set of the (u, i) pairs (16 B
+ *                per interaction, built when selected; ~1 sector per
+ *                candidate), 0 = scan the user's sorted CSR row (default:
+ *                8 candidates per scan; A/B at cfg2 within noise).  The same
+ *                batches either way: both take each negative's first attempt
+ *                outside Pos(u) in the same draw sequence.
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
  *                item occurrences are counted like user ones, a row seen
  *                once stores its gradient row into the bound buffer, a

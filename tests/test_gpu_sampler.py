@@ -123,3 +123,37 @@ def test_same_seed_same_stream(fold1):
     assert not np.array_equal(pa, pc)
     for s in (a, b, c):
         s.close()
+
+
+@pytest.mark.parametrize("model,W,G", [("bpr", 1, 1), ("bpr", 5, 1), ("bpr", 12, 1), ("gbpr", 5, 2)])
+def test_pos_set_draw_equals_row_scan(fold1, model, W, G):
+    """cf_set_option("neg_check"): the Pos(u) set probe and the CSR row scan
+    take the same attempt sequence, so they draw identical batches -- on ml-100k
+    fold 1 and on a dense toy graph where most candidates are rejected."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    rng = np.random.RandomState(5)
+    dense = []
+    for u in range(30):   # 40 items, users own 5..38 of them
+        dense.append(np.sort(rng.choice(40, size=rng.randint(5, 39), replace=False)).astype(np.int32))
+    graphs = [(int(fold1["n_users"]), int(fold1["n_items"]), fold1["train_indptr"], fold1["train_indices"]),
+              (30, 40, np.concatenate([[0], np.cumsum([len(r) for r in dense])]).astype(np.int64),
+               np.concatenate(dense))]
+    for gi, (nu, ni, ip, ix) in enumerate(graphs):
+        out = []
+        for check in (1, 0):
+            e = Engine(model, nu, ni, 8, n_neg=W, gsize=G, seed=11)
+            if gi == 0:   # set built by cf_set_interactions
+                e.set_option("neg_check", check)
+                e.set_interactions(ip, ix)
+            else:         # set built when the option is selected
+                e.set_interactions(ip, ix)
+                e.set_option("neg_check", check)
+            out.append([e.sample(64) for _ in range(12)])
+            e.close()
+        pos = csr_sets(ip, ix)
+        for ba, bb in zip(*out):
+            for xa, xb in zip(ba, bb):
+                assert np.array_equal(xa, xb)
+            pairs, negs = ba[0], ba[1]
+            for (u, i), js in zip(pairs, negs):
+                assert not any(int(j) in pos[u] for j in js)
