@@ -339,6 +339,10 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
             sq += __shfl_xor(sq, 32, 64);
             if (wc == 0 && h == 0) unorm[r] = sq;   // |u|^2 of row r
         }
+        // the A operands are complete before the sweep: otherwise the
+        // wait-count model merges them with the in-flight tile prefetch at the
+        // loop header and every step's first MFMA waits for that prefetch
+        __builtin_amdgcn_s_waitcnt(0);
     }
     int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
     int64_t nxt = INT64_MAX;                 // the train item at the cursor, kept in a register
@@ -415,34 +419,26 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
         float vsq = 0.f;
         const int br = wc * 32 + c;              // B operand row (item) of this lane
-#ifdef CF_FUSED_2ACC   // experiment: two independent MFMA chains, summed at the end
-        floatx16 acc2;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc2[q] = 0.f;
-#endif
 #ifndef CF_FUSED_EXP_NOMFMA   // attribution builds (wrong results by design)
+        auto mfma4 = [&](int t0) {
+            const float4 b4 = *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0));
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
+            if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+        };
+        if (Dh == kAH) {
+            // branch-free: a conditional per k-chunk made the compiler wait
+            // for every outstanding global load (the prefetched next tile)
+            // at each chunk (s_waitcnt vmcnt(0) before the LDS reads)
 #pragma unroll
-        for (int t0 = 0; t0 < kAH; t0 += 4) {
-            if (t0 < Dh) {   // block-uniform
-                const float4 b4 = *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0));
-#ifdef CF_FUSED_2ACC
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
-                acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc2, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
-                acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc2, 0, 0, 0);
-#else
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
-#endif
-                if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
-            }
+            for (int t0 = 0; t0 < kAH; t0 += 4) mfma4(t0);
+        } else {
+#pragma unroll
+            for (int t0 = 0; t0 < kAH; t0 += 4)
+                if (t0 < Dh) mfma4(t0);   // block-uniform
         }
-#endif
-#ifdef CF_FUSED_2ACC
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
 #endif
         float vnorm = 0.f;
         if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
