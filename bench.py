@@ -6,23 +6,31 @@
 Metric (BASELINE.json): BPR triplets/sec (d=64) + achieved HBM GB/s.
 Default workload = configs[1]: BPR-MF on a synthetic implicit-feedback graph,
 1,000,000 users x 100,000 items, 50M interactions (degree 1+Poisson(49),
-Zipf(0.8) item popularity), d=64, W=1, B=65,536 pairs per GPU per step.
+Zipf(0.8) item popularity), d=64, W=1, B=524,288 pairs per GPU per step
+(SURVEY 8(d)'s B=65,536 is timed beside it: "batch_65536").
 A step = one pass of the hot path over one batch, all on the GPU: device
 sampler (epoch bijection + negative rejection) -> gather -> loss ->
 gradient scatter -> duplicate-row sum -> Adagrad apply.  Inputs are resident
 in HBM before the timed region.
 
-N>1 (launched by torch.distributed.run, one rank per GPU): users are sharded
-by contiguous id ranges (each rank generates and samples its own shard), item
-rows are replicated; per step each rank runs the local phase, RCCL all-reduces
-the dense fp32 item gradient, and every replica applies the identical item
-Adagrad.  value = triplets of all ranks / max-over-ranks time ("weak").
+N>1, one rank per GPU: users are sharded by contiguous id ranges (each rank
+generates and samples its own shard), item rows are replicated; per step each
+rank runs the local phase, the dense fp32 item gradient is exchanged over
+RCCL (all-reduce + replicated item Adagrad, or reduce-scatter -> owner
+Adagrad -> all-gather: --item-exchange) and every replica holds the identical
+item table.  value = triplets of all ranks / max-over-ranks time ("weak").
+`bench.py --gpus N` without a launcher starts its own N ranks
+(torch.distributed.run as a child process, before anything touches the GPU)
+and relays rank 0's line; every rank checks that the process group it formed
+has exactly N ranks.
 
 rank 0 prints ONE JSON line; diagnostics go to stderr.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,11 +39,6 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PROFILE_EVERY = 8
 sys.path.insert(0, ROOT)
-
-from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_degrees, synth_graph  # noqa: E402,E501
-from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_group_exchange,  # noqa: E402
-                                                                   make_gpu_sharded, shard_users)
-from collaborativefilteringusingtensorflow_amd._native import KERNELS  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -207,6 +210,83 @@ def cpu_baseline(cfg, indptr, indices, budget_s=12.0):
                       "oracle/cf_oracle.c single thread, %.1f s" % (n1, B, cfg["W"], cfg["desc"], dt1)}
 
 
+def launcher_cmd(n_gpus, argv, port, python=None):
+    """The torch.distributed.run command bench.py starts for itself when it
+    is asked for N > 1 GPUs without a launcher (one rank per GPU, rendezvous
+    on 127.0.0.1)."""
+    return [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node", str(int(n_gpus)), "--master-addr", "127.0.0.1",
+            "--master-port", str(int(port)), os.path.abspath(__file__)] + list(argv)
+
+
+def needs_launch(n_gpus, env=None):
+    env = os.environ if env is None else env
+    return int(n_gpus) > 1 and "WORLD_SIZE" not in env
+
+
+def check_world(formed, n_gpus):
+    """Every rank: the process group must hold exactly --gpus ranks."""
+    if int(formed) != int(n_gpus):
+        raise SystemExit("bench.py: --gpus %d but the process group has %d ranks" % (n_gpus, formed))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(n_gpus, argv):
+    """Run the N ranks as a child process (never exec: this process has not
+    touched the GPU and stays the parent), relay rank 0's JSON line to stdout
+    and everything else to stderr; return the child's exit code."""
+    env = dict(os.environ)
+    env["CF_BENCH_LAUNCHED"] = "1"
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = launcher_cmd(n_gpus, argv, free_port())
+    log("bench.py: launching %d ranks: %s" % (n_gpus, " ".join(cmd)))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, universal_newlines=True)
+    line = None
+    for raw in proc.stdout:
+        t = raw.strip()
+        if t.startswith("{") and '"metric"' in t:
+            line = t
+        elif t:
+            log(t)
+    rc = proc.wait()
+    if line is not None:
+        sys.stdout.write(line + "\n")
+        sys.stdout.flush()
+    return rc
+
+
+def batch_stats(pairs, negs, groups, d, W):
+    """Algorithmic bytes of one drawn batch, from its row multiplicities:
+    * apply: every row seen >= 2 times reads its c gradient rows, reads and
+      writes its row and accumulator: (c + 4) * 4d;
+    * dedup-aware step: every UNIQUE row read + written with its accumulator
+      (16d) + the int32 ids of every occurrence -- the bytes a step must move
+      at the least (SURVEY 8(d)'s full-step figure without the duplicates)."""
+    u = [pairs[:, 0]] + ([groups.reshape(-1)] if groups is not None else [])
+    users = np.concatenate(u)
+    items = np.concatenate([pairs[:, 1], negs.reshape(-1)])
+    out = {}
+    apply_b, uniq = 0.0, 0
+    for ids in (users[users >= 0], items):
+        _, c = np.unique(ids, return_counts=True)
+        uniq += len(c)
+        dup = c[c >= 2]
+        apply_b += float(((dup + 4) * 4 * d).sum())
+        out.setdefault("dup_rows", []).append(int(len(dup)))
+    occ = len(users) + len(items)
+    out["apply_bytes"] = apply_b
+    out["dedup_step_bytes"] = float(uniq * 16 * d + 4 * occ)
+    out["unique_rows"] = int(uniq)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,7 +317,17 @@ def main():
                     help="cf_set_option hot_replicas (0 = engine default)")
     ap.add_argument("--zipf", type=float, default=-1.0,
                     help="override the item popularity exponent (experiments; 0 = uniform)")
+    ap.add_argument("--item-exchange", default=os.environ.get("CF_ITEM_EXCHANGE", "allreduce"),
+                    choices=["allreduce", "rs_ag"],
+                    help="multi-GPU item step: RCCL all-reduce + replicated Adagrad, or "
+                         "reduce-scatter -> owner Adagrad -> all-gather")
+    ap.add_argument("--secondary-batch", type=int, default=65536,
+                    help="also time this batch size (SURVEY 8(d)'s B); 0 = off")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="form the process group, check it, print a line; no GPU work (tests)")
     args = ap.parse_args()
+    if needs_launch(args.gpus):
+        sys.exit(launch(args.gpus, sys.argv[1:]))
     # the JSON line is the only thing on stdout: RCCL / HIP print banners
     # there from native code, so fd 1 points at stderr until the end
     json_out = os.fdopen(os.dup(1), "w")
@@ -254,9 +344,15 @@ def main():
         cfg["zipf"] = args.zipf
         cfg["desc"] += " [experiment: zipf %.2f]" % args.zipf
 
+    from collaborativefilteringusingtensorflow_amd.engine import (Engine, synth_degrees, synth_graph,
+                                                                  synth_item_users)
+    from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_group_exchange,
+                                                                       make_gpu_sharded, shard_users)
+    from collaborativefilteringusingtensorflow_amd._native import KERNELS
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(world, args.gpus)
     dist = None
     torch = None
     # CF_DIST_BACKEND=gloo + CF_SHARE_DEVICE=1 rehearse the N>1 path with all
@@ -273,14 +369,34 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         cfg["desc"] += " [sharded code path, 1 rank]"
-    if sharded:
+    if args.dry_run:
+        backend = os.environ.get("CF_DIST_BACKEND", "gloo")
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+    if sharded or args.dry_run:
         import torch  # noqa: F811
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local_rank)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
+        if args.dry_run:
             dist.init_process_group(backend)
+        else:
+            torch.cuda.set_device(local_rank)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group(backend)
+        check_world(dist.get_world_size(), args.gpus)
+    if args.dry_run:
+        if rank == 0:
+            json_out.write(json.dumps({"metric": "dry-run", "value": 0, "n_gpus": dist.get_world_size(),
+                                       "backend": dist.get_backend(),
+                                       "launched": os.environ.get("CF_BENCH_LAUNCHED") == "1"}) + "\n")
+            json_out.flush()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
 
     # ---- inputs: this rank's user shard of the synthetic graph ----------------
     nu_all, ni, d, W, B = cfg["n_users"], cfg["n_items"], cfg["d"], cfg["W"], cfg["B"]
@@ -313,29 +429,33 @@ def main():
         eng.begin_phase(1)
 
     if sharded and cfg["model"] == "gbpr":
-        # group members come from every shard: the global CSR feeds the
-        # item -> user source, the exchange fetches / returns remote rows
+        # group members come from every shard: the global item -> user CSR
+        # (built natively, cf_synth_item_users) feeds the group draw, the
+        # exchange fetches / returns remote rows
         degs = synth_degrees(nu_all, cfg["mean_degree"], cfg["graph_seed"])
         bounds = [shard_users(degs, world, r)[0] for r in range(world)] + [nu_all]
-        gip, gix = synth_graph(nu_all, ni, cfg["mean_degree"], cfg["zipf"], cfg["graph_seed"],
-                               n_threads=min(16, os.cpu_count() or 1))
-        step, _grad = make_gpu_group_exchange(eng, world, rank, bounds, gip, gix, ni, d, B,
-                                              torch.device("cuda", local_rank))
-        del gip, gix
+        t1 = time.perf_counter()
+        item_csr = synth_item_users(nu_all, ni, cfg["mean_degree"], cfg["zipf"], cfg["graph_seed"],
+                                    n_threads=min(16, os.cpu_count() or 1))
+        log("rank %d: item -> user CSR built in %.1fs" % (rank, time.perf_counter() - t1))
+        step, _items = make_gpu_group_exchange(eng, world, rank, bounds, None, None, ni, d, B,
+                                               torch.device("cuda", local_rank),
+                                               exchange=args.item_exchange, item_csr=item_csr)
+        del item_csr
     elif sharded:
-        step, _grad = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
-                                       torch.device("cuda", local_rank))
+        step, _items = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
+                                        torch.device("cuda", local_rank), exchange=args.item_exchange)
     if sharded:
-        def run(k):
+        def run(k, b=B):
             for _ in range(k):
-                step(B)
+                step(b)
 
         def sync():
             torch.cuda.synchronize()
             dist.barrier()
     else:
-        def run(k):
-            eng.train_steps(B, k, return_loss=False)
+        def run(k, b=B):
+            eng.train_steps(b, k, return_loss=False)
 
         def sync():
             eng.synchronize()
@@ -345,9 +465,10 @@ def main():
     # timed region: HIP events around the dominant kernel only (an event pair
     # around every launch would add ~20 us per step to the loop)
     eng.profile_reset()
-    # pipeline 2 (default): the dominant launch is the gradient of step s fused
-    # with the draw + count of step s+1 ("grad_prep"); otherwise "step"
-    dom = "step"
+    # pipeline 2: the gradient launch of step s also carries the draw + count
+    # of step s+1 ("grad_prep"); otherwise (pipeline 1, the default) the
+    # gradient launch is "step" and the draw rides in the apply launch
+    dom = "grad_prep" if (args.pipeline == 2 and not sharded) else "step"
     eng.set_option("profile_mask", 1 << KERNELS[dom])
     # every PROFILE_EVERY-th launch is timed: an event pair on every launch
     # costs the loop ~6 us/step (cfg2), sampled launches ~1/PROFILE_EVERY of it
@@ -385,6 +506,32 @@ def main():
     loss = eng.take_loss()
     log("rank %d: loss accumulated %.4e" % (rank, loss))
 
+    # SURVEY 8(d)'s batch (65,536 pairs per GPU) on the same engine and graph
+    secondary = None
+    B2 = args.secondary_batch
+    if B2 and B2 != B and B2 <= len(indices):
+        run(max(2, args.warmup // 2), B2)
+        sync()
+        t0 = time.perf_counter()
+        run(args.steps, B2)
+        sync()
+        el2 = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el2], dtype=torch.float64, device="cuda:%d" % local_rank)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2 = float(t.item())
+        secondary = {"batch_pairs_per_gpu": B2, "steps": args.steps,
+                     "value": B2 * W * args.steps * world / el2, "unit": "triplets/s",
+                     "ms_per_step": 1e3 * el2 / args.steps}
+    # one drawn batch's row multiplicities -> the apply + draw launch's and a
+    # dedup-aware step's algorithmic bytes (batch_stats)
+    st = None
+    try:
+        bp, bn, bg = eng.sample(B)
+        st = batch_stats(bp, bn, bg, d, W)
+    except Exception as ex:  # diagnostics only
+        log("batch stats failed: %r" % (ex,))
+
     trip_per_step = B * W
     total_trip = trip_per_step * args.steps * world
     value = total_trip / elapsed
@@ -417,6 +564,32 @@ def main():
                 "timed_launches": step_n,
                 "timed_every": PROFILE_EVERY if not args.no_profile else None}
     full_b = full_step_bytes_per_pair(d, W) * B * args.steps * world
+    roofline_apply = None
+    ap_k = kernels.get("apply_prep")
+    if st is not None and ap_k:
+        dbp = draw_bytes_per_pair(W, Gm, mean_row) * B
+        ab = st["apply_bytes"] + dbp
+        roofline_apply = {
+            "kernel": "apply_prep_kernel: Adagrad of the duplicated rows of step s (slot sums) "
+                      "+ device draw + count of step s+1",
+            "bound": "hbm", "achieved": ab / (1e-6 * ap_k["avg_us"]) / 1e9, "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": ab / (1e-6 * ap_k["avg_us"]) / 1e9 / HBM_PEAK_GBPS,
+            "bytes_per_launch": ab, "apply_bytes": st["apply_bytes"], "draw_bytes": dbp,
+            "bytes_def": "sum over rows seen c >= 2 times in the batch of (c + 4) * 4d (c gradient "
+                         "rows read, row + accumulator read and written) + the draw bytes "
+                         "B*(8 + 16 + 4*E[row] + 12(2+W)), E[row] = %.1f" % mean_row,
+            "avg_launch_us": ap_k["avg_us"], "dup_rows_user_item": st["dup_rows"]}
+    dedup = None
+    if st is not None:
+        dedup = {"bytes_per_step": st["dedup_step_bytes"], "unique_rows": st["unique_rows"],
+                 "GBps": st["dedup_step_bytes"] * args.steps * world / elapsed / 1e9,
+                 "def": "unique rows touched x 16d (row + accumulator read and written) + 4 B per "
+                        "occurrence id, one drawn batch"}
+    dist_info = {}
+    if sharded:
+        dist_info = {"world_size_formed": dist.get_world_size(), "backend": dist.get_backend(),
+                     "item_exchange": args.item_exchange,
+                     "launched_by_bench": os.environ.get("CF_BENCH_LAUNCHED") == "1"}
     out = {
         "metric": "BPR triplets/sec/GPU (d=64) + achieved HBM GB/s; NDCG@10 vs ref",
         "value": value, "unit": "triplets/s", "n_gpus": world, "steps": args.steps,
@@ -426,22 +599,33 @@ def main():
         "config": {"workload": cfg["desc"], "model": cfg["model"], "n_users": nu_all,
                    "n_items": ni, "nnz_rank0": int(len(indices)), "d": d, "W": W,
                    "batch_pairs_per_gpu": B, "global_batch": B * world,
-                   "parallelism": ("dp%d user-sharded, RCCL item-grad all-reduce" % world
+                   "parallelism": ("dp%d user-sharded, RCCL item-grad %s" % (
+                                       world, "all-reduce" if args.item_exchange == "allreduce"
+                                       else "reduce-scatter + owner Adagrad + all-gather")
                                    + (" + group-member all-to-all" if cfg["model"] == "gbpr" else ""))
                    if world > 1 else "single GPU"},
         "per_gpu_value": value / world,
         "full_step_algorithmic_GBps": full_b / elapsed / 1e9,
         "roofline": roofline,
+        "roofline_apply_prep": roofline_apply,
+        "dedup_step": dedup,
+        "batch_65536": secondary,
         "kernels": kernels,
     }
+    out["config"].update(dist_info)
     if args.score_pass or args.config == "cfg5":
         users = np.arange(u1 - u0, dtype=np.int32)
         eng.score_topk(users[:1024], 10)          # warm-up
         sync()
+        eng.profile_reset()
+        eng.set_option("profile_mask", 1 << KERNELS["topk"])
+        eng.profile(True)
         t0 = time.perf_counter()
         eng.score_topk(users, 10, exclude_train=True)
         sync()
         ts = time.perf_counter() - t0
+        eng.profile(False)
+        tk_ms, tk_n = eng.profile_read("topk")
         if world > 1:
             t = torch.tensor([ts], dtype=torch.float64, device="cuda:%d" % local_rank)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -450,7 +634,10 @@ def main():
         out["score_pass"] = {"users": nu_all, "items": ni, "d": d, "k": 10, "seconds": ts,
                              "TFLOPs": flop / ts / 1e12,
                              "frac_fp32_mfma_peak": flop / ts / 1e12 / (157.3 * world),
-                             "kernel": "fused_topk_kernel (v_mfma_f32_32x32x2_f32 + streaming top-k)"}
+                             "kernel": "fused_topk_kernel (v_mfma_f32_32x32x2_f32 + streaming top-k)",
+                             "kernel_ms_hip_events": tk_ms if tk_n else None,
+                             "kernel_TFLOPs": (2.0 * (u1 - u0) * ni * d / (1e-3 * tk_ms) / 1e12)
+                             if tk_n and tk_ms > 0 else None}
     if rank == 0 and world == 1 and not args.no_ndcg:
         try:
             out["ndcg10_vs_ref"] = ndcg_cfg1(local_rank)

@@ -88,6 +88,11 @@ SIGNATURES = {
     "cf_bind_item_grad": (ctypes.c_int, [_P, _P, _I64]),
     "cf_step_local": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_items": (ctypes.c_int, [_P]),
+    "cf_step_local_draw": (ctypes.c_int, [_P, _I32]),
+    "cf_bind_item_grad_split": (ctypes.c_int, [_P, _P, _I64, _P, _I64]),
+    "cf_clear_item_grad": (ctypes.c_int, [_P]),
+    "cf_step_items_range": (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
+    "cf_bind_table": (ctypes.c_int, [_P, _I32, _P, _I64]),
     "cf_step_local_grad": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_local_apply": (ctypes.c_int, [_P, _I32]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
@@ -129,6 +134,8 @@ SIGNATURES = {
     "cf_ens_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
     "cf_synth_degrees": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64]),
     "cf_synth_items": (ctypes.c_int, [_I64, ctypes.c_double, _U64, _I64, _I64, _PI64, _PI32, _I32]),
+    "cf_synth_item_users": (ctypes.c_int, [_I64, _I64, ctypes.c_double, ctypes.c_double, _U64, _PI64,
+                                           _PI32, _I32]),
 }
 
 _lib = None

@@ -123,6 +123,7 @@ struct cf_engine {
 
     // device sampler position
     int64_t epoch = 0, batch = 0;
+    int64_t full_row_user = -1;   // a user with every item as a positive (no negative exists)
     int sampler_B = 0;
 
     // user sharding + GBPR group exchange (cf_set_shard / cf_bind_exchange /
@@ -157,6 +158,15 @@ struct cf_engine {
     StepArgs x_args{};
     int x_set = 0;
     int x_B = 0;
+
+    // tables bound to caller device memory (cf_bind_table): the engine's own
+    // buffer of table t while it is bound, else null
+    float* own_tab[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // item occurrences of the last local gradient launch: the rows of the
+    // bound item gradient that cf_clear_item_grad re-zeroes
+    const int32_t* last_occV = nullptr;
+    int64_t last_nV = 0;
+    int lg_done_set = -1;     // buffer set of the last cf_step_local_apply
 
     // model state
     int phase = 0;
@@ -332,6 +342,9 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
 int sampler_args(cf_engine* e, int B, StepArgs* a) {
     if (!e->pairs) return fail(CF_ESTATE, "no interactions: call cf_set_interactions first");
     if ((int64_t)B > e->nnz) return fail(CF_EINVAL, "batch size exceeds the number of interactions");
+    if (e->full_row_user >= 0)   // the reference's rejection loop would never end for this user
+        return fail(CF_EINVAL, "user " + std::to_string(e->full_row_user) +
+                                   " has every item as a positive; the device sampler cannot draw a negative");
     if (e->sampler_B != B) {
         if (e->sampler_B != 0 && e->batch != 0) {
             e->epoch += 1;
@@ -614,6 +627,7 @@ int run_items_dense(cf_engine* e) {
     d.lr = c.lr;
     d.clip_norm = c.clip_norm;
     d.clip = c.model == CF_CML ? 1 : 0;
+    d.zero_g = 1;
     d.n_rows = c.n_items;
     d.X = e->V; d.A = e->AV; d.G = e->GV;
     d.b = e->b; d.Ab = e->Ab; d.Gb = e->Gb;
@@ -681,6 +695,24 @@ float* table_ptr(cf_engine* e, int t, int64_t* n) {
     }
 }
 
+int check_device_ptr(const void* p, const char* what) {
+    hipPointerAttribute_t attr;
+    if (!p || hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeDevice)
+        return fail(CF_EINVAL, std::string(what) + " is not device memory");
+    return CF_OK;
+}
+
+float** table_slot(cf_engine* e, int t) {
+    switch (t) {
+        case CF_TABLE_USER: return &e->U;
+        case CF_TABLE_ITEM: return &e->V;
+        case CF_TABLE_BIAS: return &e->b;
+        case CF_TABLE_ACC_USER: return &e->AU;
+        case CF_TABLE_ACC_ITEM: return &e->AV;
+        case CF_TABLE_ACC_BIAS: return &e->Ab;
+        default: return nullptr;
+    }
+}
 
 // fused fp32-MFMA scoring + streaming top-k: no score matrix in HBM
 int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclude_train,
@@ -861,6 +893,8 @@ int cf_destroy(cf_engine* e) {
             (void)hipEventDestroy(pr.second);
         }
     for (auto x : e->ev_pool) (void)hipEventDestroy(x);
+    for (int t = 0; t < 6; ++t)   // bound tables belong to the caller
+        if (e->own_tab[t]) *table_slot(e, t) = e->own_tab[t];
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
@@ -927,12 +961,13 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     if (nnz < 1) return fail(CF_EINVAL, "no interactions");
     if (nnz > INT32_MAX) return fail(CF_EINVAL, "nnz must be < 2^31 (int32 row offsets in the pair records)");
     if (indptr[0] != 0 || indptr[c.n_users] != nnz) return fail(CF_EINVAL, "indptr does not span nnz");
+    int64_t full_row = -1;
     for (int64_t u = 0; u < c.n_users; ++u) {
         const int64_t rb = indptr[u], re = indptr[u + 1];
         if (re < rb) return fail(CF_EINVAL, "indptr not monotone");
-        if (re - rb >= c.n_items)
-            return fail(CF_EINVAL, "user " + std::to_string(u) +
-                                       " has every item as a positive; no negative can be drawn");
+        // only the device sampler needs a negative for every user; host-fed
+        // and tuple models skip such users like sampler_uitj_ranking.py:28
+        if (re - rb >= c.n_items && full_row < 0) full_row = u;
         for (int64_t k = rb; k < re; ++k) {
             const int32_t it = indices[k];
             if (it < 0 || it >= c.n_items) return fail(CF_EINVAL, "item id out of range");
@@ -966,6 +1001,7 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     }
     CF_HIP(hipStreamSynchronize(e->stream));
     e->h_indptr.assign(indptr, indptr + c.n_users + 1);
+    e->full_row_user = full_row;
     e->nnz = nnz;
     e->epoch = 0;
     e->batch = 0;
@@ -1201,6 +1237,8 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
+    e->last_occV = a.occV;
+    e->last_nV = (int64_t)B * items_per_pair(e->cfg);
     if (a.items_grad_only && a.capV > 0) {
         // duplicated item rows: slot rows summed into the bound buffer now, so
         // it holds this rank's complete item gradient when the all-reduce starts
@@ -1224,6 +1262,7 @@ int cf_step_local_apply(cf_engine* e, int32_t next_B) {
     ApplyArgs p = apply_args(e, e->lg_args, e->lg_B, k, e->loss);
     if (p.items_grad_only) p.count_items = 0;  // reduced in cf_step_local_grad
     e->lg_stage = 0;
+    e->lg_done_set = k;
     if (next_B > 0 && next_B <= e->Bcap && e->prep_side == 0) {
         // draw + count the next batch in the same launch (other buffer set)
         StepArgs nx = base_step_args(e, next_B, k ^ 1);
@@ -1247,6 +1286,32 @@ int cf_step_local_apply(cf_engine* e, int32_t next_B) {
     return pending_clips(e);
 }
 
+int cf_step_local_draw(cf_engine* e, int32_t B) {
+    CF_TRY(check_engine(e));
+    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "the split step needs dense_item_apply=1");
+    CF_TRY(check_not_xchg(e));
+    if (e->lg_stage != 0 || e->lg_done_set < 0)
+        return fail(CF_ESTATE, "cf_step_local_draw follows cf_step_local_apply");
+    if (e->pend) return fail(CF_ESTATE, "the next batch is already drawn");
+    if (B < 1 || B > e->Bcap) return fail(CF_EINVAL, "B must be in [1, the largest batch stepped so far]");
+    const int k = e->lg_done_set;
+    StepArgs nx = base_step_args(e, B, k ^ 1);
+    e->pend_epoch = e->epoch;
+    e->pend_batch = e->batch;
+    e->pend_sampler_B = e->sampler_B;
+    CF_TRY(sampler_args(e, B, &nx));
+    {
+        ProfScope ps(e, CF_K_SAMPLE);
+        CF_HIP(launch_prep(nx, e->stream));
+    }
+    e->pend = true;
+    e->pend_args = nx;
+    e->pend_set = k ^ 1;
+    e->pend_B = B;
+    e->set = k;
+    return CF_OK;
+}
+
 int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
                   const int32_t* groups) {
     CF_TRY(cf_step_local_grad(e, B, pairs, negs, groups));
@@ -1256,7 +1321,120 @@ int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
 int cf_step_items(cf_engine* e) {
     CF_TRY(check_engine(e));
     if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "cf_step_items needs dense_item_apply=1");
+    e->last_nV = 0;   // the dense apply re-zeroes what it consumes
     return run_items_dense(e);
+}
+
+int cf_bind_table(cf_engine* e, int32_t t, void* ptr, int64_t n) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (t != CF_TABLE_ITEM && t != CF_TABLE_BIAS && t != CF_TABLE_ACC_ITEM && t != CF_TABLE_ACC_BIAS)
+        return fail(CF_EINVAL, "only the item-side tables (item, bias and their accumulators) can be bound");
+    int64_t want = 0;
+    float** slot = table_slot(e, t);
+    if (!table_ptr(e, t, &want)) return fail(CF_EINVAL, "table not present in this model");
+    CF_TRY(discard_pending(e));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    if (!ptr) {
+        if (e->own_tab[t]) {
+            CF_HIP(hipMemcpyAsync(e->own_tab[t], *slot, (size_t)want * 4, hipMemcpyDeviceToDevice, e->stream));
+            CF_HIP(hipStreamSynchronize(e->stream));
+            *slot = e->own_tab[t];
+            e->own_tab[t] = nullptr;
+        }
+        return CF_OK;
+    }
+    if (n < want) return fail(CF_EINVAL, "bound table must hold at least " + std::to_string(want) + " floats");
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess || attr.type != hipMemoryTypeDevice)
+        return fail(CF_EINVAL, "bound table is not device memory");
+    if ((float*)ptr == *slot) return CF_OK;
+    CF_HIP(hipMemcpyAsync(ptr, *slot, (size_t)want * 4, hipMemcpyDeviceToDevice, e->stream));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    if (!e->own_tab[t]) e->own_tab[t] = *slot;
+    *slot = (float*)ptr;
+    (void)c;
+    return CF_OK;
+}
+
+int cf_bind_item_grad_split(cf_engine* e, void* gv, int64_t gv_n, void* gb, int64_t gb_n) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (!c.dense_item_apply) return fail(CF_ESTATE, "cf_bind_item_grad_split needs dense_item_apply=1");
+    if (!gv) {
+        e->GV = e->GV_own;
+        e->Gb = e->Gb_own;
+        return CF_OK;
+    }
+    const int64_t id = c.n_items * (int64_t)c.n_factors;
+    if (gv_n < id) return fail(CF_EINVAL, "item-grad buffer must hold at least " + std::to_string(id) + " floats");
+    CF_TRY(check_device_ptr(gv, "item-grad buffer"));
+    if (has_bias(c)) {
+        if (gb_n < c.n_items) return fail(CF_EINVAL, "bias-grad buffer must hold at least n_items floats");
+        CF_TRY(check_device_ptr(gb, "bias-grad buffer"));
+    }
+    e->GV = (float*)gv;
+    e->Gb = has_bias(c) ? (float*)gb : e->Gb_own;
+    CF_HIP(hipMemsetAsync(gv, 0, (size_t)gv_n * 4, e->stream));
+    if (has_bias(c)) CF_HIP(hipMemsetAsync(gb, 0, (size_t)gb_n * 4, e->stream));
+    e->last_nV = 0;
+    return CF_OK;
+}
+
+int cf_clear_item_grad(cf_engine* e) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (!c.dense_item_apply) return fail(CF_ESTATE, "cf_clear_item_grad needs dense_item_apply=1");
+    if (e->last_nV <= 0) return CF_OK;
+    float* gb = has_bias(c) ? e->Gb : nullptr;
+    if (2 * e->last_nV < c.n_items) {
+        CF_HIP(launch_zero_rows(e->last_occV, e->last_nV, e->GV, gb, c.n_factors, e->stream));
+    } else {
+        CF_HIP(hipMemsetAsync(e->GV, 0, (size_t)c.n_items * c.n_factors * 4, e->stream));
+        if (gb) CF_HIP(hipMemsetAsync(gb, 0, (size_t)c.n_items * 4, e->stream));
+    }
+    e->last_nV = 0;
+    return CF_OK;
+}
+
+int cf_step_items_range(cf_engine* e, int64_t row0, int64_t row1, const void* grad,
+                        const void* grad_bias) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (!c.dense_item_apply) return fail(CF_ESTATE, "cf_step_items_range needs dense_item_apply=1");
+    if (row0 < 0 || row1 < row0) return fail(CF_EINVAL, "bad row range");
+    row0 = std::min<int64_t>(row0, c.n_items);
+    row1 = std::min<int64_t>(row1, c.n_items);
+    if (row1 > row0) {
+        CF_TRY(check_device_ptr(grad, "grad"));
+        if (has_bias(c)) CF_TRY(check_device_ptr(grad_bias, "grad_bias"));
+        DenseArgs d{};
+        d.d = c.n_factors;
+        d.lr = c.lr;
+        d.clip_norm = c.clip_norm;
+        d.clip = c.model == CF_CML ? 1 : 0;
+        d.zero_g = 0;
+        d.n_rows = row1 - row0;
+        d.X = e->V + row0 * c.n_factors;
+        d.A = e->AV + row0 * c.n_factors;
+        d.G = (float*)grad;
+        if (has_bias(c)) {
+            d.b = e->b + row0;
+            d.Ab = e->Ab + row0;
+            d.Gb = (float*)grad_bias;
+        }
+        {
+            ProfScope ps(e, CF_K_APPLY_DENSE);
+            CF_HIP(launch_apply_dense(d, e->stream));
+        }
+        if (e->need_clip_V) {   // CML: this rank's rows of the pending full clip
+            ProfScope ps(e, CF_K_CLIP);
+            CF_HIP(launch_clip_full(e->V + row0 * c.n_factors, row1 - row0, c.n_factors, c.clip_norm,
+                                    e->stream));
+        }
+    }
+    e->need_clip_V = false;
+    return CF_OK;
 }
 
 // ---- user sharding + GBPR group exchange ------------------------------------
@@ -1307,13 +1485,6 @@ int cf_set_group_source(cf_engine* e, const int64_t* indptr_t, const int32_t* in
     CF_HIP(hipMemcpy(e->indptr_t, indptr_t, ((size_t)c.n_items + 1) * 8, hipMemcpyHostToDevice));
     CF_HIP(hipMemcpy(e->indices_t, indices_t, (size_t)nnz * 4, hipMemcpyHostToDevice));
     e->group_source_global = true;
-    return CF_OK;
-}
-
-static int check_device_ptr(const void* p, const char* what) {
-    hipPointerAttribute_t attr;
-    if (!p || hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeDevice)
-        return fail(CF_EINVAL, std::string(what) + " is not device memory");
     return CF_OK;
 }
 
@@ -1411,6 +1582,8 @@ int cf_xchg_grad(cf_engine* e) {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
+    e->last_occV = a.occV;
+    e->last_nV = (int64_t)e->x_B * items_per_pair(e->cfg);
     e->x_stage = 3;
     return CF_OK;
 }

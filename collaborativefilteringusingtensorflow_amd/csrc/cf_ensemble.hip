@@ -493,6 +493,7 @@ int dense_apply(cf_ensemble* e, float* X, float* A, float* G, int64_t rows) {
     d.d = e->d;
     d.lr = e->lr;
     d.clip = 0;
+    d.zero_g = 1;
     d.n_rows = rows;
     d.X = X; d.A = A; d.G = G;
     ENS_HIP(launch_apply_dense(d, e->stream));

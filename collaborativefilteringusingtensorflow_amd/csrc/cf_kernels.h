@@ -155,6 +155,8 @@ struct DenseArgs {
     float lr;
     float clip_norm;
     int clip;
+    int zero_g;          // re-zero the consumed gradient rows (the all-reduced
+                         // buffer is reused; a reduce-scatter slice is not)
     int64_t n_rows;
     float* __restrict__ X; float* __restrict__ A; float* __restrict__ G;
     float* __restrict__ b; float* __restrict__ Ab; float* __restrict__ Gb;  // nullable
@@ -220,6 +222,8 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s);
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& next, hipStream_t s);
 
 hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s);
+// zero the rows of G (and Gb, nullable) that a batch's occurrences touched
+hipError_t launch_zero_rows(const int32_t* occ, int64_t n, float* G, float* Gb, int d, hipStream_t s);
 hipError_t launch_clip_full(float* X, int64_t n_rows, int d, float clip_norm, hipStream_t s);
 hipError_t launch_init_normal(float* X, int64_t n, float mean, float stddev, int truncated,
                               uint64_t seed, hipStream_t s);

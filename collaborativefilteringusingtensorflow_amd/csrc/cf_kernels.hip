@@ -1420,7 +1420,7 @@ __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
         if (gor(nz) == 0u) continue;  // group-uniform
         float x[EPL];
         gload<EPL>(a.X, r, a.d, gl, x);
-        row_zero<EPL>(a.G + r * (int64_t)a.d, a.d, gl);
+        if (a.zero_g) row_zero<EPL>(a.G + r * (int64_t)a.d, a.d, gl);
         gapply<EPL>(a.X, a.A, r, a.d, gl, x, g, a.lr, a.clip != 0, a.clip_norm);
     }
     if (a.b != nullptr) {
@@ -1432,9 +1432,26 @@ __global__ __launch_bounds__(kBlock) void apply_dense_kernel(DenseArgs a) {
                 const float acc = fmaf(g, g, a.Ab[r]);
                 a.Ab[r] = acc;
                 a.b[r] -= adagrad_delta(a.lr, g, acc);
-                a.Gb[r] = 0.f;
+                if (a.zero_g) a.Gb[r] = 0.f;
             }
         }
+    }
+}
+
+// the rows of the dense item gradient a batch touched, re-zeroed after the
+// collective that consumed them (cheaper than a memset when the batch touches
+// fewer rows than the table has)
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void zero_rows_kernel(const int32_t* __restrict__ occ, int64_t n,
+                                                           float* __restrict__ G, float* __restrict__ Gb,
+                                                           int d) {
+    const int gl = threadIdx.x & (kGL - 1);
+    const int64_t g0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
+    const int64_t ng = ((int64_t)gridDim.x * kBlock) >> 4;
+    for (int64_t q = g0; q < n; q += ng) {
+        const int32_t r = occ[q];
+        row_zero<EPL>(G + (int64_t)r * d, d, gl);
+        if (Gb != nullptr && gl == 0) Gb[r] = 0.f;
     }
 }
 
@@ -1825,6 +1842,19 @@ hipError_t launch_apply_dense(const DenseArgs& a, hipStream_t s) {
         case 4: hipLaunchKernelGGL(apply_dense_kernel<4>, grid, block, 0, s, a); break;
         case 8: hipLaunchKernelGGL(apply_dense_kernel<8>, grid, block, 0, s, a); break;
         default: hipLaunchKernelGGL(apply_dense_kernel<16>, grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_zero_rows(const int32_t* occ, int64_t n, float* G, float* Gb, int d, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const dim3 grid(row_grid(n)), block(kBlock);
+    switch (epl_for(d)) {
+        case 1: hipLaunchKernelGGL(zero_rows_kernel<1>, grid, block, 0, s, occ, n, G, Gb, d); break;
+        case 2: hipLaunchKernelGGL(zero_rows_kernel<2>, grid, block, 0, s, occ, n, G, Gb, d); break;
+        case 4: hipLaunchKernelGGL(zero_rows_kernel<4>, grid, block, 0, s, occ, n, G, Gb, d); break;
+        case 8: hipLaunchKernelGGL(zero_rows_kernel<8>, grid, block, 0, s, occ, n, G, Gb, d); break;
+        default: hipLaunchKernelGGL(zero_rows_kernel<16>, grid, block, 0, s, occ, n, G, Gb, d); break;
     }
     return hipGetLastError();
 }

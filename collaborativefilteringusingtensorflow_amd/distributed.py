@@ -51,31 +51,155 @@ def local_csr(indptr, indices, u0, u1):
     return (indptr[u0:u1 + 1] - lo).astype(np.int64), np.asarray(indices[lo:hi], dtype=np.int32)
 
 
+def _gloo_dev(dist, t, group):
+    """gloo stages device tensors through host copies (the collectives below
+    are called on host copies and copied back)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+class _Works(object):
+    def __init__(self, works):
+        self.works = [w for w in works if w is not None]
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+class AllReduceItems(object):
+    """Replicated item Adagrad: the dense item gradient (this rank's sum in
+    ``grad``) is all-reduced, then every replica applies the identical update
+    (``step_items``)."""
+
+    name = "allreduce"
+    draw_with_apply = True   # the next draw rides in the user-apply launch
+
+    def __init__(self, grad, group=None):
+        self.grad = grad
+        self.group = group
+
+    def overlap(self, dist):
+        return self.grad.is_cuda and dist.get_backend(self.group) != "gloo"
+
+    def reduce(self, dist, async_op):
+        return dist.all_reduce(self.grad, group=self.group, async_op=async_op)
+
+    def apply(self, be):
+        be.step_items()
+
+    def gather(self, dist, async_op):
+        return None
+
+    def sync_state(self, dist):
+        return None
+
+
+class ReduceScatterItems(object):
+    """Item-range ownership.  The dense item gradient (padded to world * chunk
+    rows) is reduce-scattered: rank r receives the cross-rank sum of rows
+    [r*chunk, (r+1)*chunk), applies Adagrad to them alone
+    (``step_items_range``) and the updated rows are all-gathered into every
+    replica's table.  The same bytes cross xGMI as an all-reduce; the item
+    Adagrad (and the accumulator rows it keeps current) is 1/world of the
+    replicated one, and the user apply and the next draw each run beside one
+    of the two collectives.  TF1's sum-before-update semantics are unchanged:
+    every row's update sees the sum over the global batch.
+
+    ``grad`` [world*chunk*d] (+ ``grad_bias`` [world*chunk], GBPR) are the
+    bound gradient buffers, ``tables`` the (padded, flat) table storages to
+    all-gather after the owner update as (tensor, row width) -- V and b --
+    and ``state`` the accumulators gathered by ``sync_state``."""
+
+    name = "rs_ag"
+    draw_with_apply = False  # the next draw runs beside the all-gather
+
+    def __init__(self, grad, grad_slice, tables, chunk, rank, grad_bias=None, bias_slice=None,
+                 state=(), group=None):
+        self.grad, self.grad_slice = grad, grad_slice
+        self.grad_bias, self.bias_slice = grad_bias, bias_slice
+        self.tables = list(tables)
+        self.state = list(state)
+        self.chunk, self.rank = int(chunk), int(rank)
+        self.row0, self.row1 = self.rank * self.chunk, (self.rank + 1) * self.chunk
+        self.group = group
+
+    def overlap(self, dist):
+        return self.grad.is_cuda and dist.get_backend(self.group) != "gloo"
+
+    def _rs(self, dist, out, inp, async_op):
+        if _gloo_dev(dist, inp, self.group):
+            o = out.cpu()
+            dist.reduce_scatter_tensor(o, inp.cpu(), group=self.group)
+            out.copy_(o)
+            return None
+        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
+
+    def _ag(self, dist, full, width, async_op):
+        lo, hi = self.row0 * width, self.row1 * width
+        if _gloo_dev(dist, full, self.group):
+            f = full.cpu()
+            dist.all_gather_into_tensor(f, f[lo:hi].clone(), group=self.group)
+            full.copy_(f)
+            return None
+        # in place: this rank's chunk of the output is the input
+        return dist.all_gather_into_tensor(full, full[lo:hi], group=self.group, async_op=async_op)
+
+    def reduce(self, dist, async_op):
+        w = [self._rs(dist, self.grad_slice, self.grad, async_op)]
+        if self.grad_bias is not None:
+            w.append(self._rs(dist, self.bias_slice, self.grad_bias, async_op))
+        return _Works(w)
+
+    def apply(self, be):
+        # the full buffers are consumed: re-zero the touched rows for the next
+        # step, then the owner's Adagrad on its rows
+        be.clear_item_grad()
+        be.step_items_range(self.row0, self.row1, self.grad_slice, self.bias_slice)
+
+    def gather(self, dist, async_op):
+        return _Works([self._ag(dist, t, w, async_op) for t, w in self.tables])
+
+    def sync_state(self, dist):
+        """All-gather the owners' accumulator rows (checkpoint / inspection:
+        only the owner keeps its range current during training)."""
+        for t, w in self.state:
+            self._ag(dist, t, w, False)
+
+
+def _items(items, group):
+    import torch
+    return AllReduceItems(items, group) if torch.is_tensor(items) else items
+
+
 class ShardedStep(object):
-    """One data-parallel optimizer step: local phase -> all-reduce -> items.
+    """One data-parallel optimizer step: local phase -> item exchange -> items.
 
-    With a backend that splits the local phase (step_local_grad /
-    step_local_apply, include/cf_engine.h) the all-reduce is issued as soon
-    as the item gradient is complete and runs beside the user update and the
-    draw of the next batch; the item update waits for it."""
+    ``items`` is the item exchange (``AllReduceItems`` / ``ReduceScatterItems``;
+    a bare tensor means the all-reduce of that item-gradient tensor).  With a
+    backend that splits the local phase (step_local_grad / step_local_apply,
+    include/cf_engine.h) the exchange is issued as soon as the item gradient
+    is complete and runs beside the user update and the draw of the next
+    batch; the item update waits for it."""
 
-    def __init__(self, backend, item_grad, process_group=None, draw_ahead=True):
+    def __init__(self, backend, items, process_group=None, draw_ahead=True):
         import torch.distributed as dist
         self.backend = backend
-        self.item_grad = item_grad
+        self.items = _items(items, process_group)
+        self.item_grad = self.items.grad
         self.group = process_group
         self.draw_ahead = draw_ahead
         self._dist = dist
 
     def __call__(self, batch_size=None, pairs=None, negs=None, groups=None):
-        be = self.backend
+        be, x, dist = self.backend, self.items, self._dist
         if not hasattr(be, "step_local_grad"):
             if pairs is None:
                 be.step_local(batch_size)
             else:
                 be.step_local(pairs=pairs, negs=negs, groups=groups)
-            self._dist.all_reduce(self.item_grad, group=self.group)
-            be.step_items()
+            x.reduce(dist, False)
+            x.apply(be)
+            x.gather(dist, False)
             return
         if pairs is None:
             be.step_local_grad(batch_size)
@@ -83,13 +207,22 @@ class ShardedStep(object):
             be.step_local_grad(pairs=pairs, negs=negs, groups=groups)
         # gloo stages device tensors through the host: overlap buys nothing
         # there (and its async device path serialises both ranks of a shared
-        # GPU), so only RCCL gets the asynchronous all-reduce
-        overlap = self.item_grad.is_cuda and self._dist.get_backend(self.group) != "gloo"
-        work = self._dist.all_reduce(self.item_grad, group=self.group, async_op=overlap)
-        be.step_local_apply(batch_size if (pairs is None and self.draw_ahead) else 0)
-        if overlap:
+        # GPU), so only RCCL gets the asynchronous collectives
+        overlap = x.overlap(dist)
+        nb = batch_size if (pairs is None and self.draw_ahead) else 0
+        work = x.reduce(dist, overlap)
+        be.step_local_apply(nb if x.draw_with_apply else 0)
+        if overlap and work is not None:
             work.wait()
-        be.step_items()
+        x.apply(be)
+        work = x.gather(dist, overlap)
+        if nb and not x.draw_with_apply:
+            be.step_local_draw(nb)
+        if overlap and work is not None:
+            work.wait()
+
+    def sync_state(self):
+        self.items.sync_state(self._dist)
 
 
 def share_stream(engine, device):
@@ -106,16 +239,53 @@ def share_stream(engine, device):
     return cur
 
 
-def make_gpu_sharded(engine, n_items, d, with_bias, device):
-    """Bind a torch tensor as the engine's item-gradient buffer, run the
-    engine on torch's current stream so RCCL orders after it, and return the
-    step callable."""
+def _bind_rs_items(engine, n_items, d, with_bias, device, group=None):
+    """Padded torch buffers for item-range ownership, bound to the engine:
+    gradient (+ bias gradient), the table storages V (+ b) the all-gather
+    writes, and the accumulators (gathered by sync_state)."""
     import torch
-    n = n_items * d + (n_items if with_bias else 0)
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    chunk = -(-n_items // world)
+    rows = world * chunk
+    z = lambda n: torch.zeros(n, dtype=torch.float32, device=device)  # noqa: E731
+    grad, gb = z(rows * d), (z(rows) if with_bias else None)
+    engine.bind_item_grad_split(grad.data_ptr(), grad.numel(),
+                                gb.data_ptr() if with_bias else None, rows if with_bias else 0)
+    V, AV = z(rows * d), z(rows * d)
+    engine.bind_table("item", V.data_ptr(), V.numel())
+    engine.bind_table("acc_item", AV.data_ptr(), AV.numel())
+    tables, state = [(V, d)], [(AV, d)]
+    if with_bias:
+        b, Ab = z(rows), z(rows)
+        engine.bind_table("bias", b.data_ptr(), b.numel())
+        engine.bind_table("acc_bias", Ab.data_ptr(), Ab.numel())
+        tables.append((b, 1))
+        state.append((Ab, 1))
+    items = ReduceScatterItems(grad, z(chunk * d), tables, chunk, rank, grad_bias=gb,
+                               bias_slice=z(chunk) if with_bias else None, state=state, group=group)
+    items._keep = (V, AV) + ((b, Ab) if with_bias else ())
+    return items
+
+
+def make_gpu_sharded(engine, n_items, d, with_bias, device, exchange="allreduce", process_group=None):
+    """Bind the item-gradient buffer(s) to the engine, run the engine on
+    torch's current stream so RCCL orders after it, and return the step
+    callable and its item exchange.  ``exchange``: "allreduce" (dense
+    all-reduce + replicated item Adagrad) or "rs_ag" (reduce-scatter ->
+    owner Adagrad -> all-gather)."""
+    import torch
     share_stream(engine, device)
-    grad = torch.zeros(n, dtype=torch.float32, device=device)
-    engine.bind_item_grad(grad.data_ptr(), n)
-    return ShardedStep(engine, grad), grad
+    if exchange == "rs_ag":
+        items = _bind_rs_items(engine, n_items, d, with_bias, device, process_group)
+    elif exchange == "allreduce":
+        n = n_items * d + (n_items if with_bias else 0)
+        grad = torch.zeros(n, dtype=torch.float32, device=device)
+        engine.bind_item_grad(grad.data_ptr(), n)
+        items = AllReduceItems(grad, process_group)
+    else:
+        raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
+    return ShardedStep(engine, items, process_group), items
 
 
 def item_users(indptr, indices, n_items):
@@ -148,11 +318,12 @@ class GroupExchangeStep(object):
     tensors send_ids, rows, grads, recv_ids, serve_rows, serve_grads,
     ``ensure_recv(n)`` and ``device``."""
 
-    def __init__(self, backend, item_grad, world, process_group=None):
+    def __init__(self, backend, items, world, process_group=None):
         import torch
         import torch.distributed as dist
         self.backend = backend
-        self.item_grad = item_grad
+        self.items = _items(items, process_group)
+        self.item_grad = self.items.grad
         self.world = world
         self.group = process_group
         self._dist = dist
@@ -174,8 +345,13 @@ class GroupExchangeStep(object):
         be.xchg_grad()
         _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group)
         be.xchg_finish(nr)
-        dist.all_reduce(self.item_grad, group=self.group)
-        be.step_items()
+        x = self.items
+        x.reduce(dist, False)
+        x.apply(be)
+        x.gather(dist, False)
+
+    def sync_state(self):
+        self.items.sync_state(self._dist)
 
 
 class EngineExchange(object):
@@ -226,18 +402,31 @@ class EngineExchange(object):
     def step_items(self):
         self.e.step_items()
 
+    def clear_item_grad(self):
+        self.e.clear_item_grad()
+
+    def step_items_range(self, row0, row1, grad, grad_bias=None):
+        self.e.step_items_range(row0, row1, grad, grad_bias)
+
 
 def make_gpu_group_exchange(engine, world, rank, bounds, indptr, indices, n_items, d, batch_size,
-                            device, process_group=None):
-    """Sharded GBPR on the real engine: bind the item-gradient tensor and the
+                            device, process_group=None, exchange="allreduce", item_csr=None):
+    """Sharded GBPR on the real engine: bind the item-gradient buffers and the
     exchange buffers, run on torch's current stream (RCCL orders after the
-    engine's kernels), return the step callable and the item-gradient tensor.
-    ``indptr``/``indices`` are the GLOBAL user -> item CSR."""
+    engine's kernels), return the step callable and its item exchange.
+    ``indptr``/``indices`` are the GLOBAL user -> item CSR, or pass the global
+    item -> user CSR directly as ``item_csr`` = (indptr_t, indices_t)."""
     import torch
-    n = n_items * d + n_items
     share_stream(engine, device)
-    grad = torch.zeros(n, dtype=torch.float32, device=device)
-    engine.bind_item_grad(grad.data_ptr(), n)
-    ip_t, ix_t = item_users(indptr, indices, n_items)
+    if exchange == "rs_ag":
+        items = _bind_rs_items(engine, n_items, d, True, device, process_group)
+    elif exchange == "allreduce":
+        n = n_items * d + n_items
+        grad = torch.zeros(n, dtype=torch.float32, device=device)
+        engine.bind_item_grad(grad.data_ptr(), n)
+        items = AllReduceItems(grad, process_group)
+    else:
+        raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
+    ip_t, ix_t = item_csr if item_csr is not None else item_users(indptr, indices, n_items)
     be = EngineExchange(engine, world, rank, bounds, ip_t, ix_t, batch_size, d, device)
-    return GroupExchangeStep(be, grad, world, process_group), grad
+    return GroupExchangeStep(be, items, world, process_group), items

@@ -267,6 +267,32 @@ class Engine(object):
     def step_items(self):
         N.check(self._L.cf_step_items(self._h), "cf_step_items")
 
+    def step_local_draw(self, batch_size):
+        N.check(self._L.cf_step_local_draw(self._h, int(batch_size)), "cf_step_local_draw")
+
+    # item-range ownership (reduce-scatter -> owner Adagrad -> all-gather)
+    def bind_item_grad_split(self, grad_items_ptr, n_grad_items, grad_bias_ptr=None, n_grad_bias=0):
+        v = ctypes.c_void_p
+        N.check(self._L.cf_bind_item_grad_split(self._h, v(grad_items_ptr), int(n_grad_items),
+                                                v(grad_bias_ptr or None), int(n_grad_bias)),
+                "cf_bind_item_grad_split")
+
+    def clear_item_grad(self):
+        N.check(self._L.cf_clear_item_grad(self._h), "cf_clear_item_grad")
+
+    def step_items_range(self, row0, row1, grad, grad_bias=None):
+        """grad / grad_bias: device pointers or torch device tensors."""
+        v = ctypes.c_void_p
+        p = lambda t: (t.data_ptr() if hasattr(t, "data_ptr") else t) or None  # noqa: E731
+        N.check(self._L.cf_step_items_range(self._h, int(row0), int(row1), v(p(grad)),
+                                            v(p(grad_bias))), "cf_step_items_range")
+
+    def bind_table(self, name, device_ptr, n_elems):
+        """Caller device memory (e.g. a padded torch tensor) as the storage
+        of an item-side table; None returns it to engine-owned memory."""
+        N.check(self._L.cf_bind_table(self._h, N.TABLES[name], ctypes.c_void_p(device_ptr or None),
+                                      int(n_elems)), "cf_bind_table(%s)" % name)
+
     # ---- user sharding + GBPR group exchange (include/cf_engine.h) --------------
     def set_shard(self, world, rank, bounds):
         b = np.ascontiguousarray(bounds, dtype=np.int64)
@@ -297,8 +323,8 @@ class Engine(object):
                     "cf_xchg_begin")
         else:
             B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
-            N.check(self._L.cf_xchg_begin(self._h, B, _ptr(pairs, ctypes.c_int32),
-                                          _ptr(negs, ctypes.c_int32), gp, cp), "cf_xchg_begin")
+            N.check(self._L.cf_xchg_begin(self._h, B, _arg(pairs, ctypes.c_int32),
+                                          _arg(negs, ctypes.c_int32), gp, cp), "cf_xchg_begin")
         return counts
 
     def xchg_serve(self, n_recv):
@@ -380,3 +406,20 @@ def synth_graph(n_users, n_items, mean_degree, zipf_s, seed, u_begin=0, u_end=No
                              _ptr(indptr, ctypes.c_int64), _ptr(indices, ctypes.c_int32),
                              int(n_threads)), "cf_synth_items")
     return indptr, indices
+
+
+def synth_item_users(n_users, n_items, mean_degree, zipf_s, seed, n_threads=0):
+    """Item -> user CSR (indptr int64 [n_items+1], indices int32) of the whole
+    synthetic graph, users of each item ascending (cf_synth_item_users): the
+    GBPR group source of a user-sharded engine, built natively."""
+    L = N.lib()
+    degs = synth_degrees(n_users, mean_degree, seed)
+    nnz = int(degs[-1])
+    del degs
+    indptr_t = np.empty(int(n_items) + 1, dtype=np.int64)
+    indices_t = np.empty(nnz, dtype=np.int32)
+    N.check(L.cf_synth_item_users(int(n_users), int(n_items), float(mean_degree), float(zipf_s),
+                                  int(seed), _ptr(indptr_t, ctypes.c_int64),
+                                  _ptr(indices_t, ctypes.c_int32), int(n_threads)),
+            "cf_synth_item_users")
+    return indptr_t, indices_t

@@ -243,6 +243,43 @@ int cf_step_local_apply(cf_engine* eng, int32_t next_B);
 /* Phase 2, after the buffer holds the cross-rank sum: dense item Adagrad
  * (and CML clip of updated rows); zeroes the buffer. */
 int cf_step_items(cf_engine* eng);
+/* Draw + count the next device-sampled batch of B pairs after
+ * cf_step_local_apply(eng, 0) (the next cf_step_local_grad with that B takes
+ * it), so that the draw can run beside a collective of its own. */
+int cf_step_local_draw(cf_engine* eng, int32_t B);
+/*
+ * Item-range ownership (reduce-scatter -> owner Adagrad -> all-gather), the
+ * alternative to the all-reduce + replicated item Adagrad above; same
+ * arithmetic (TF1 sums over the whole global batch before the update,
+ * gbprmf.py:101-106, bprmf.py:83-88):
+ *   cf_bind_item_grad_split  dense item gradient (>= n_items*d floats) and,
+ *                            GBPR, bias gradient (>= n_items) in caller
+ *                            buffers, e.g. padded to world * chunk rows so a
+ *                            reduce-scatter splits them evenly
+ *   cf_step_local_grad / _apply (/ _draw) as above
+ *   (reduce-scatter of the gradient buffers: rank r receives rows
+ *    [r*chunk, (r+1)*chunk))
+ *   cf_clear_item_grad       re-zero the rows of the bound gradient buffers
+ *                            the last local gradient touched (stream-ordered
+ *                            after the collective that read them)
+ *   cf_step_items_range      Adagrad (+ CML clip) of item rows [row0, row1)
+ *                            from gradient rows in `grad` ((row1-row0)*d) and
+ *                            `grad_bias` (GBPR); all-zero rows are untouched
+ *   (all-gather of the owned rows of V (and b) into every rank's table:
+ *    bind the table storage with cf_bind_table so the collective writes it)
+ * Only the owner keeps the accumulator rows of its range current.
+ */
+int cf_bind_item_grad_split(cf_engine* eng, void* grad_items, int64_t n_grad_items,
+                            void* grad_bias, int64_t n_grad_bias);
+int cf_clear_item_grad(cf_engine* eng);
+int cf_step_items_range(cf_engine* eng, int64_t row0, int64_t row1, const void* grad,
+                        const void* grad_bias);
+/* Use caller device memory (>= the table's size in floats, e.g. padded for an
+ * all-gather) as the storage of CF_TABLE_ITEM, CF_TABLE_BIAS,
+ * CF_TABLE_ACC_ITEM or CF_TABLE_ACC_BIAS; the current contents are copied
+ * in.  NULL returns the table to engine-owned memory (contents copied
+ * back).  The caller keeps the buffer alive while it is bound. */
+int cf_bind_table(cf_engine* eng, int32_t table, void* device_ptr, int64_t n_elems);
 /* ---- user sharding + GBPR group exchange ------------------------
  * A user-sharded GBPR engine draws each pair's group members from the item's
  * users over ALL ranks (item_posUserList, sampler_gbpr.py:15,41); a member
@@ -456,6 +493,14 @@ int cf_synth_degrees(int64_t n_users, double mean_degree, uint64_t seed,
 int cf_synth_items(int64_t n_items, double zipf_s, uint64_t seed,
                    int64_t u_begin, int64_t u_end, const int64_t* host_indptr,
                    int32_t* host_indices_out, int32_t n_threads);
+/* The item -> user transpose of the whole graph (users of each item in
+ * increasing id order) -- the GBPR group source of a user-sharded engine
+ * (item_posUserList, sampler_gbpr.py:15) -- without materialising the
+ * user -> item CSR: indptr_t_out [n_items+1], indices_t_out [nnz] with nnz
+ * the last entry of cf_synth_degrees over all users. */
+int cf_synth_item_users(int64_t n_users, int64_t n_items, double mean_degree, double zipf_s,
+                        uint64_t seed, int64_t* host_indptr_t_out, int32_t* host_indices_t_out,
+                        int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -56,21 +56,69 @@ class SplitOracleShard(OracleShard):
         self.O.dedup_adagrad(self.U, self.AU, ur, ug, self.lr)
 
 
+class RSOracleShard(SplitOracleShard):
+    """Item-range ownership (ReduceScatterItems): the item table, its
+    accumulator and the gradient live in buffers padded to world * chunk
+    rows; the owner of rows [r*chunk, (r+1)*chunk) applies their Adagrad."""
+
+    def __init__(self, U_local, V, reg, world, lr=0.1):
+        super(RSOracleShard, self).__init__(U_local, V, reg, lr)
+        n, d = V.shape
+        self.n, self.d = n, d
+        self.chunk = -(-n // world)
+        rows = world * self.chunk
+        self.Vfull = torch.zeros(rows * d, dtype=torch.float64)
+        self.Vfull[:n * d] = torch.from_numpy(V.ravel())
+        self.AVfull = torch.full((rows * d,), 0.1, dtype=torch.float64)
+        self.V = self.Vfull.numpy()[:n * d].reshape(n, d)      # views: the all-gather
+        self.AV = self.AVfull.numpy()[:n * d].reshape(n, d)    # writes them
+        self.item_grad = torch.zeros(rows * d, dtype=torch.float64)
+
+    def step_local_grad(self, batch_size=None, pairs=None, negs=None, groups=None):
+        _, _, self._users, (vr, vg) = self.O.bpr_loss_grads(self.U, self.V, pairs, negs, self.reg)
+        G = self.item_grad.numpy()[:self.n * self.d].reshape(self.n, self.d)
+        np.add.at(G, vr, vg)
+
+    def clear_item_grad(self):
+        self.item_grad.zero_()
+
+    def step_items_range(self, r0, r1, grad, grad_bias=None):
+        r1 = min(r1, self.n)
+        if r1 <= r0:
+            return
+        G = grad.numpy().reshape(-1, self.d)[:r1 - r0]
+        rows = np.nonzero(np.any(G != 0, axis=1))[0]
+        self.AV[r0 + rows] += G[rows] ** 2
+        self.V[r0 + rows] -= self.lr * G[rows] / np.sqrt(self.AV[r0 + rows])
+
+    def step_local_draw(self, batch_size):
+        pass
+
+
 def _worker(rank, world, port, fold, batches, U0, V0, q, split=False):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
-    from collaborativefilteringusingtensorflow_amd.distributed import ShardedStep, shard_users
+    from collaborativefilteringusingtensorflow_amd.distributed import (ReduceScatterItems, ShardedStep,
+                                                                       shard_users)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
                             world_size=world)
     u0, u1 = shard_users(fold["train_indptr"], world, rank)
-    be = (SplitOracleShard if split else OracleShard)(U0[u0:u1], V0, reg=0.05)
-    step = ShardedStep(be, be.item_grad)
+    if split == "rs_ag":
+        be = RSOracleShard(U0[u0:u1], V0, reg=0.05, world=world)
+        d = V0.shape[1]
+        items = ReduceScatterItems(be.item_grad, torch.zeros(be.chunk * d, dtype=torch.float64),
+                                   [(be.Vfull, d)], be.chunk, rank, state=[(be.AVfull, d)])
+        step = ShardedStep(be, items)
+    else:
+        be = (SplitOracleShard if split else OracleShard)(U0[u0:u1], V0, reg=0.05)
+        step = ShardedStep(be, be.item_grad)
     for pairs, negs in batches:
         mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
         lp = pairs[mine].copy()
         lp[:, 0] -= u0
         step(pairs=lp, negs=negs[mine])
-    q.put((rank, u0, u1, be.U, be.V, be.AV))
+    step.sync_state()
+    q.put((rank, u0, u1, be.U, be.V.copy(), be.AV.copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -96,7 +144,7 @@ def test_shard_users_balances_nnz(fold1):
         assert lp[0] == 0 and lp[-1] == len(lx)
 
 
-@pytest.mark.parametrize("world,split", [(2, False), (2, True)])
+@pytest.mark.parametrize("world,split", [(2, False), (2, True), (2, "rs_ag"), (3, "rs_ag")])
 def test_sharded_step_equals_global_step(fold1, streams, world, split):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(4)

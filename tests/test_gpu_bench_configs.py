@@ -1,0 +1,239 @@
+"""GPU parity at the benchmarked configurations' own kernel instantiations
+(BASELINE.json configs[2..4], bench.py CONFIGS), against the float64 oracle.
+
+* trajectories on ml-100k fold 1 through the device-sampler pipeline
+  (cf_train_steps: draw of step s+1 fused into the apply of step s) at the
+  bench shapes: CML d=128, W=5 on the generic (auto) and the phased gradient
+  kernel (cml.py:55-129); GBPR d=64, W=5, G=1 on the phased kernel
+  (gbprmf.py:58-106); AMF d=128, W=5 across the phase switch
+  (amf.py:139-162, 216-244).  The oracle replays the same batches (an engine
+  with the same seed draws the identical stream with cf_sample).
+* one full-size step of cfg3 (CML) and cfg5 (AMF phase 2) on the 1M x 100K
+  graph, and of cfg4 (GBPR, 10M x 1M) checked on the rows the batch touches
+  (a compact oracle: the touched rows re-indexed) plus untouched rows
+  unchanged.
+* the fused MFMA scoring + top-10 at d=128 on 4,096 users of the cfg5 graph;
+  CML's final top-1000 (cml.py:203-212) on the materialised path.
+
+Tolerance: the north star's 1e-5 relative on fp32 embeddings, elementwise:
+|gpu - oracle| <= ATOL + RTOL |oracle| with RTOL = 1e-5 and ATOL = 1e-6
+(elements that cancel to ~0 after Adagrad updates of ~0.1); the per-step
+loss within 1e-5 relative.
+"""
+import numpy as np
+import pytest
+
+from oracle import cf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-5, 1e-6
+
+
+def assert_close(got, ref, what):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(got - ref)
+    bad = err > ATOL + RTOL * np.abs(ref)
+    worst = float(np.max(err / (ATOL + RTOL * np.abs(ref)))) if err.size else 0.0
+    assert not bad.any(), (what, int(bad.sum()), float(err.max()), worst)
+
+
+HP = {"cml": dict(margin=1.0, reg_cov=1.0, clip_norm=1.0),   # testcml.py:26-34
+      "gbpr": dict(rho=0.4, reg=0.01),                        # testgbprmf.py:23-32
+      "amf": dict(reg=0.05, reg_adv=1.0)}                     # testamf.py:23-33
+
+
+def _engine(model, fold1, d, W, grad_path, seed=41):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=1, seed=seed,
+               **HP[model])
+    e.set_option("grad_path", grad_path)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=6)
+    return e
+
+
+def _oracle_step(model, T, pairs, negs, groups, adversarial, n_items):
+    if model == "cml":
+        return O.cml_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs,
+                          1.0, 1.0, 1.0, n_items=n_items)
+    if model == "gbpr":
+        return O.gbpr_step(T["user"], T["item"], T["bias"], T["acc_user"], T["acc_item"],
+                           T["acc_bias"], pairs, negs, groups, 0.4, 0.01)
+    return O.amf_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.05,
+                      adversarial, reg_adv=1.0)
+
+
+TABLES = {"cml": ("user", "item", "acc_user", "acc_item"),
+          "amf": ("user", "item", "acc_user", "acc_item"),
+          "gbpr": ("user", "item", "bias", "acc_user", "acc_item", "acc_bias")}
+
+
+@pytest.mark.parametrize("model,d,grad_path,switch", [
+    ("cml", 128, 0, None),    # cfg3 as benched: auto = the generic kernel for CML at W = 5
+    ("cml", 128, 2, None),    # cfg3 on the phased kernel
+    ("gbpr", 64, 0, None),    # cfg4: auto = phased grad_fast_kernel<GBPR, EPL 4, W 5>
+    ("amf", 128, 0, 14),      # cfg5 across the phase switch (fresh accumulators)
+], ids=["cml-d128-generic", "cml-d128-phased", "gbpr-d64-w5-g1", "amf-d128-switch"])
+def test_bench_shape_pipeline_trajectory(fold1, model, d, grad_path, switch):
+    W, B, K = 5, 100, 28
+    dev = _engine(model, fold1, d, W, grad_path)
+    rep = _engine(model, fold1, d, W, grad_path)       # same seed: the same batch stream
+    T = {t: dev.get_table(t).astype(np.float64) for t in TABLES[model]}
+    batches = [rep.sample(B) for _ in range(K)]
+    rep.close()
+    loss_dev = 0.0
+    if switch is None:
+        loss_dev = dev.train_steps(B, K)
+    else:
+        loss_dev = dev.train_steps(B, switch)
+        dev.begin_phase(1)
+        loss_dev += dev.train_steps(B, K - switch)
+    loss_ref = 0.0
+    for s, (pairs, negs, groups) in enumerate(batches):
+        adv = switch is not None and s >= switch
+        if switch is not None and s == switch:   # amf.py:157-162: a fresh AdagradOptimizer
+            T["acc_user"][...] = 0.1
+            T["acc_item"][...] = 0.1
+        loss_ref += _oracle_step(model, T, pairs, negs, groups, adv, int(fold1["n_items"]))
+    assert abs(loss_dev - loss_ref) <= RTOL * abs(loss_ref), (loss_dev, loss_ref)
+    for t in TABLES[model]:
+        assert_close(dev.get_table(t), T[t], t)
+    dev.close()
+
+
+def _cfg2_graph():
+    from collaborativefilteringusingtensorflow_amd.engine import synth_graph
+    return synth_graph(1_000_000, 100_000, 50.0, 0.8, 20261015, n_threads=16)
+
+
+@pytest.mark.parametrize("model", ["cml", "amf"], ids=["cfg3-cml", "cfg5-amf-phase2"])
+def test_full_size_step(model):
+    """One step at full cfg3 / cfg5 size (1M users x 100K items, d=128, W=5,
+    B=65,536), after three pipelined steps, against the float64 oracle."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d, W, B = 1_000_000, 100_000, 128, 5, 65536
+    ip, ix = _cfg2_graph()
+    e = Engine(model, nu, ni, d, n_neg=W, seed=78, **HP[model])
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=1)
+    if model == "amf":
+        e.begin_phase(1)
+    e.train_steps(B, 3)
+    T = {t: e.get_table(t).astype(np.float64) for t in TABLES[model]}
+    pairs, negs, groups = e.sample(B)
+    loss = e.step(pairs, negs)
+    lo = _oracle_step(model, T, pairs, negs, groups, True, ni)
+    assert abs(loss - lo) <= RTOL * abs(lo), (loss, lo)
+    for t in TABLES[model]:
+        assert_close(e.get_table(t), T[t], t)
+    e.close()
+
+
+def test_cfg4_full_size_step_touched_rows():
+    """cfg4 (GBPR, 10M users x 1M items, d=64, W=5, G=1, B=65,536): one step
+    after two pipelined ones.  The oracle steps a compact copy of the rows the
+    batch touches (ids re-indexed), which is the whole step: Adagrad leaves
+    untouched rows alone; a sample of untouched rows must be bit-unchanged."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+    nu, ni, d, W, B = 10_000_000, 1_000_000, 64, 5, 65536
+    ip, ix = synth_graph(nu, ni, 20.0, 0.8, 20261015, n_threads=16)
+    e = Engine("gbpr", nu, ni, d, n_neg=W, gsize=1, seed=79, **HP["gbpr"])
+    e.set_interactions(ip, ix)
+    del ip, ix
+    e.init_params(0.0, 0.1, truncated=True, seed=1)
+    e.train_steps(B, 2)
+    pairs, negs, groups = e.sample(B)
+    users = np.unique(np.concatenate([pairs[:, 0], groups.reshape(-1)]))
+    items = np.unique(np.concatenate([pairs[:, 1], negs.reshape(-1)]))
+    rng = np.random.RandomState(3)
+    ou = np.setdiff1d(rng.randint(0, nu, 4096), users)
+    oi = np.setdiff1d(rng.randint(0, ni, 4096), items)
+    pre = {}
+    for t in TABLES["gbpr"]:
+        full = e.get_table(t)
+        rows, other = (users, ou) if t in ("user", "acc_user") else (items, oi)
+        pre[t] = (full[rows].astype(np.float64), full[other].copy())
+        del full
+    cp = np.stack([np.searchsorted(users, pairs[:, 0]), np.searchsorted(items, pairs[:, 1])], 1)
+    cn = np.searchsorted(items, negs)
+    cg = np.searchsorted(users, groups)
+    T = {t: pre[t][0] for t in TABLES["gbpr"]}
+    loss = e.step(pairs, negs, groups)
+    lo = _oracle_step("gbpr", T, cp, cn, cg, False, ni)
+    assert abs(loss - lo) <= RTOL * abs(lo), (loss, lo)
+    for t in TABLES["gbpr"]:
+        full = e.get_table(t)
+        rows, other = (users, ou) if t in ("user", "acc_user") else (items, oi)
+        assert_close(full[rows], T[t], t)
+        assert np.array_equal(full[other], pre[t][1]), t + ": an untouched row moved"
+        del full
+    e.close()
+
+
+def _check_lists(gpu_idx, scores, ref_lists, atol):
+    """Exact order except adjacent near-ties (|ds| <= atol in fp64)."""
+    for r, (g, o) in enumerate(zip(gpu_idx, ref_lists)):
+        g = [int(x) for x in g if x >= 0]
+        assert len(g) == len(o), r
+        for a, b in zip(g, o):
+            if a != b:
+                assert abs(scores[r][a] - scores[r][b]) <= atol, (r, a, b, scores[r][a], scores[r][b])
+
+
+def test_fused_topk_d128_cfg5_slice():
+    """The fused fp32-MFMA scoring + streaming top-10 (the cfg5 scoring
+    kernel, amf.py:144-148 + bprmf.py:90-103) at d=128 on 4,096 users of the
+    cfg5 graph, train items excluded."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d = 1_000_000, 100_000, 128
+    ip, ix = _cfg2_graph()
+    e = Engine("amf", nu, ni, d, n_neg=5, seed=80, **HP["amf"])
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, truncated=True, seed=1)
+    e.train_steps(65536, 2)
+    U = e.get_table("user")
+    V = e.get_table("item").astype(np.float64)
+    users = np.arange(4096, dtype=np.int32) * 241 % nu
+    idx = e.score_topk(users, 10, exclude_train=True)
+    for c0 in range(0, len(users), 512):
+        us = users[c0:c0 + 512]
+        S = U[us].astype(np.float64) @ V.T
+        _check_lists(idx[c0:c0 + 512], S, _topk_ref(S, ip, ix, us, 10), atol=1e-5)
+    e.close()
+
+
+def _topk_ref(S, ip, ix, users, k):
+    """O.recommend's order (descending, ties to the lower id, train items
+    dropped) without a full sort of every 100K-item row: everything at or
+    above the k-th largest non-train score, sorted by (-score, id)."""
+    out = []
+    for r, u in enumerate(users):
+        s = S[r].copy()
+        s[ix[ip[u]:ip[u + 1]]] = -np.inf
+        kth = np.partition(s, -k)[-k]
+        cand = np.nonzero(s >= kth)[0]
+        cand = cand[np.lexsort((cand, -s[cand]))]
+        out.append([int(x) for x in cand[:k]])
+    return out
+
+
+def test_cml_final_top1000_materialised(fold1):
+    """CML's final evaluation takes one top-k of width max|train| + 1000 and
+    reports topN up to 1000 (cml.py:203-212): the materialised score + radix
+    select path at k = 1000 against the oracle's recommend."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d = int(fold1["n_users"]), int(fold1["n_items"]), 50
+    e = Engine("cml", nu, ni, d, n_neg=5, seed=81, **HP["cml"])
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.init_params(0.0, 0.1, truncated=False, seed=2)
+    e.train_steps(50, 200)
+    U = e.get_table("user").astype(np.float64)
+    V = e.get_table("item").astype(np.float64)
+    users = np.nonzero(np.diff(fold1["test_indptr"]))[0].astype(np.int32)
+    idx = e.score_topk(users, 1000, exclude_train=True)
+    S = O.predict("cml", U, V, None, users)
+    ref = O.recommend(S, fold1["train_indptr"], fold1["train_indices"], users, 1000)
+    _check_lists(idx, S, ref, atol=1e-5)
+    e.close()

@@ -26,15 +26,21 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q):
+def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q, exchange="allreduce",
+            backend="gloo"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
     from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_sharded,
                                                                        shard_users, local_csr)
     from collaborativefilteringusingtensorflow_amd.engine import Engine
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
-                            world_size=world)
+    if backend == "nccl":   # RCCL accepts a one-rank communicator on device 0
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                                world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                                world_size=world)
     ip, ix = fold["train_indptr"], fold["train_indices"]
     u0, u1 = shard_users(ip, world, rank)
     lip, lix = local_csr(ip, ix, u0, u1)
@@ -46,12 +52,14 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q):
     e.set_interactions(lip, lix)
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
-    step, grad = make_gpu_sharded(e, 1682, U0.shape[1], False, torch.device("cuda", 0))
+    step, items = make_gpu_sharded(e, 1682, U0.shape[1], False, torch.device("cuda", 0),
+                                   exchange=exchange)
     for pairs, negs in batches:
         mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
         lp = pairs[mine].copy()
         lp[:, 0] -= u0
         step(pairs=lp, negs=negs[mine])
+    step.sync_state()     # rs_ag: the owners' accumulator rows to every rank
     torch.cuda.synchronize()
     q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("acc_item")))
     e.close()
@@ -59,9 +67,58 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("item_reduce", [1, 2, 0], ids=["reduce", "store-singletons", "atomic"])
+def _oracle_run(model, batches, U0, V0):
+    from oracle import cf_oracle as O
+    U, V = U0.astype(np.float64), V0.astype(np.float64)
+    AU, AV = np.full_like(U, 0.1), np.full_like(V, 0.1)
+    for pairs, negs in batches:
+        if model == "bpr":
+            O.bpr_step(U, V, AU, AV, pairs, negs, 0.05)
+        else:
+            O.cml_step(U, V, AU, AV, pairs, negs, 1.0, 1.0, 1.0)
+    return U, V, AU, AV
+
+
+def _check_elementwise(got, ref, rtol=1e-5, atol=1e-7):
+    """Elementwise |got - ref| <= atol + rtol |ref| (north star: 1e-5
+    relative on fp32 embeddings; atol covers elements that cancel to ~0)."""
+    err = np.abs(got.astype(np.float64) - ref)
+    bad = err > atol + rtol * np.abs(ref)
+    assert not bad.any(), (int(bad.sum()), float(err.max()))
+
+
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
 @pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
-def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream, item_reduce):
+def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange):
+    """The RCCL path itself (nccl backend, world size 1 on device 0): the
+    asynchronous collectives, the user apply beside them and the stream
+    ordering of cf_step_local_apply / cf_step_items(_range) against them."""
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(9)
+    d = 32
+    U0 = O.init_table(rng, (943, d), truncated=(model != "cml"))
+    V0 = O.init_table(rng, (1682, d), truncated=(model != "cml"))
+    batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s]) for s in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, _free_port(), fold1, batches, U0, V0, model, 1, q,
+                                          exchange, "nccl"))
+    p.start()
+    rank, u0, u1, Ul, Vr, AVr = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    U, V, AU, AV = _oracle_run(model, batches, U0, V0)
+    _check_elementwise(Ul, U)
+    _check_elementwise(Vr, V)
+    _check_elementwise(AVr, AV)
+
+
+@pytest.mark.parametrize("item_reduce,exchange", [(1, "allreduce"), (2, "allreduce"), (0, "allreduce"),
+                                                  (1, "rs_ag")],
+                         ids=["reduce", "store-singletons", "atomic", "reduce-scatter"])
+@pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
+def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream, item_reduce,
+                                                    exchange):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(8)
     d = 24
@@ -71,7 +128,8 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, item_reduce, q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, item_reduce, q,
+                                               exchange))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -79,21 +137,17 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    U, V = U0.astype(np.float64), V0.astype(np.float64)
-    AU, AV = np.full_like(U, 0.1), np.full_like(V, 0.1)
-    for pairs, negs in batches:
-        if model == "bpr":
-            O.bpr_step(U, V, AU, AV, pairs, negs, 0.05)
-        else:
-            O.cml_step(U, V, AU, AV, pairs, negs, 1.0, 1.0, 1.0)
+    U, V, AU, AV = _oracle_run(model, batches, U0, V0)
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
     for rank, u0, u1, Ul, Vr, AVr in res:
         assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
         assert rel(Vr, V) <= 1e-5 and rel(AVr, AV) <= 1e-5
+        _check_elementwise(Ul, U[u0:u1])
+        _check_elementwise(Vr, V)
     assert np.array_equal(res[0][4], res[1][4])   # replicas bit-identical
 
 
-def _draw_ahead_worker(port, fold, q):
+def _draw_ahead_worker(port, fold, q, exchange="allreduce"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -106,7 +160,7 @@ def _draw_ahead_worker(port, fold, q):
         e = Engine("bpr", 943, 1682, 16, n_neg=2, reg=0.05, dense_item_apply=True, seed=77)
         e.set_interactions(ip, ix)
         e.init_params(0.0, 0.1, seed=5)
-        step, _ = make_gpu_sharded(e, 1682, 16, False, torch.device("cuda", 0))
+        step, _ = make_gpu_sharded(e, 1682, 16, False, torch.device("cuda", 0), exchange=exchange)
         step.draw_ahead = ahead
         for _ in range(9):
             step(batch_size=120)
@@ -120,12 +174,14 @@ def _draw_ahead_worker(port, fold, q):
     dist.destroy_process_group()
 
 
-def test_draw_ahead_split_step_equals_plain_split_step(fold1):
-    """cf_step_local_grad / cf_step_local_apply(next_B): the batch drawn in the
-    apply launch is the one the sampler would draw next; dropping it rewinds."""
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
+def test_draw_ahead_split_step_equals_plain_split_step(fold1, exchange):
+    """cf_step_local_grad / cf_step_local_apply(next_B) (all-reduce) or
+    cf_step_local_draw (reduce-scatter): the batch drawn ahead is the one the
+    sampler would draw next; dropping it rewinds."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_draw_ahead_worker, args=(_free_port(), fold1, q))
+    p = ctx.Process(target=_draw_ahead_worker, args=(_free_port(), fold1, q, exchange))
     p.start()
     a, b = q.get(timeout=300)
     p.join(timeout=120)

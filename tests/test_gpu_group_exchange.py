@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled):
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -50,8 +50,8 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled):
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
     e.set_table("bias", b0)
-    step, _grad = make_gpu_group_exchange(e, world, rank, bounds, ip, ix, 1682, d, 100,
-                                          torch.device("cuda", 0))
+    step, _items = make_gpu_group_exchange(e, world, rank, bounds, ip, ix, 1682, d, 100,
+                                           torch.device("cuda", 0), exchange=exchange)
     drawn = []
     if sampled:
         for _ in range(6):
@@ -66,19 +66,20 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled):
             lp = pairs[mine].copy()
             lp[:, 0] -= u0
             step(pairs=lp, negs=negs[mine], groups=groups[mine])
+    step.sync_state()
     torch.cuda.synchronize()
     q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("bias"),
-           e.get_table("acc_user"), drawn))
+           e.get_table("acc_user"), drawn, e.get_table("acc_item"), e.get_table("acc_bias")))
     e.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(fold1, batches, U0, V0, b0, sampled=False):
+def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -89,8 +90,9 @@ def _run(fold1, batches, U0, V0, b0, sampled=False):
     return res
 
 
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
 @pytest.mark.parametrize("stream", ["gbpr_b100_g1_w5", "gbpr_b100_g3_w2"])
-def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream):
+def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exchange):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(12)
     d = 16
@@ -99,16 +101,17 @@ def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream):
     b0 = O.init_table(rng, (1682,))
     batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
                 streams[stream + "/groups"][s]) for s in range(8)]
-    res = _run(fold1, batches, U0, V0, b0)
+    res = _run(fold1, batches, U0, V0, b0, exchange=exchange)
     U, V, b = U0.astype(np.float64), V0.astype(np.float64), b0.astype(np.float64)
     AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
     for pairs, negs, groups in batches:
         O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
     rel = lambda a, c: np.abs(a - c).max() / np.abs(c).max()
-    for rank, u0, u1, Ul, Vr, br, AUl, _ in res:
+    for rank, u0, u1, Ul, Vr, br, AUl, _, AVr, Abr in res:
         assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
         assert rel(AUl, AU[u0:u1]) <= 1e-5, (rank, rel(AUl, AU[u0:u1]))
         assert rel(Vr, V) <= 1e-5 and rel(br, b) <= 1e-5
+        assert rel(AVr, AV) <= 1e-5 and rel(Abr, Ab) <= 1e-5
     assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
 
 
@@ -123,7 +126,7 @@ def test_two_rank_device_sampled_groups_span_shards(fold1):
     res = _run(fold1, dummy, U0, V0, b0, sampled=True)
     ip, ix = fold1["train_indptr"], fold1["train_indices"]
     cross = 0
-    for rank, u0, u1, Ul, Vr, br, AUl, drawn in res:
+    for rank, u0, u1, Ul, Vr, br, AUl, drawn, _, _ in res:
         assert np.all(np.isfinite(Ul)) and np.all(np.isfinite(Vr))
         for pairs, groups in drawn:
             for (u, i), g in zip(pairs, groups):

@@ -154,3 +154,17 @@ def test_native_loader_fold_roundtrip(fold1, tmp_path):
     p.write_text("".join(lines[k] for k in order))
     ip2, ix2 = IO.load_csr(str(p), 943, 1682, threshold=3)
     assert np.array_equal(ip2, ip) and np.array_equal(ix2, ix)
+
+
+def test_native_item_user_transpose_matches_numpy():
+    """cf_synth_item_users (the sharded GBPR group source) equals the
+    transpose of the synthetic user -> item CSR (distributed.item_users)."""
+    from collaborativefilteringusingtensorflow_amd.engine import synth_graph, synth_item_users
+    from collaborativefilteringusingtensorflow_amd.distributed import item_users
+    nu, ni = 3000, 700
+    ip, ix = synth_graph(nu, ni, 12.0, 0.8, 99, n_threads=3)
+    tp, tu = item_users(ip, ix, ni)
+    for nt in (1, 4):
+        tp2, tu2 = synth_item_users(nu, ni, 12.0, 0.8, 99, n_threads=nt)
+        np.testing.assert_array_equal(tp2, tp)
+        np.testing.assert_array_equal(tu2, tu)
