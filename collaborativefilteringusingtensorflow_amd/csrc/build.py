@@ -19,7 +19,7 @@ VARIANT = os.environ.get("CF_BUILD_VARIANT", "")
 OUT = os.path.join(PKG, "build", "variants", VARIANT) if VARIANT else os.path.join(PKG, "build")
 LIB = os.path.join(OUT, "libcf_engine.so")
 SOURCES = ["cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp", "cf_ingest.cpp",
-           "cf_mt_sampler.cpp", "cf_ensemble.hip"]
+           "cf_mt_sampler.cpp", "cf_ensemble.hip", "cf_det.hip"]
 HEADERS = ["cf_kernels.h", "cf_device.h", os.path.join(ROOT, "include", "cf_engine.h")]
 ARCH = os.environ.get("CF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

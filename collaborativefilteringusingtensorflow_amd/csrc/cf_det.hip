@@ -1,0 +1,93 @@
+// cf_det.hip -- deterministic occurrence ranks (cf_set_option "deterministic").
+//
+// The fast path ranks the occurrences of a row by the order their returning
+// count atomics land, so the order in which a duplicated row's gradients are
+// summed -- and with it the last bits of the fp32 sum -- changes run to run.
+// TF1's CPU UnsortedSegmentSum behind AdagradOptimizer (bprmf.py:83-88) is
+// deterministic; this restores that property: a stable LSD radix sort of the
+// batch's row ids (users, then items offset by n_users) puts every row's
+// occurrences in batch order, rank = sorted position - the row's first sorted
+// position (off[row]), and the gradient kernels store occurrence k of row r
+// in the compact slot off[r] + k, which the apply sums in k order.
+#include <hipcub/hipcub.hpp>
+
+#include "cf_kernels.h"
+
+namespace cfk {
+
+namespace {
+
+__global__ void det_keys_kernel(const int32_t* __restrict__ occU, int64_t nU,
+                                const int32_t* __restrict__ occV, int64_t nV, int64_t n_users,
+                                int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = t0; q < nU + nV; q += nt) {
+        keys[q] = q < nU ? occU[q] : (int32_t)(n_users + occV[q - nU]);
+        vals[q] = (int32_t)q;
+    }
+}
+
+// the first sorted position of every row present in the batch
+__global__ void det_heads_kernel(const int32_t* __restrict__ skeys, int64_t n,
+                                 int32_t* __restrict__ off) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = t0; p < n; p += nt)
+        if (p == 0 || skeys[p] != skeys[p - 1]) off[skeys[p]] = (int32_t)p;
+}
+
+__global__ void det_rank_kernel(const int32_t* __restrict__ skeys, const int32_t* __restrict__ svals,
+                                int64_t n, int64_t nU, const int32_t* __restrict__ off,
+                                int32_t* __restrict__ rankU, int32_t* __restrict__ rankV) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t p = t0; p < n; p += nt) {
+        const int32_t q = svals[p];
+        const int32_t rk = (int32_t)(p - off[skeys[p]]);
+        if (q < nU) rankU[q] = rk;
+        else rankV[q - nU] = rk;
+    }
+}
+
+int key_bits(int64_t n_rows) {
+    int b = 1;
+    while (b < 31 && (1ll << b) < n_rows) ++b;
+    return b;
+}
+
+int grid_of(int64_t n) {
+    int64_t b = (n + 255) / 256;
+    return (int)(b < 1 ? 1 : b > 4096 ? 4096 : b);
+}
+
+}  // namespace
+
+size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)n_occ, 0,
+                                             key_bits(n_rows));
+    return bytes;
+}
+
+// keys / vals hold 2 * n_occ int32 each (in + out halves)
+hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV, int64_t nV,
+                            int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
+                            int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
+                            hipStream_t s) {
+    const int64_t n = nU + nV;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(det_keys_kernel, dim3(grid_of(n)), dim3(256), 0, s, occU, nU, occV, nV, n_users,
+                       keys, vals);
+    size_t bytes = tmp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, keys + n, vals, vals + n, (int)n, 0,
+                                                      key_bits(n_rows), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(det_heads_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, n, off);
+    hipLaunchKernelGGL(det_rank_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, vals + n, n, nU, off,
+                       rankU, rankV);
+    return hipGetLastError();
+}
+
+}  // namespace cfk

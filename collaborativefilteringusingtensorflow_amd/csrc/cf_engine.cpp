@@ -168,6 +168,15 @@ struct cf_engine {
     int64_t last_nV = 0;
     int lg_done_set = -1;     // buffer set of the last cf_step_local_apply
 
+    // deterministic mode (cf_set_option "deterministic"): sort-based ranks,
+    // compact slots, no float atomics on duplicated rows (cf_det.hip)
+    int det = 0;
+    int64_t det_cap = 0;                 // occurrences the buffers below hold
+    int32_t *det_keys = nullptr, *det_vals = nullptr, *det_off = nullptr;
+    void* det_tmp = nullptr;
+    size_t det_tmp_bytes = 0;
+    float *slotUc = nullptr, *slotVc = nullptr, *slotVbc = nullptr;
+
     // model state
     int phase = 0;
     bool need_clip_U = false, need_clip_V = false;
@@ -254,8 +263,37 @@ int ensure_slots(cf_engine* e) {
     return CF_OK;
 }
 
+int ensure_det(cf_engine* e, int B) {
+    const cf_config& c = e->cfg;
+    const int64_t nU = (int64_t)B * users_per_pair(c), nV = (int64_t)B * items_per_pair(c);
+    const int64_t n = nU + nV;
+    if (n <= e->det_cap && e->det_off) return CF_OK;
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipStreamSynchronize(e->side));
+    dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
+    dfree(e->slotVbc);
+    if (e->det_tmp) (void)hipFree(e->det_tmp);
+    e->det_tmp = nullptr;
+    e->det_cap = 0;
+    const int64_t rows = c.n_users + c.n_items;
+    CF_TRY(dalloc(&e->det_keys, (size_t)(2 * n)));
+    CF_TRY(dalloc(&e->det_vals, (size_t)(2 * n)));
+    CF_TRY(dalloc(&e->det_off, (size_t)rows));
+    CF_TRY(dalloc(&e->slotUc, (size_t)nU * c.n_factors));
+    CF_TRY(dalloc(&e->slotVc, (size_t)nV * c.n_factors));
+    if (has_bias(c)) CF_TRY(dalloc(&e->slotVbc, (size_t)nV));
+    e->det_tmp_bytes = det_ranks_scratch(n, rows);
+    if (e->det_tmp_bytes) {
+        hipError_t he = hipMalloc(&e->det_tmp, e->det_tmp_bytes);
+        if (he != hipSuccess) return fail(CF_ENOMEM, std::string("hipMalloc (sort scratch): ") + hipGetErrorString(he));
+    }
+    e->det_cap = n;
+    return CF_OK;
+}
+
 int ensure_batch(cf_engine* e, int B) {
     CF_TRY(ensure_slots(e));
+    if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap)));
     if (B <= e->Bcap) return CF_OK;
     CF_HIP(hipStreamSynchronize(e->stream));
     CF_HIP(hipStreamSynchronize(e->side));
@@ -302,6 +340,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.indices_t = e->indices_t;
     a.pos_set = e->neg_check ? e->pos_set : nullptr;
     a.pos_mask = e->pos_mask;
+    a.lane_draw = e->neg_check == 2 ? 1 : 0;
     a.U = e->U; a.AU = e->AU; a.GU = e->GU;
     a.V = e->V; a.AV = e->AV; a.GV = e->GV;
     a.b = e->b; a.Ab = e->Ab; a.Gb = e->Gb;
@@ -325,6 +364,20 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.count_items = (!c.dense_item_apply || e->item_reduce) ? 1 : 0;
     a.items_grad_only = (c.dense_item_apply && e->item_reduce) ? 1 : 0;
     if (c.dense_item_apply && e->item_reduce == 2) a.capV = 0;  // duplicates: float atomics
+    if (e->det) {   // compact slots at off[row] + rank, no caps, no atomics
+        a.offU = e->det_off;
+        a.offV = e->det_off + c.n_users;
+        a.slotU = e->slotUc;
+        a.slotV = e->slotVc;
+        a.slotVb = has_bias(c) ? e->slotVbc : nullptr;
+        a.capU = a.capV = 1 << 30;
+        a.GVrep = nullptr;
+        a.repV = 0;
+        if (c.dense_item_apply) {   // the item reduce (item_reduce 1): stores, no atomics
+            a.count_items = 1;
+            a.items_grad_only = 1;
+        }
+    }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
     a.plr_kind = c.plr_kind;
@@ -499,10 +552,13 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
     p.clip = c.model == CF_CML ? 1 : 0;
-    p.capU = e->capU;
-    p.capV = e->capV;
-    p.GVrep = e->GVrep;
-    p.repV = e->GVrep ? e->hot_rep - 1 : 0;
+    p.capU = a.capU;
+    p.capV = a.capV;
+    p.GVrep = a.GVrep;
+    p.repV = a.repV;
+    p.offU = a.offU;
+    p.offV = a.offV;
+    p.slotVb = a.slotVb;
     p.n_items = c.n_items;
     p.count_users = a.count_users;
     p.count_items = a.count_items;
@@ -515,8 +571,8 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.rankV = e->rankV_[k];
     p.nV = (int64_t)B * items_per_pair(c);
     p.shard_u0 = e->shard_u0;
-    p.slotU = e->slotU;
-    p.slotV = e->slotV;
+    p.slotU = a.slotU;
+    p.slotV = a.slotV;
     p.cntU = e->cntU_[k];
     p.cntV = e->cntV_[k];
     p.U = e->U; p.AU = e->AU; p.GU = e->GU;
@@ -545,8 +601,20 @@ int pending_clips(cf_engine* e) {
     return CF_OK;
 }
 
+// deterministic mode: replace the batch's atomic ranks by sort-based ones
+// (and write off[row]) before its gradient launch
+int det_ranks(cf_engine* e, const StepArgs& a) {
+    if (!e->det) return CF_OK;
+    const cf_config& c = e->cfg;
+    const int64_t nU = (int64_t)a.B * users_per_pair(c), nV = (int64_t)a.B * items_per_pair(c);
+    CF_HIP(launch_det_ranks(a.occU, nU, a.occV, nV, c.n_users, c.n_users + c.n_items, a.rankU, a.rankV,
+                            e->det_off, e->det_keys, e->det_vals, e->det_tmp, e->det_tmp_bytes, e->stream));
+    return CF_OK;
+}
+
 int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
+    CF_TRY(det_ranks(e, a));
     ApplyArgs p = apply_args(e, a, B, k, loss_acc);
     if (next && e->pipeline == 2) {
         p.n_partial = grad_blocks(a, true);   // the launch with draw blocks keeps 256-lane groups
@@ -671,7 +739,7 @@ int discard_pending(cf_engine* e) {
 
 // a user-sharded GBPR engine steps only through the group exchange
 int check_not_xchg(cf_engine* e) {
-    if (e->cfg.model == CF_GBPR && e->world > 1)
+    if (e->cfg.model == CF_GBPR && e->group_source_global)
         return fail(CF_ESTATE, "user-sharded GBPR steps through cf_xchg_begin/serve/grad/finish");
     return CF_OK;
 }
@@ -908,6 +976,9 @@ int cf_destroy(cf_engine* e) {
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
     dfree(e->slotU); dfree(e->slotV); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
+    dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
+    dfree(e->slotVbc);
+    if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
@@ -1233,6 +1304,7 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         e->set ^= 1;
         CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
     }
+    CF_TRY(det_ranks(e, a));
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
@@ -1469,7 +1541,7 @@ int cf_set_group_source(cf_engine* e, const int64_t* indptr_t, const int32_t* in
     CF_TRY(check_engine(e));
     const cf_config& c = e->cfg;
     if (c.model != CF_GBPR) return fail(CF_EINVAL, "group sources exist only for GBPR");
-    if (e->world < 2) return fail(CF_ESTATE, "call cf_set_shard first (world > 1)");
+    if (e->h_bounds.empty()) return fail(CF_ESTATE, "call cf_set_shard first");
     if (!indptr_t || !indices_t || nnz < 1) return fail(CF_EINVAL, "null / empty item->user CSR");
     if (indptr_t[0] != 0 || indptr_t[c.n_items] != nnz) return fail(CF_EINVAL, "indptr_t does not span nnz");
     const int64_t nu = e->h_bounds[e->world];
@@ -1519,10 +1591,11 @@ int cf_bind_exchange(cf_engine* e, void* send_ids, void* rows, void* grads, int6
 static int check_xchg(cf_engine* e, int stage) {
     CF_TRY(check_engine(e));
     const cf_config& c = e->cfg;
-    if (c.model != CF_GBPR || !c.dense_item_apply || e->world < 2)
-        return fail(CF_ESTATE, "the group exchange needs GBPR, dense_item_apply=1 and cf_set_shard(world > 1)");
+    if (c.model != CF_GBPR || !c.dense_item_apply || e->h_bounds.empty())
+        return fail(CF_ESTATE, "the group exchange needs GBPR, dense_item_apply=1 and cf_set_shard");
     if (!e->group_source_global) return fail(CF_ESTATE, "set the global item->user CSR first (cf_set_group_source)");
     if (e->x_stage != stage) return fail(CF_ESTATE, "exchange calls out of order (begin, serve, grad, finish)");
+    if (e->det) return fail(CF_ESTATE, "deterministic mode does not cover the GBPR group exchange (float atomics of served rows)");
     return CF_OK;
 }
 
@@ -1738,10 +1811,10 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "neg_check") {
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "neg_check must be 0 or 1");
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "neg_check must be 0, 1 or 2");
         CF_TRY(discard_pending(e));
         e->neg_check = (int)value;
-        if (value == 1 && e->pairs && !e->pos_set) CF_TRY(build_pos_set(e));
+        if (value >= 1 && e->pairs && !e->pos_set) CF_TRY(build_pos_set(e));
         return CF_OK;
     }
     if (n == "item_reduce") {
@@ -1751,6 +1824,15 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_HIP(hipStreamSynchronize(e->stream));
         e->item_reduce = (int)value;
         e->slots_ready = false;
+        return CF_OK;
+    }
+    if (n == "deterministic") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "deterministic must be 0 or 1");
+        if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        e->det = (int)value;
+        if (e->det && e->Bcap > 0) CF_TRY(ensure_det(e, e->Bcap));
         return CF_OK;
     }
     if (n == "grad_path") {

@@ -68,6 +68,7 @@ struct StepArgs {
     // (u << 32 | i) keys, linear probing (null: scan the user's CSR row)
     const unsigned long long* __restrict__ pos_set;
     uint64_t pos_mask;                      // capacity - 1 (power of two)
+    int lane_draw;                          // 1: one lane per pair (neg_check 2, with the set)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
     float* __restrict__ V; float* __restrict__ AV; float* __restrict__ GV;
@@ -86,6 +87,13 @@ struct StepArgs {
     int capU, capV;               // occurrences at rank >= cap use float atomics into G
     float* __restrict__ GVrep;    // [repV][n_items, d] extra item accumulators (hot rows)
     int repV;                     // replica mask: item occurrence k >= capV adds to copy k & repV
+    // deterministic mode (cf_set_option "deterministic"): ranks come from a
+    // stable sort of the batch's row ids, every occurrence of a duplicated row
+    // owns the compact slot off[row] + rank (no caps, no float atomics), the
+    // GBPR / PLR item-bias gradient too (slotVb); null = the fast path
+    const int32_t* __restrict__ offU;   // [n_users] first sorted position of each touched row
+    const int32_t* __restrict__ offV;   // [n_items]
+    float* __restrict__ slotVb;         // [B*(1+W)] bias gradient per item occurrence
     double* __restrict__ loss_partial;  // [grad grid]
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
@@ -139,6 +147,9 @@ struct ApplyArgs {
     int64_t shard_u0;
     const float* __restrict__ slotU;
     const float* __restrict__ slotV;
+    const int32_t* __restrict__ offU;    // deterministic mode (StepArgs)
+    const int32_t* __restrict__ offV;
+    const float* __restrict__ slotVb;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -248,6 +259,15 @@ struct PackArgs {
     int32_t* occU; int32_t* occV; int32_t* bad;
 };
 hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
+// deterministic ranks (cf_det.hip): a stable radix sort of the batch's row ids
+// (users, then items offset by n_users) gives every occurrence its rank among
+// the earlier occurrences of its row, and off[row] = the row's first sorted
+// position; tmp / keys / vals sized by det_ranks_scratch
+size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows);
+hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV, int64_t nV,
+                            int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
+                            int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
+                            hipStream_t s);
 hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
                                 uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,

@@ -206,7 +206,9 @@ __device__ __forceinline__ void gstore(float* __restrict__ S, int64_t r, int d, 
 // exchange and those of an uncounted table go to float atomics: -1 - k means
 // accumulator copy k (0 = G itself; items spread a hot row over repV + 1
 // copies by rank, so its atomics do not all queue on one address)
-__device__ __forceinline__ int64_t slot_of(int count, int64_t r, int rank, int cap, int rep) {
+__device__ __forceinline__ int64_t slot_of(int count, int64_t r, int rank, int cap, int rep,
+                                           const int32_t* __restrict__ off) {
+    if (off != nullptr) return count >= 2 ? (int64_t)off[r] + rank : -1;  // deterministic: compact
     if (count >= 2 && !(count & kRemoteFlag) && rank < cap) return r * (int64_t)cap + rank;
     return -1 - (rank & rep);
 }
@@ -241,12 +243,16 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
     }
 }
 
-__device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g) {
+__device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g,
+                                            int64_t slot) {
     // GBPR item bias: one scalar row
     if (count == 1 && !a.items_grad_only) {
         const float acc = fmaf(g, g, a.Ab[r]);
         a.Ab[r] = acc;
         a.b[r] -= adagrad_delta(a.lr, g, acc);
+    } else if (a.slotVb != nullptr) {   // deterministic: stored, summed in rank order
+        if (count == 1) a.Gb[r] = g;    // multi-rank item reduce: the sole writer
+        else a.slotVb[slot] = g;
     } else {
         unsafeAtomicAdd(a.Gb + r, g);
     }
@@ -454,9 +460,138 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// prep, one lane per pair (neg_check = 2): with the Pos(u) set a pair needs no
+// cooperative row scan, so a wave draws 64 pairs at once -- 8x the pairs of
+// the 8-lane groups per wave generation -- and every negative's probes are in
+// flight together.  Same draw sequence as prep_body (negative w takes the
+// first attempt k = 0, 1, .. of draw(key, (w << 32) + k) outside Pos(u)), so
+// the same batches.  Measured SLOWER than the 8-lane groups at every bench
+// config (cfg2 draw 135 vs 118 us, apply + draw 266 vs 232 us; cfg4 apply +
+// draw 100 vs 67 us): 64 scattered probes and returning count atomics per
+// wave instruction serialise in the address path, and 8-lane groups keep
+// more waves -- more independent chains -- in flight.  Kept as an option.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ bool lane_prep(const StepArgs& a) {
+    return a.lane_draw != 0 && (!a.sample || a.pos_set != nullptr);
+}
+
+template <int MODEL, int WT>
+__device__ __forceinline__ void prep_lane_body(const StepArgs& a, int block) {
+    const int p = block * kBlock + (int)threadIdx.x;
+    if (p >= a.B) return;  // no block barrier below
+    constexpr int NJ = WT > 0 ? WT : 1;
+    const int W = WT > 0 ? WT : a.W;
+    const int G = (MODEL == GBPR) ? a.G : 0;
+    const int B = a.B;
+    int u, i;
+    uint64_t key = 0;
+    if (a.sample) {
+        const uint64_t slot = a.slot_base + (uint64_t)p;
+        const int4 pr = a.pairs[permute(slot, a.perm)];   // sampler_ranking.py:24
+        u = pr.x;
+        i = pr.y;
+        key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
+    } else {
+        u = a.occU[p];
+        i = a.occV[p];
+    }
+    int64_t cb = 0, ce = 0;   // GBPR: the item's user column, fetched beside the probes
+    if (MODEL == GBPR && a.sample) {
+        cb = a.indptr_t[i];
+        ce = a.indptr_t[i + 1];
+    }
+    for (int w0 = 0; w0 < W; w0 += NJ) {
+        int32_t j[NJ];
+        if (a.sample) {
+            // negItems = randint(0, n_items), redrawn while j in Pos(u)
+            // (sampler_ranking.py:30-36), every negative's probe chain at once
+            uint64_t ctr[NJ], s[NJ];
+            unsigned long long kk[NJ];
+            uint32_t pend = 0;
+#pragma unroll
+            for (int q = 0; q < NJ; ++q) {
+                ctr[q] = (uint64_t)(w0 + q) << 32;
+                j[q] = draw_item(key, ctr[q]++, a.n_items);
+                kk[q] = ((unsigned long long)(uint32_t)u << 32) | (uint32_t)j[q];
+                s[q] = pos_slot(kk[q], a.pos_mask);
+                pend |= (w0 + q < W) ? (1u << q) : 0u;
+            }
+            while (pend) {
+                unsigned long long t[NJ];
+#pragma unroll
+                for (int q = 0; q < NJ; ++q) t[q] = ((pend >> q) & 1u) ? a.pos_set[s[q]] : kPosEmpty;
+#pragma unroll
+                for (int q = 0; q < NJ; ++q) {
+                    if (!((pend >> q) & 1u)) continue;
+                    if (t[q] == kk[q]) {            // a positive: the next attempt
+                        j[q] = draw_item(key, ctr[q]++, a.n_items);
+                        kk[q] = ((unsigned long long)(uint32_t)u << 32) | (uint32_t)j[q];
+                        s[q] = pos_slot(kk[q], a.pos_mask);
+                    } else if (t[q] == kPosEmpty) { // not in Pos(u): accepted
+                        pend &= ~(1u << q);
+                    } else {                        // another key: probe on
+                        s[q] = (s[q] + 1) & a.pos_mask;
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NJ; ++q)
+                if (w0 + q < W) a.occV[B + (int64_t)p * W + w0 + q] = j[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < NJ; ++q)
+                if (w0 + q < W) j[q] = a.occV[B + (int64_t)p * W + w0 + q];
+        }
+        if (a.count_items) {
+#pragma unroll
+            for (int q = 0; q < NJ; ++q)
+                if (w0 + q < W) a.rankV[B + (int64_t)p * W + w0 + q] = atomicAdd(&a.cntV[j[q]], 1);
+        }
+    }
+    if (MODEL == GBPR) {
+        for (int k = 0; k < G; ++k) {
+            int32_t g;
+            if (a.sample) {
+                // group = np.random.choice(item_posUserList[i], gsize) (sampler_gbpr.py:41)
+                const uint64_t h = mix64(key + ((uint64_t)(kMaxNeg + k) << 32));
+                g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
+                g = (g >= a.shard_u0 && g < a.shard_u1) ? g - a.shard_u0 : -1 - g;
+                a.occU[B + (int64_t)p * G + k] = g;
+            } else {
+                g = a.occU[B + (int64_t)p * G + k];
+            }
+            if (a.count_users && g >= 0) a.rankU[B + (int64_t)p * G + k] = atomicAdd(&a.cntU[g], 1);
+        }
+    }
+    if (a.sample) {
+        a.occU[p] = u;
+        a.occV[p] = i;
+    }
+    if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
+    if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
+}
+
+// the draw + count of one block of a step's batch: one lane per pair when no
+// row scan is needed (lane_prep), else the 8-lane cooperative row scan
+template <int MODEL>
+__device__ __forceinline__ void prep_any(const StepArgs& a, int block) {
+    if (lane_prep(a)) {
+        if (a.W == 1) prep_lane_body<MODEL, 1>(a, block);
+        else if (a.W == 5) prep_lane_body<MODEL, 5>(a, block);
+        else prep_lane_body<MODEL, 0>(a, block);
+    } else {
+        prep_body<MODEL>(a, block);
+    }
+}
+
+__host__ __device__ __forceinline__ int prep_pairs_per_block(const StepArgs& a) {
+    return lane_prep(a) ? kBlock : kPrepPairsPerBlock;
+}
+
 template <int MODEL>
 __global__ __launch_bounds__(kBlock) void prep_kernel(StepArgs a) {
-    prep_body<MODEL>(a, blockIdx.x);
+    prep_any<MODEL>(a, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -483,7 +618,7 @@ struct NegRows {
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 c[w] = a.count_items ? a.cntV[j[w]] : 0;
-                sl[w] = slot_of(c[w], j[w], rk[w], a.capV, a.repV);
+                sl[w] = slot_of(c[w], j[w], rk[w], a.capV, a.repV, a.offV);
                 gload<EPL>(a.V, j[w], a.d, gl, v[w]);
             }
         }
@@ -496,7 +631,7 @@ struct NegRows {
             j[0] = a.occV[a.B + p * a.W + w];
             const int rk = a.count_items ? a.rankV[a.B + p * a.W + w] : 0;
             c[0] = a.count_items ? a.cntV[j[0]] : 0;
-            sl[0] = slot_of(c[0], j[0], rk, a.capV, a.repV);
+            sl[0] = slot_of(c[0], j[0], rk, a.capV, a.repV, a.offV);
             gload<EPL>(a.V, j[0], a.d, gl, v[0]);
             return 0;
         }
@@ -526,8 +661,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
         J.prefetch(a, p, gl);
         const int cu = a.count_users ? a.cntU[u] : 0;
         const int ci = a.count_items ? a.cntV[i] : 0;
-        const int64_t su = slot_of(cu, u, ru, a.capU, 0);
-        const int64_t si = slot_of(ci, i, ri, a.capV, a.repV);
+        const int64_t su = slot_of(cu, u, ru, a.capU, 0, a.offU);
+        const int64_t si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
         float uu[EPL], vi[EPL];
         gload<EPL>(a.U, u, d, gl, uu);
         gload<EPL>(a.V, i, d, gl, vi);
@@ -613,7 +748,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gu[s] = fmaf(-c, J.v[sl][s], gu[s]);
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
-                if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj);
+                if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj, J.sl[sl]);
                 gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j, J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
             }
             const float rg = a.rho / Gf;
@@ -637,10 +772,10 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     continue;
                 }
                 const int cg = a.cntU[g];
-                const int64_t sg_ = slot_of(cg, g, a.rankU[B + p * G + k2], a.capU, 0);
+                const int64_t sg_ = slot_of(cg, g, a.rankU[B + p * G + k2], a.capU, 0, a.offU);
                 gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
-            if (gl == 0) bias_finish(a, i, ci, sc);
+            if (gl == 0) bias_finish(a, i, ci, sc, si);
             gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else if (MODEL == PLR) {
             // tuple ranking: s_x = <u, v_x> + b_x over the tuple's items
@@ -691,7 +826,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gj[s] = ds[w + 1] * uu[s] + a.reg * J.v[w][s];
                     sq = fmaf(J.v[w][s], J.v[w][s], sq);
                 }
-                if (a.train_bias && gl == 0) bias_finish(a, J.j[w], J.c[w], ds[w + 1] + a.reg * bx[w + 1]);
+                if (a.train_bias && gl == 0) bias_finish(a, J.j[w], J.c[w], ds[w + 1] + a.reg * bx[w + 1], J.sl[w]);
                 gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[w], J.c[w], J.sl[w], d, gl, J.v[w], gj, a);
             }
             float gi[EPL];
@@ -702,7 +837,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 sq = fmaf(vi[s], vi[s], sq);
             }
             gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
-            if (a.train_bias && gl == 0) bias_finish(a, i, ci, ds[0] + a.reg * bx[0]);
+            if (a.train_bias && gl == 0) bias_finish(a, i, ci, ds[0] + a.reg * bx[0], si);
             gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
         } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
@@ -809,7 +944,7 @@ template <int MODEL, int EPL, int WT>
 __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a, StepArgs nx, int ng, int np) {
     int idx;
     if (minor_block(blockIdx.x, ng, np, idx))
-        prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
+        prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
         grad_body<MODEL, EPL, WT>(a, idx);
 }
@@ -937,12 +1072,12 @@ struct PairRows {
         }
     }
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
-        su = slot_of(cu, u, ru, a.capU, 0);
-        si = slot_of(ci, i, ri, a.capV, a.repV);
+        su = slot_of(cu, u, ru, a.capU, 0, a.offU);
+        si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
 #pragma unroll
-        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV);
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
 #pragma unroll
-        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0);
+        for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0, a.offU);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
         const bool item_acc = !a.items_grad_only;
         gload_acc<EPL>(a.AV, i, a.d, gl, item_acc && ci == 1, ai);
@@ -1015,7 +1150,7 @@ struct PairRows {
                     gu[s] = fmaf(-c, vj[w][s], gu[s]);
                     gj[s] = -c * uu[s];
                 }
-                if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w]);
+                if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w], sj[w]);
                 gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
             }
             const float rg = a.rho;  // rho / G with G == 1
@@ -1033,7 +1168,7 @@ struct PairRows {
                 gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
             else  // another rank's user: its gradient row goes back to the owner
                 gstore<EPL>(a.xgrads, -1 - g[0], d, gl, gg);
-            if (gl == 0) bias_finish(a, i, ci, sc);
+            if (gl == 0) bias_finish(a, i, ci, sc, si);
             gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
         } else {  // CML
             float du[EPL];
@@ -1148,7 +1283,7 @@ template <int MODEL, int EPL, int WT, int P>
 __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
     int idx;
     if (minor_block(blockIdx.x, ng, np, idx))
-        prep_body<MODEL == GBPR ? GBPR : BPR>(nx, idx);
+        prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
         grad_fast_body<MODEL, EPL, WT, P>(a, idx);
 }
@@ -1191,12 +1326,13 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     // group exchange served (all its contributions went to G)
     const int flagged = c & kRemoteFlag;
     const int local = c & (kRemoteFlag - 1);
-    const int ns = flagged ? 0 : (local < cap ? local : cap);
+    const int32_t* off = isU ? a.offU : a.offV;   // deterministic mode: compact slots
+    const int ns = flagged ? 0 : (off != nullptr || local < cap) ? local : cap;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
     {
         const float* S = isU ? a.slotU : a.slotV;
-        const int64_t s0 = r * (int64_t)cap;
+        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
 #ifndef CF_APPLY_NF
 #define CF_APPLY_NF 4
 #endif
@@ -1214,7 +1350,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
                 }
         }
     }
-    if (flagged || local > cap) {  // the atomic sums: G, and for items the copies in use
+    if (off == nullptr && (flagged || local > cap)) {  // the atomic sums: G, and for items the copies in use
         const int nrep = isU ? 0 : a.repV;   // copies 1..repV (unused ones are zero)
         float h[EPL];
         gload<EPL>(G, r, a.d, gl, h);
@@ -1229,20 +1365,29 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
             row_zero<EPL>(Gk + r * a.d, a.d, gl);
         }
     }
+    // deterministic bias: the row's bias slots in rank order (lane 0)
+    float gbias = 0.f;
+    if (!isU && a.slotVb != nullptr && gl == 0 && a.Gb != nullptr) {
+        const int64_t s0 = (int64_t)off[r];
+        for (int t = 0; t < local; ++t) gbias += a.slotVb[s0 + t];
+    }
     if (reduce_only) {
         row_st<EPL>(G + r * (int64_t)a.d, a.d, gl, g);
-        if (gl == 0) cnt[r] = 0;
+        if (gl == 0) {
+            cnt[r] = 0;
+            if (a.slotVb != nullptr && a.Gb != nullptr) a.Gb[r] = gbias;
+        }
         return;
     }
     gapply_pre<EPL>(X, A, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
     if (gl == 0) {
         cnt[r] = 0;
         if (!isU && a.b != nullptr) {
-            const float gb = a.Gb[r];
+            const float gb = a.slotVb != nullptr ? gbias : a.Gb[r];
             const float ab = fmaf(gb, gb, a.Ab[r]);
             a.Ab[r] = ab;
             a.b[r] -= adagrad_delta(a.lr, gb, ab);
-            a.Gb[r] = 0.f;
+            if (a.slotVb == nullptr) a.Gb[r] = 0.f;
         }
     }
 }
@@ -1385,19 +1530,19 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
 #if CF_APPLY_PREP_ORDER == 2
     int idx;
     if (minor_block(blockIdx.x, napply, nprep, idx))
-        prep_body<MODEL>(a, idx);
+        prep_any<MODEL>(a, idx);
     else
         apply_body<EPL>(p, idx, napply);
 #elif CF_APPLY_PREP_ORDER == 1
     if ((int)blockIdx.x < nprep)
-        prep_body<MODEL>(a, blockIdx.x);
+        prep_any<MODEL>(a, blockIdx.x);
     else
         apply_body<EPL>(p, blockIdx.x - nprep, napply);
 #else
     if ((int)blockIdx.x < napply)
         apply_body<EPL>(p, blockIdx.x, napply);
     else
-        prep_body<MODEL>(a, blockIdx.x - napply);
+        prep_any<MODEL>(a, blockIdx.x - napply);
 #endif
 }
 
@@ -1683,7 +1828,8 @@ int grad_blocks_max(int B) { return (B + kWave / kGL - 1) / (kWave / kGL); }
 
 hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    const int blocks = (a.B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock;
+    const int ppb = prep_pairs_per_block(a);
+    const int blocks = (a.B + ppb - 1) / ppb;
     switch (a.model) {
         case GBPR: hipLaunchKernelGGL(prep_kernel<GBPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
         default: hipLaunchKernelGGL(prep_kernel<BPR>, dim3(blocks), dim3(kBlock), 0, s, a); break;
@@ -1692,7 +1838,9 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s) {
 }
 
 static int prep_blocks(const StepArgs* nx) {
-    return (nx && nx->B > 0) ? (nx->B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock : 0;
+    if (!nx || nx->B <= 0) return 0;
+    const int ppb = prep_pairs_per_block(*nx);
+    return (nx->B + ppb - 1) / ppb;
 }
 
 template <int MODEL, int WT>
@@ -1810,7 +1958,7 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
 template <int MODEL>
 static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     const int na = apply_grid(p);
-    const int np = (a.B + kPrepPairsPerBlock - 1) / kPrepPairsPerBlock;
+    const int np = prep_blocks(&a);
     const dim3 grid(na + np), block(kBlock);
     switch (epl_for(p.d)) {
         case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL>), grid, block, 0, s, p, a, na); break;

@@ -370,9 +370,17 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                1 = probe an open-addressed set of the (u, i) pairs (16 B
  *                per interaction, built when selected; ~1 sector per
  *                candidate), 0 = scan the user's sorted CSR row (default:
- *                8 candidates per scan; A/B at cfg2 within noise).  The same
- *                batches either way: both take each negative's first attempt
- *                outside Pos(u) in the same draw sequence.
+ *                8 candidates per scan; A/B at cfg2 within noise), 2 = the
+ *                set probed by one lane per pair (measured slower, DESIGN).
+ *                The same batches every way: each negative takes its first
+ *                attempt outside Pos(u) in the same draw sequence.
+ *   "deterministic" 1 = bitwise-reproducible steps: occurrence ranks from a
+ *                stable sort of the batch's row ids, every occurrence of a
+ *                duplicated row stored in its own compact slot and summed in
+ *                batch order, no float atomics anywhere (the GBPR group
+ *                exchange is excluded); 0 = the fast path (default), whose
+ *                rank order -- and so the last bits of duplicate sums --
+ *                follows the order the count atomics land.
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
  *                item occurrences are counted like user ones, a row seen
  *                once stores its gradient row into the bound buffer, a

@@ -1,0 +1,97 @@
+"""Deterministic mode (cf_set_option "deterministic", SURVEY 5: "sort-based
+dedup, no float atomics").
+
+The fast path ranks a duplicated row's occurrences by the order their count
+atomics land and adds the occurrences of hot rows with float atomics, so the
+last bits of a step depend on timing.  TF1's CPU path (UnsortedSegmentSum
+behind AdagradOptimizer, bprmf.py:83-88) is deterministic.  With the option
+set, two runs from the same state must be BITWISE identical -- here on a
+reduced graph with the cfg2 Zipf(0.8) item skew, where hundreds of rows are
+far above the fast path's slot cap and would take atomics -- and the result
+must still match the float64 oracle (1e-5 relative).
+"""
+import numpy as np
+import pytest
+
+from oracle import cf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TABLES = {"bpr": ("user", "item", "acc_user", "acc_item"),
+          "amf": ("user", "item", "acc_user", "acc_item"),
+          "cml": ("user", "item", "acc_user", "acc_item"),
+          "gbpr": ("user", "item", "bias", "acc_user", "acc_item", "acc_bias")}
+HP = {"bpr": dict(reg=0.02), "amf": dict(reg=0.05, reg_adv=1.0),
+      "cml": dict(margin=1.0, reg_cov=1.0, clip_norm=1.0), "gbpr": dict(rho=0.4, reg=0.01)}
+
+
+@pytest.fixture(scope="module")
+def skewed_graph():
+    from collaborativefilteringusingtensorflow_amd.engine import synth_graph
+    return synth_graph(40_000, 4_000, 30.0, 0.8, 20261015, n_threads=8)
+
+
+def _run(model, graph, d, W, B, steps, det, dense=False, phase=False):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    ip, ix = graph
+    e = Engine(model, len(ip) - 1, 4_000, d, n_neg=W, gsize=1, seed=17, dense_item_apply=dense,
+               **HP[model])
+    e.set_option("deterministic", 1 if det else 0)
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=3)
+    if phase:
+        e.begin_phase(1)
+    loss = e.train_steps(B, steps)
+    out = {t: e.get_table(t) for t in TABLES[model]}
+    e.close()
+    return loss, out
+
+
+@pytest.mark.parametrize("model,d,W,dense", [("bpr", 64, 1, False), ("gbpr", 64, 5, False),
+                                             ("cml", 32, 5, False), ("amf", 32, 5, False),
+                                             ("bpr", 32, 1, True)],
+                         ids=["bpr", "gbpr", "cml", "amf-adv", "bpr-dense-items"])
+def test_two_runs_bitwise_identical(skewed_graph, model, d, W, dense):
+    a = _run(model, skewed_graph, d, W, 16384, 6, det=True, dense=dense, phase=(model == "amf"))
+    b = _run(model, skewed_graph, d, W, 16384, 6, det=True, dense=dense, phase=(model == "amf"))
+    assert a[0] == b[0]                                   # the loss, bit for bit
+    for t in TABLES[model]:
+        assert np.array_equal(a[1][t], b[1][t]), t
+    # the fast path trains the same model (fp32 summation order aside)
+    c = _run(model, skewed_graph, d, W, 16384, 6, det=False, dense=dense, phase=(model == "amf"))
+    assert abs(c[0] - a[0]) <= 1e-5 * abs(a[0])
+    for t in TABLES[model]:
+        ref = a[1][t].astype(np.float64)
+        assert np.abs(c[1][t] - ref).max() <= 1e-5 * np.abs(ref).max(), t
+
+
+@pytest.mark.parametrize("model", ["bpr", "gbpr", "cml"])
+def test_deterministic_steps_match_oracle(skewed_graph, model):
+    """Host-fed deterministic steps on device-drawn batches with hot rows
+    (hundreds of occurrences of the Zipf head) against the float64 oracle."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    ip, ix = skewed_graph
+    nu, ni, d, W, B = len(ip) - 1, 4_000, 32, (1 if model == "bpr" else 5), 8192
+    e = Engine(model, nu, ni, d, n_neg=W, gsize=1, seed=23, **HP[model])
+    e.set_option("deterministic", 1)
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=4)
+    T = {t: e.get_table(t).astype(np.float64) for t in TABLES[model]}
+    hot = 0
+    for _ in range(4):
+        pairs, negs, groups = e.sample(B)
+        hot = max(hot, int(np.bincount(pairs[:, 1], minlength=ni).max()))
+        lg = e.step(pairs, negs, groups)
+        if model == "bpr":
+            lo = O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.02)
+        elif model == "gbpr":
+            lo = O.gbpr_step(T["user"], T["item"], T["bias"], T["acc_user"], T["acc_item"], T["acc_bias"],
+                             pairs, negs, groups, 0.4, 0.01)
+        else:
+            lo = O.cml_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 1.0, 1.0, 1.0)
+        assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
+    assert hot > 100    # rows far above the fast path's slot cap (32) were summed without atomics
+    for t in TABLES[model]:
+        got = e.get_table(t).astype(np.float64)
+        assert np.abs(got - T[t]).max() <= 1e-5 * np.abs(T[t]).max(), t
+    e.close()

@@ -86,9 +86,7 @@ class OracleGroupShard(object):
         self.pending = (np.concatenate([u_idx, flat[loc] - self.u0]),
                         np.concatenate([gUu, gUg[loc]]))
         self.grads[:] = torch.as_tensor(gUg[~loc][np.argsort(self.slot[~loc])])
-        n_items = self.V.shape[0]
-        GV = self.item_grad[:n_items * d].numpy().reshape(n_items, d)
-        Gb = self.item_grad[n_items * d:].numpy()
+        GV, Gb = self._gv(), self._gb()
         np.add.at(GV, np.concatenate([i_idx, negs.reshape(-1)]),
                   np.concatenate([gVi, gVj.reshape(-1, d)]))
         np.add.at(Gb, np.concatenate([i_idx, negs.reshape(-1)]),
@@ -101,10 +99,16 @@ class OracleGroupShard(object):
         O.dedup_adagrad(self.U, self.AU, np.concatenate([rows, ids]),
                         np.concatenate([grads, self.serve_grads[:n].numpy()]), self.lr)
 
-    def step_items(self):
+    def _gv(self):
         n_items, d = self.V.shape
-        GV = self.item_grad[:n_items * d].numpy().reshape(n_items, d)
-        Gb = self.item_grad[n_items * d:].numpy()
+        return self.item_grad[:n_items * d].numpy().reshape(n_items, d)
+
+    def _gb(self):
+        n_items, d = self.V.shape
+        return self.item_grad[n_items * d:].numpy()
+
+    def step_items(self):
+        GV, Gb = self._gv(), self._gb()
         rows = np.nonzero(np.any(GV != 0, axis=1))[0]
         self.AV[rows] += GV[rows] ** 2
         self.V[rows] -= self.lr * GV[rows] / np.sqrt(self.AV[rows])
@@ -114,18 +118,71 @@ class OracleGroupShard(object):
         self.item_grad.zero_()
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, b0, q):
+class RSOracleGroupShard(OracleGroupShard):
+    """Item-range ownership (ReduceScatterItems): V, b, their accumulators and
+    the item / bias gradients in buffers padded to world * chunk rows."""
+
+    def __init__(self, U_local, V, b, bounds, rank, rho, reg, world, lr=0.1):
+        super(RSOracleGroupShard, self).__init__(U_local, V, b, bounds, rank, rho, reg, lr)
+        n, d = V.shape
+        self.chunk = -(-n // world)
+        rows = world * self.chunk
+        f64 = dict(dtype=torch.float64)
+        self.Vfull, self.bfull = torch.zeros(rows * d, **f64), torch.zeros(rows, **f64)
+        self.AVfull, self.Abfull = torch.full((rows * d,), 0.1, **f64), torch.full((rows,), 0.1, **f64)
+        self.Vfull[:n * d] = torch.from_numpy(V.ravel())
+        self.bfull[:n] = torch.from_numpy(b)
+        self.V = self.Vfull.numpy()[:n * d].reshape(n, d)
+        self.AV = self.AVfull.numpy()[:n * d].reshape(n, d)
+        self.b, self.Ab = self.bfull.numpy()[:n], self.Abfull.numpy()[:n]
+        self.item_grad = torch.zeros(rows * d, **f64)
+        self.bias_grad = torch.zeros(rows, **f64)
+
+    def _gv(self):
+        n, d = self.V.shape
+        return self.item_grad.numpy()[:n * d].reshape(n, d)
+
+    def _gb(self):
+        return self.bias_grad.numpy()[:self.V.shape[0]]
+
+    def clear_item_grad(self):
+        self.item_grad.zero_()
+        self.bias_grad.zero_()
+
+    def step_items_range(self, r0, r1, grad, grad_bias):
+        n, d = self.V.shape
+        r1 = min(r1, n)
+        GV = grad.numpy().reshape(-1, d)[:r1 - r0]
+        Gb = grad_bias.numpy()[:r1 - r0]
+        rows = np.nonzero(np.any(GV != 0, axis=1))[0]
+        self.AV[r0 + rows] += GV[rows] ** 2
+        self.V[r0 + rows] -= self.lr * GV[rows] / np.sqrt(self.AV[r0 + rows])
+        rb = np.nonzero(Gb != 0)[0]
+        self.Ab[r0 + rb] += Gb[rb] ** 2
+        self.b[r0 + rb] -= self.lr * Gb[rb] / np.sqrt(self.Ab[r0 + rb])
+
+
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q, exchange="allreduce"):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from collaborativefilteringusingtensorflow_amd.distributed import (GroupExchangeStep,
-                                                                       shard_users)
+                                                                       ReduceScatterItems, shard_users)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
                             world_size=world)
     ip = fold["train_indptr"]
     bounds = [shard_users(ip, world, r)[0] for r in range(world)] + [U0.shape[0]]
     u0, u1 = bounds[rank], bounds[rank + 1]
-    be = OracleGroupShard(U0[u0:u1], V0, b0, bounds, rank, rho=0.4, reg=0.01)
-    step = GroupExchangeStep(be, be.item_grad, world)
+    if exchange == "rs_ag":
+        be = RSOracleGroupShard(U0[u0:u1], V0, b0, bounds, rank, rho=0.4, reg=0.01, world=world)
+        d, ch = V0.shape[1], be.chunk
+        items = ReduceScatterItems(be.item_grad, torch.zeros(ch * d, dtype=torch.float64),
+                                   [(be.Vfull, d), (be.bfull, 1)], ch, rank, grad_bias=be.bias_grad,
+                                   bias_slice=torch.zeros(ch, dtype=torch.float64),
+                                   state=[(be.AVfull, d), (be.Abfull, 1)])
+        step = GroupExchangeStep(be, items, world)
+    else:
+        be = OracleGroupShard(U0[u0:u1], V0, b0, bounds, rank, rho=0.4, reg=0.01)
+        step = GroupExchangeStep(be, be.item_grad, world)
     n_remote = 0
     for pairs, negs, groups in batches:
         mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
@@ -134,7 +191,8 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q):
         g = groups[mine]
         n_remote += int(np.sum((g < u0) | (g >= u1)))
         step(pairs=lp, negs=negs[mine], groups=g)
-    q.put((rank, u0, u1, be.U, be.V, be.b, be.AU, n_remote))
+    step.sync_state()
+    q.put((rank, u0, u1, be.U, be.V.copy(), be.b.copy(), be.AU, n_remote, be.AV.copy(), be.Ab.copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -158,8 +216,11 @@ def test_item_users_is_the_transpose(fold1):
         assert sorted(tu[tp[i]:tp[i + 1]].tolist()) == sorted(np.asarray(ru[rp[i]:rp[i + 1]]).tolist())
 
 
-@pytest.mark.parametrize("stream,world", [("gbpr_b100_g1_w5", 2), ("gbpr_b100_g3_w2", 2)])
-def test_group_exchange_equals_global_step(fold1, streams, stream, world):
+@pytest.mark.parametrize("stream,world,exchange", [("gbpr_b100_g1_w5", 2, "allreduce"),
+                                                   ("gbpr_b100_g3_w2", 2, "allreduce"),
+                                                   ("gbpr_b100_g1_w5", 2, "rs_ag"),
+                                                   ("gbpr_b100_g1_w5", 3, "rs_ag")])
+def test_group_exchange_equals_global_step(fold1, streams, stream, world, exchange):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(9)
     U0 = O.init_table(rng, (943, 8), dtype=np.float64)
@@ -170,7 +231,7 @@ def test_group_exchange_equals_global_step(fold1, streams, stream, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q, exchange))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -183,8 +244,10 @@ def test_group_exchange_equals_global_step(fold1, streams, stream, world):
     for pairs, negs, groups in batches:
         O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
     assert sum(r[7] for r in res) > 50          # the exchange actually carried members
-    for rank, u0, u1, Ul, Vr, br, AUl, _ in res:
+    for rank, u0, u1, Ul, Vr, br, AUl, _, AVr, Abr in res:
         np.testing.assert_allclose(Ul, U[u0:u1], rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(AUl, AU[u0:u1], rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(Vr, V, rtol=1e-12, atol=1e-14)
         np.testing.assert_allclose(br, b, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(AVr, AV, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(Abr, Ab, rtol=1e-12, atol=1e-14)

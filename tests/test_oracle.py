@@ -461,3 +461,43 @@ def test_ensemble_w_oracle_matches_literal_autograd(K, W, reg, lam, singles):
         for k in tabs:
             assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
             assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
+
+
+def test_fp32_oracle_drift_bounds_cml_tolerance(fold1):
+    """The CML trajectory tolerance of the GPU tests (elementwise rtol 5e-5,
+    atol 3e-6; tests/test_gpu_bench_configs.py, test_gpu_distributed.py):
+    the oracle itself in float32 -- the arithmetic width of TF1's CPU path --
+    leaves the strict band (rtol 1e-5, atol 1e-6) around the float64 oracle
+    within 28 steps of CML at the cfg3 shape (d=128, W=5: the rank weight
+    log(1 + n_items * ...) scales gradients by ~7 and the accumulators sum
+    squares up to ~300), while staying well inside the relaxed one (under 0.75 of it); BPR stays
+    inside the strict band."""
+    from oracle import cf_oracle as O
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    pairs_all = np.stack([np.repeat(np.arange(943), np.diff(ip)), ix], 1)
+
+    def ratio(a, b, rtol, atol):
+        return float(np.max(np.abs(a - b) / (atol + rtol * np.abs(b))))
+
+    out = {}
+    for model, d in (("cml", 128), ("bpr", 64)):
+        rng = np.random.RandomState(0)
+        U = O.init_table(rng, (943, d), truncated=(model != "cml"))
+        V = O.init_table(rng, (1682, d), truncated=(model != "cml"))
+        res = {}
+        for dt in (np.float32, np.float64):
+            r2 = np.random.RandomState(1)
+            T = [U.astype(dt), V.astype(dt), np.full((943, d), 0.1, dt), np.full((1682, d), 0.1, dt)]
+            for s in range(28):
+                p = pairs_all[r2.choice(len(pairs_all), 100, replace=False)]
+                n = r2.randint(0, 1682, (100, 5))
+                if model == "cml":
+                    O.cml_step(T[0], T[1], T[2], T[3], p, n, 1.0, 1.0, 1.0)
+                else:
+                    O.bpr_step(T[0], T[1], T[2], T[3], p, n, 0.05)
+            res[dt] = T
+        out[model] = [(ratio(a.astype(np.float64), b, 1e-5, 1e-6), ratio(a.astype(np.float64), b, 5e-5, 3e-6))
+                      for a, b in zip(res[np.float32], res[np.float64])]
+    assert max(r[0] for r in out["cml"]) > 1.0, out          # the strict band is not fp32-attainable
+    assert max(r[1] for r in out["cml"]) < 0.75, out         # the relaxed band holds it with headroom
+    assert max(r[0] for r in out["bpr"]) < 0.5, out
