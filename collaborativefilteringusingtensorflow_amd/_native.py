@@ -101,6 +101,8 @@ SIGNATURES = {
     "cf_set_group_source": (ctypes.c_int, [_P, _PI64, _PI32, _I64]),
     "cf_bind_exchange": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _P, _P, _I64]),
     "cf_xchg_begin": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32, _PI32]),
+    "cf_xchg_draw": (ctypes.c_int, [_P, _I32, _P, _PI32]),
+    "cf_xchg_adopt": (ctypes.c_int, [_P]),
     "cf_xchg_serve": (ctypes.c_int, [_P, _I64]),
     "cf_xchg_grad": (ctypes.c_int, [_P]),
     "cf_xchg_finish": (ctypes.c_int, [_P, _I64]),

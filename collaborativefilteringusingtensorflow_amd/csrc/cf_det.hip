@@ -28,23 +28,33 @@ __global__ void det_keys_kernel(const int32_t* __restrict__ occU, int64_t nU,
     }
 }
 
-// the first sorted position of every row present in the batch
-__global__ void det_heads_kernel(const int32_t* __restrict__ skeys, int64_t n,
-                                 int32_t* __restrict__ off) {
+// every user key sorts before every item key (items are offset by n_users),
+// so the items' sorted positions start at nU: a row's slot base is its first
+// sorted position inside its own table's part ([0, nU) users, [0, nV) items)
+__device__ __forceinline__ int64_t part_base(int32_t key, int64_t n_users, int64_t nU) {
+    return key >= n_users ? nU : 0;
+}
+
+// the first position of every row present in the batch, within its table's part
+__global__ void det_heads_kernel(const int32_t* __restrict__ skeys, int64_t n, int64_t n_users,
+                                 int64_t nU, int32_t* __restrict__ off) {
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nt = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t p = t0; p < n; p += nt)
-        if (p == 0 || skeys[p] != skeys[p - 1]) off[skeys[p]] = (int32_t)p;
+    for (int64_t p = t0; p < n; p += nt) {
+        const int32_t k = skeys[p];
+        if (p == 0 || k != skeys[p - 1]) off[k] = (int32_t)(p - part_base(k, n_users, nU));
+    }
 }
 
 __global__ void det_rank_kernel(const int32_t* __restrict__ skeys, const int32_t* __restrict__ svals,
-                                int64_t n, int64_t nU, const int32_t* __restrict__ off,
+                                int64_t n, int64_t n_users, int64_t nU, const int32_t* __restrict__ off,
                                 int32_t* __restrict__ rankU, int32_t* __restrict__ rankV) {
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nt = (int64_t)gridDim.x * blockDim.x;
     for (int64_t p = t0; p < n; p += nt) {
+        const int32_t k = skeys[p];
         const int32_t q = svals[p];
-        const int32_t rk = (int32_t)(p - off[skeys[p]]);
+        const int32_t rk = (int32_t)(p - part_base(k, n_users, nU) - off[k]);
         if (q < nU) rankU[q] = rk;
         else rankV[q - nU] = rk;
     }
@@ -84,9 +94,9 @@ hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, keys + n, vals, vals + n, (int)n, 0,
                                                       key_bits(n_rows), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(det_heads_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, n, off);
-    hipLaunchKernelGGL(det_rank_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, vals + n, n, nU, off,
-                       rankU, rankV);
+    hipLaunchKernelGGL(det_heads_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, n, n_users, nU, off);
+    hipLaunchKernelGGL(det_rank_kernel, dim3(grid_of(n)), dim3(256), 0, s, keys + n, vals + n, n, n_users, nU,
+                       off, rankU, rankV);
     return hipGetLastError();
 }
 

@@ -87,6 +87,7 @@ struct cf_engine {
     // "slot_max_user" = user cap); rows above their cap use float atomics
     float* slotU = nullptr;   // [n_users * capU, d]
     float* slotV = nullptr;   // [n_items * capV, d]
+    float* slotVb = nullptr;  // [n_items * capV] item-bias gradient beside each slot row (GBPR / PLR)
     int capU = 2, capV = 32;
     // hot item rows (occurrences past capV) spread their float atomics over
     // GV and hot_rep - 1 extra copies (cf_set_option "hot_replicas")
@@ -142,6 +143,12 @@ struct cf_engine {
     float *x_rows = nullptr, *x_grads = nullptr, *x_serve_rows = nullptr, *x_serve_grads = nullptr;
     int64_t x_send_cap = 0, x_recv_cap = 0;
     int x_stage = 0;                 // 0 idle, 1 begun, 2 served, 3 grads done
+    // the next exchange batch drawn ahead (cf_xchg_draw), taken by cf_xchg_adopt;
+    // send_ids holds two halves of send_cap ids, one per buffer set
+    bool x_pend = false;
+    StepArgs x_pend_args{};
+    int x_pend_set = 0, x_pend_B = 0, x_pend_sampler_B = 0;
+    int64_t x_pend_epoch = 0, x_pend_batch = 0;
 
     // split local step (cf_step_local_grad / cf_step_local_apply): the step
     // between its two halves, and a batch already drawn + counted by the
@@ -247,10 +254,12 @@ int ensure_slots(cf_engine* e) {
     CF_HIP(hipStreamSynchronize(e->stream));
     dfree(e->slotU);
     dfree(e->slotV);
+    dfree(e->slotVb);
     dfree(e->GVrep);
     CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
     if (!c.dense_item_apply || e->item_reduce == 1) {
         CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+        if (has_bias(c)) CF_TRY(dalloc(&e->slotVb, (size_t)c.n_items * e->capV));
     }
     if (!c.dense_item_apply) {
         if (e->hot_rep > 1) {
@@ -355,6 +364,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.rankV = e->rankV_[k];
     a.slotU = e->slotU;
     a.slotV = e->slotV;
+    a.slotVb = (has_bias(c) && e->slotV) ? e->slotVb : nullptr;
     a.capU = e->capU;
     a.capV = e->capV;
     a.GVrep = e->GVrep;
@@ -723,6 +733,18 @@ int read_loss(cf_engine* e, int slot, double* out) {
 // drop a batch the previous apply launch drew ahead: clear its occurrence
 // counts and put the sampler back where that draw started
 int discard_pending(cf_engine* e) {
+    if (e->x_pend) {   // a drawn-ahead exchange batch: uncount it, rewind the sampler
+        const cf_config& c = e->cfg;
+        const StepArgs& a = e->x_pend_args;
+        const int64_t nU = (int64_t)e->x_pend_B * users_per_pair(c), nV = (int64_t)e->x_pend_B * items_per_pair(c);
+        if (a.count_users) CF_HIP(launch_uncount(a.occU, nU, a.cntU, e->stream));
+        if (a.count_items) CF_HIP(launch_uncount(a.occV, nV, a.cntV, e->stream));
+        e->epoch = e->x_pend_epoch;
+        e->batch = e->x_pend_batch;
+        e->sampler_B = e->x_pend_sampler_B;
+        e->set = e->x_pend_set;
+        e->x_pend = false;
+    }
     if (!e->pend) return CF_OK;
     const cf_config& c = e->cfg;
     const StepArgs& a = e->pend_args;
@@ -974,7 +996,7 @@ int cf_destroy(cf_engine* e) {
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
     dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
-    dfree(e->slotU); dfree(e->slotV); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
+    dfree(e->slotU); dfree(e->slotV); dfree(e->slotVb); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc);
@@ -1229,6 +1251,11 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
 
 int cf_get_sampler_state(cf_engine* e, int64_t* epoch, int64_t* batch) {
     if (!e) return fail(CF_EINVAL, "null engine");
+    if (e->x_pend) {  // an exchange batch drawn ahead is not consumed yet
+        if (epoch) *epoch = e->x_pend_epoch;
+        if (batch) *batch = e->x_pend_batch;
+        return CF_OK;
+    }
     if (e->pend) {  // a batch drawn ahead is not consumed yet
         if (epoch) *epoch = e->pend_epoch;
         if (batch) *batch = e->pend_batch;
@@ -1599,21 +1626,20 @@ static int check_xchg(cf_engine* e, int stage) {
     return CF_OK;
 }
 
-int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
-                  const int32_t* groups, int32_t* send_counts_out) {
-    CF_TRY(check_xchg(e, 0));
-    if (B < 1 || !send_counts_out) return fail(CF_EINVAL, "bad arguments");
+// draw (or stage) one exchange batch into buffer set k and pack its remote
+// group members by owner into half k of send_ids; counts stay on the device
+static int xchg_stage(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                      const int32_t* groups, int k, int half, StepArgs* a) {
+    if (B < 1) return fail(CF_EINVAL, "bad arguments");
     if (e->GV == e->GV_own) return fail(CF_ESTATE, "bind the item-gradient buffer first (cf_bind_item_grad)");
     const cf_config& c = e->cfg;
     const int n = B * group_count(c);
     if (n > e->x_send_cap) return fail(CF_EINVAL, "exchange send capacity < B * gsize (cf_bind_exchange)");
     CF_TRY(ensure_batch(e, B));
-    const int k = e->set;
-    e->set ^= 1;
-    StepArgs a;
-    CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
+    CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, a));
     const size_t nblk = (size_t)(n + kBlock - 1) / kBlock;
     if (nblk * (size_t)e->world > e->xhist_cap) {
+        CF_HIP(hipStreamSynchronize(e->stream));
         dfree(e->xhist);
         CF_TRY(dalloc(&e->xhist, nblk * (size_t)e->world));
         e->xhist_cap = nblk * (size_t)e->world;
@@ -1625,8 +1651,20 @@ int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
     x.occ = e->occU_[k] + B;
     x.hist = e->xhist;
     x.counts = e->xcounts;
-    x.send_ids = e->x_send_ids;
+    x.send_ids = e->x_send_ids + (int64_t)half * e->x_send_cap;
     CF_HIP(launch_xchg_pack(x, e->stream));
+    return CF_OK;
+}
+
+int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                  const int32_t* groups, int32_t* send_counts_out) {
+    CF_TRY(check_xchg(e, 0));
+    if (!send_counts_out) return fail(CF_EINVAL, "bad arguments");
+    CF_TRY(discard_pending(e));
+    const int k = e->set;
+    e->set ^= 1;
+    StepArgs a;
+    CF_TRY(xchg_stage(e, B, pairs, negs, groups, k, 0, &a));   // send_ids half 0
     CF_HIP(hipMemcpyAsync(e->h_xcounts, e->xcounts, ((size_t)e->world + 1) * 4, hipMemcpyDeviceToHost,
                           e->stream));
     CF_HIP(hipStreamSynchronize(e->stream));
@@ -1634,6 +1672,45 @@ int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
     e->x_args = a;
     e->x_set = k;
     e->x_B = B;
+    e->x_stage = 1;
+    return CF_OK;
+}
+
+int cf_xchg_draw(cf_engine* e, int32_t B, void* send_counts_dev, int32_t* half_out) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (c.model != CF_GBPR || !c.dense_item_apply || e->h_bounds.empty() || !e->group_source_global)
+        return fail(CF_ESTATE, "the group exchange needs GBPR, dense_item_apply=1, cf_set_shard and cf_set_group_source");
+    if (e->det) return fail(CF_ESTATE, "deterministic mode does not cover the GBPR group exchange");
+    if (e->x_pend) return fail(CF_ESTATE, "an exchange batch is already drawn (cf_xchg_adopt takes it)");
+    if (!half_out) return fail(CF_EINVAL, "null half_out");
+    CF_TRY(check_device_ptr(send_counts_dev, "send_counts_dev"));
+    const int k = e->set;
+    const int64_t ep = e->epoch, bt = e->batch;
+    const int sb = e->sampler_B;
+    e->set ^= 1;
+    StepArgs a;
+    CF_TRY(xchg_stage(e, B, nullptr, nullptr, nullptr, k, k, &a));
+    CF_HIP(hipMemcpyAsync((int32_t*)send_counts_dev + (int64_t)k * e->world, e->xcounts,
+                          (size_t)e->world * 4, hipMemcpyDeviceToDevice, e->stream));
+    e->x_pend = true;
+    e->x_pend_args = a;
+    e->x_pend_set = k;
+    e->x_pend_B = B;
+    e->x_pend_epoch = ep;
+    e->x_pend_batch = bt;
+    e->x_pend_sampler_B = sb;
+    *half_out = k;
+    return CF_OK;
+}
+
+int cf_xchg_adopt(cf_engine* e) {
+    CF_TRY(check_xchg(e, 0));
+    if (!e->x_pend) return fail(CF_ESTATE, "no exchange batch drawn ahead (cf_xchg_draw)");
+    e->x_args = e->x_pend_args;
+    e->x_set = e->x_pend_set;
+    e->x_B = e->x_pend_B;
+    e->x_pend = false;
     e->x_stage = 1;
     return CF_OK;
 }

@@ -245,16 +245,19 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
 
 __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g,
                                             int64_t slot) {
-    // GBPR item bias: one scalar row
-    if (count == 1 && !a.items_grad_only) {
-        const float acc = fmaf(g, g, a.Ab[r]);
-        a.Ab[r] = acc;
-        a.b[r] -= adagrad_delta(a.lr, g, acc);
-    } else if (a.slotVb != nullptr) {   // deterministic: stored, summed in rank order
-        if (count == 1) a.Gb[r] = g;    // multi-rank item reduce: the sole writer
-        else a.slotVb[slot] = g;
+    // GBPR / CPLR item bias: one scalar per row, summed like the row itself
+    if (count == 1) {
+        if (!a.items_grad_only) {
+            const float acc = fmaf(g, g, a.Ab[r]);
+            a.Ab[r] = acc;
+            a.b[r] -= adagrad_delta(a.lr, g, acc);
+        } else {
+            a.Gb[r] = g;   // multi-rank item reduce: the sole writer of a zeroed entry
+        }
+    } else if (slot >= 0 && a.slotVb != nullptr) {
+        a.slotVb[slot] = g;   // beside the row's slot row; the apply sums them in rank order
     } else {
-        unsafeAtomicAdd(a.Gb + r, g);
+        unsafeAtomicAdd(a.Gb + r, g);   // a hot row past its slot range
     }
 }
 
@@ -1365,17 +1368,20 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
             row_zero<EPL>(Gk + r * a.d, a.d, gl);
         }
     }
-    // deterministic bias: the row's bias slots in rank order (lane 0)
+    // item bias (GBPR / CPLR): its slots in rank order (lane 0) + what hot-row
+    // atomics left in Gb
     float gbias = 0.f;
-    if (!isU && a.slotVb != nullptr && gl == 0 && a.Gb != nullptr) {
-        const int64_t s0 = (int64_t)off[r];
-        for (int t = 0; t < local; ++t) gbias += a.slotVb[s0 + t];
+    const bool bias_row = !isU && a.slotVb != nullptr && a.Gb != nullptr;
+    if (bias_row && gl == 0) {
+        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
+        for (int t = 0; t < ns; ++t) gbias += a.slotVb[s0 + t];
+        gbias += a.Gb[r];
     }
     if (reduce_only) {
         row_st<EPL>(G + r * (int64_t)a.d, a.d, gl, g);
         if (gl == 0) {
             cnt[r] = 0;
-            if (a.slotVb != nullptr && a.Gb != nullptr) a.Gb[r] = gbias;
+            if (bias_row) a.Gb[r] = gbias;
         }
         return;
     }
@@ -1383,11 +1389,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     if (gl == 0) {
         cnt[r] = 0;
         if (!isU && a.b != nullptr) {
-            const float gb = a.slotVb != nullptr ? gbias : a.Gb[r];
+            const float gb = bias_row ? gbias : a.Gb[r];
             const float ab = fmaf(gb, gb, a.Ab[r]);
             a.Ab[r] = ab;
             a.b[r] -= adagrad_delta(a.lr, gb, ab);
-            if (a.slotVb == nullptr) a.Gb[r] = 0.f;
+            a.Gb[r] = 0.f;
         }
     }
 }

@@ -316,9 +316,17 @@ class GroupExchangeStep(object):
     ``backend`` provides xchg_begin / xchg_serve / xchg_grad / xchg_finish /
     step_items (the C-ABI protocol in include/cf_engine.h), the exchange
     tensors send_ids, rows, grads, recv_ids, serve_rows, serve_grads,
-    ``ensure_recv(n)`` and ``device``."""
+    ``ensure_recv(n)`` and ``device``.
 
-    def __init__(self, backend, items, world, process_group=None):
+    Device-sampled steps (``batch_size``, no host batch) on a backend with
+    ``xchg_draw`` / ``xchg_adopt`` are pipelined so that no step waits on the
+    host: the batch of step s+1 is drawn and packed, its per-owner counts
+    all-to-all'ed and copied to pinned host memory at the START of step s
+    (before step s's exchange work in stream order); step s+1 then only waits
+    on that copy's event, long complete, for the split sizes of its
+    all-to-alls."""
+
+    def __init__(self, backend, items, world, process_group=None, pipelined=True):
         import torch
         import torch.distributed as dist
         self.backend = backend
@@ -328,18 +336,60 @@ class GroupExchangeStep(object):
         self.group = process_group
         self._dist = dist
         self._torch = torch
+        self.pipelined = pipelined and hasattr(backend, "xchg_draw")
+        self._next = None
+        if self.pipelined:
+            dev = backend.device
+            self._sc = torch.zeros((2, world), dtype=torch.int32, device=dev)
+            self._rc = torch.zeros((2, world), dtype=torch.int32, device=dev)
+            pin = dev.type == "cuda"
+            self._hsc = torch.zeros((2, world), dtype=torch.int32, pin_memory=pin)
+            self._hrc = torch.zeros((2, world), dtype=torch.int32, pin_memory=pin)
 
-    def __call__(self, batch_size=None, pairs=None, negs=None, groups=None):
+    def _draw(self, batch_size):
+        torch = self._torch
+        h = self.backend.xchg_draw(batch_size, self._sc.data_ptr())
+        _a2a(self._dist, self._rc[h], self._sc[h], None, None, self.group)
+        self._hsc[h].copy_(self._sc[h], non_blocking=True)
+        self._hrc[h].copy_(self._rc[h], non_blocking=True)
+        ev = torch.cuda.Event() if self._sc.is_cuda else None
+        if ev is not None:
+            ev.record()
+        self._next = (h, ev)
+
+    def _counts(self, batch_size, pairs, negs, groups):
+        """(send counts, recv counts, send_ids half) of this step."""
         be, dist, torch = self.backend, self._dist, self._torch
+        if self.pipelined and pairs is None:
+            if self._next is not None:
+                try:
+                    be.xchg_adopt()
+                except Exception:          # the drawn batch was dropped by another call
+                    self._next = None
+            if self._next is None:
+                self._draw(batch_size)
+                be.xchg_adopt()
+            h, ev = self._next
+            if ev is not None:
+                ev.synchronize()           # recorded a step ago: already complete
+            sc, rc = self._hsc[h].tolist(), self._hrc[h].tolist()
+            self._next = None
+            self._draw(batch_size)         # step s+1, ahead of this step's exchange
+            return sc, rc, h
+        self._next = None
         sc = be.xchg_begin(self.world, batch_size=batch_size, pairs=pairs, negs=negs, groups=groups)
         sct = torch.as_tensor(np.asarray(sc, dtype=np.int64)).to(be.device)
         rct = torch.empty_like(sct)
         _a2a(dist, rct, sct, None, None, self.group)
-        sc = [int(x) for x in sc]
-        rc = [int(x) for x in rct.tolist()]
+        return [int(x) for x in sc], [int(x) for x in rct.tolist()], 0
+
+    def __call__(self, batch_size=None, pairs=None, negs=None, groups=None):
+        be, dist = self.backend, self._dist
+        sc, rc, h = self._counts(batch_size, pairs, negs, groups)
         ns, nr = sum(sc), sum(rc)
         be.ensure_recv(nr)
-        _a2a(dist, be.recv_ids[:nr], be.send_ids[:ns], rc, sc, self.group)
+        cap = getattr(be, "send_cap", 0)
+        _a2a(dist, be.recv_ids[:nr], be.send_ids[h * cap:h * cap + ns], rc, sc, self.group)
         be.xchg_serve(nr)
         _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group)
         be.xchg_grad()
@@ -367,7 +417,8 @@ class EngineExchange(object):
         engine.set_shard(world, rank, bounds)
         engine.set_group_source(indptr_t, indices_t)
         cap = int(batch_size) * int(engine.gsize)
-        self.send_ids = torch.empty(cap, dtype=torch.int32, device=device)
+        # two halves: the batch drawn one step ahead packs into the other one
+        self.send_ids = torch.empty(2 * cap, dtype=torch.int32, device=device)
         self.rows = torch.empty((cap, d), dtype=torch.float32, device=device)
         self.grads = torch.empty((cap, d), dtype=torch.float32, device=device)
         self.send_cap = cap
@@ -389,6 +440,12 @@ class EngineExchange(object):
 
     def xchg_begin(self, world, **kw):
         return self.e.xchg_begin(world, **kw)
+
+    def xchg_draw(self, batch_size, counts_ptr):
+        return self.e.xchg_draw(batch_size, counts_ptr)
+
+    def xchg_adopt(self):
+        self.e.xchg_adopt()
 
     def xchg_serve(self, n):
         self.e.xchg_serve(n)

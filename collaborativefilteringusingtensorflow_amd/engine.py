@@ -327,6 +327,18 @@ class Engine(object):
                                           _arg(negs, ctypes.c_int32), gp, cp), "cf_xchg_begin")
         return counts
 
+    def xchg_draw(self, batch_size, send_counts_dev_ptr):
+        """Draw + pack the NEXT exchange batch (no host sync); its per-owner
+        counts go to the device int32 [2, world] buffer at row `half`, its
+        ids to half `half` of send_ids.  Returns half."""
+        h = ctypes.c_int32(0)
+        N.check(self._L.cf_xchg_draw(self._h, int(batch_size), ctypes.c_void_p(send_counts_dev_ptr),
+                                     ctypes.byref(h)), "cf_xchg_draw")
+        return int(h.value)
+
+    def xchg_adopt(self):
+        N.check(self._L.cf_xchg_adopt(self._h), "cf_xchg_adopt")
+
     def xchg_serve(self, n_recv):
         N.check(self._L.cf_xchg_serve(self._h, int(n_recv)), "cf_xchg_serve")
 

@@ -290,15 +290,27 @@ int cf_bind_table(cf_engine* eng, int32_t table, void* device_ptr, int64_t n_ele
  *   cf_xchg_begin    sample (or take the host batch; groups = GLOBAL user ids),
  *                    count, pack the remote members' ids by owner into
  *                    send_ids; send_counts_out[r] = ids for rank r (syncs)
+ *     or, with no host round trip (device sampler):
+ *   cf_xchg_draw     (one step AHEAD) draw + count + pack the next batch into
+ *                    buffer set h = *half_out: its ids go to send_ids half h,
+ *                    its per-owner counts to send_counts_dev[h*world ..]
+ *                    (device int32 [2, world]); the caller all-to-alls the
+ *                    counts and copies them to the host asynchronously
+ *   cf_xchg_adopt    take the drawn batch as this step's (stage begun)
  *   all-to-all       send_ids -> recv_ids (ids this rank serves)
  *   cf_xchg_serve    copy the served rows (pre-update) into serve_rows
  *   all-to-all       serve_rows -> rows (in send_ids order)
  *   cf_xchg_grad     slots + gradient; remote members' gradient rows -> grads
  *   all-to-all       grads -> serve_grads
  *   cf_xchg_finish   add the served rows' gradients, user Adagrad
- * then the item all-reduce + cf_step_items as for cf_step_local.  A served
- * row's count word is flagged, so all its contributions are summed before
- * the update (TF1 dedup semantics).  Requires GBPR, dense_item_apply=1. */
+ * then the item exchange (all-reduce + cf_step_items, or the item-range
+ * reduce-scatter path) as for cf_step_local.  A served row's count word is
+ * flagged, so all its contributions are summed before the update (TF1 dedup
+ * semantics).  Requires GBPR, dense_item_apply=1.  send_ids holds
+ * 2 * send_cap ids: cf_xchg_begin packs into half 0, cf_xchg_draw into the
+ * half it returns.
+ * A drawn-ahead batch is dropped (sampler rewound) by any other stepping or
+ * sampling call. */
 int cf_set_shard(cf_engine* eng, int32_t world, int32_t rank, const int64_t* user_bounds /*[world+1]*/);
 /* global item -> user CSR (sampler_gbpr.py:15), user ids global */
 int cf_set_group_source(cf_engine* eng, const int64_t* indptr_t, const int32_t* indices_t, int64_t nnz);
@@ -306,6 +318,8 @@ int cf_bind_exchange(cf_engine* eng, void* send_ids, void* rows, void* grads, in
                      void* recv_ids, void* serve_rows, void* serve_grads, int64_t recv_cap);
 int cf_xchg_begin(cf_engine* eng, int32_t B, const int32_t* host_pairs, const int32_t* host_negs,
                   const int32_t* host_groups, int32_t* send_counts_out);
+int cf_xchg_draw(cf_engine* eng, int32_t B, void* send_counts_dev, int32_t* half_out);
+int cf_xchg_adopt(cf_engine* eng);
 int cf_xchg_serve(cf_engine* eng, int64_t n_recv);
 int cf_xchg_grad(cf_engine* eng);
 int cf_xchg_finish(cf_engine* eng, int64_t n_recv);

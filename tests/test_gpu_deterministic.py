@@ -57,7 +57,11 @@ def test_two_runs_bitwise_identical(skewed_graph, model, d, W, dense):
     assert a[0] == b[0]                                   # the loss, bit for bit
     for t in TABLES[model]:
         assert np.array_equal(a[1][t], b[1][t]), t
-    # the fast path trains the same model (fp32 summation order aside)
+    # the fast path trains the same model (fp32 summation order aside); not
+    # for CML, whose hinge and closest-negative min are discontinuous, so a
+    # last-bit difference can flip a term (its oracle check is below)
+    if model == "cml":
+        return
     c = _run(model, skewed_graph, d, W, 16384, 6, det=False, dense=dense, phase=(model == "amf"))
     assert abs(c[0] - a[0]) <= 1e-5 * abs(a[0])
     for t in TABLES[model]:
@@ -77,6 +81,7 @@ def test_deterministic_steps_match_oracle(skewed_graph, model):
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=4)
     T = {t: e.get_table(t).astype(np.float64) for t in TABLES[model]}
+    T32 = {t: v.astype(np.float32) for t, v in T.items()}   # CML: the fp32 yardstick
     hot = 0
     for _ in range(4):
         pairs, negs, groups = e.sample(B)
@@ -89,9 +94,15 @@ def test_deterministic_steps_match_oracle(skewed_graph, model):
                              pairs, negs, groups, 0.4, 0.01)
         else:
             lo = O.cml_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 1.0, 1.0, 1.0)
+            O.cml_step(T32["user"], T32["item"], T32["acc_user"], T32["acc_item"], pairs, negs, 1.0, 1.0, 1.0)
         assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
     assert hot > 100    # rows far above the fast path's slot cap (32) were summed without atomics
     for t in TABLES[model]:
         got = e.get_table(t).astype(np.float64)
-        assert np.abs(got - T[t]).max() <= 1e-5 * np.abs(T[t]).max(), t
+        tol = 1e-5 * np.abs(T[t]).max()
+        if model == "cml":
+            # hot rows sum hundreds of gradients scaled by log(1 + n_items * ..) ~ 8:
+            # the same oracle in float32 lands this far from float64 too
+            tol = max(tol, 2.0 * np.abs(T32[t].astype(np.float64) - T[t]).max())
+        assert np.abs(got - T[t]).max() <= tol, t
     e.close()

@@ -29,7 +29,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce"):
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce",
+            pipelined=True):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -52,8 +53,12 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     e.set_table("bias", b0)
     step, _items = make_gpu_group_exchange(e, world, rank, bounds, ip, ix, 1682, d, 100,
                                            torch.device("cuda", 0), exchange=exchange)
+    step.pipelined = step.pipelined and pipelined
     drawn = []
-    if sampled:
+    if sampled == "steps":           # device-sampled steps only (pipelined count exchange)
+        for _ in range(7):
+            step(batch_size=64)
+    elif sampled:
         for _ in range(6):
             pairs, negs, groups = e.sample(64)
             pairs = pairs.copy()
@@ -75,11 +80,12 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     dist.destroy_process_group()
 
 
-def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce"):
+def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange,
+                                               pipelined))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -136,3 +142,24 @@ def test_two_rank_device_sampled_groups_span_shards(fold1):
                     cross += int(not (u0 <= gg < u1))
     assert cross > 0
     assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
+
+
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
+def test_pipelined_count_exchange_equals_synchronous(fold1, exchange):
+    """Device-sampled steps with the batch of step s+1 drawn, packed and its
+    per-owner counts exchanged at the start of step s (cf_xchg_draw /
+    cf_xchg_adopt: no host round trip inside the step) train exactly what the
+    synchronous cf_xchg_begin path trains on the same sampler stream."""
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(14)
+    d = 16
+    U0 = O.init_table(rng, (943, d))
+    V0 = O.init_table(rng, (1682, d))
+    b0 = O.init_table(rng, (1682,))
+    dummy = [(np.zeros((1, 2), np.int32), np.zeros((1, 5), np.int32), np.zeros((1, 1), np.int32))]
+    a = _run(fold1, dummy, U0, V0, b0, sampled="steps", exchange=exchange, pipelined=True)
+    b = _run(fold1, dummy, U0, V0, b0, sampled="steps", exchange=exchange, pipelined=False)
+    rel = lambda x, y: np.abs(x - y).max() / np.abs(y).max()
+    for ra, rb in zip(a, b):
+        for k in (3, 4, 5, 6):      # user, item, bias, acc_user
+            assert rel(ra[k], rb[k]) <= 1e-5, (ra[0], k, rel(ra[k], rb[k]))

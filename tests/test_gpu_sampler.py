@@ -158,3 +158,23 @@ def test_pos_set_draw_equals_row_scan(fold1, model, W, G):
             pairs, negs = ba[0], ba[1]
             for (u, i), js in zip(pairs, negs):
                 assert not any(int(j) in pos[u] for j in js)
+
+
+def test_user_with_every_item_only_blocks_the_device_sampler():
+    """A user whose row holds every item has no negative: the reference's
+    rejection loop would spin forever (sampler_ranking.py:30-36) and the
+    UITJ sampler skips such users (sampler_uitj_ranking.py:28).  The engine
+    accepts the interactions; host-fed steps run, the device draw refuses."""
+    from collaborativefilteringusingtensorflow_amd import _native as N
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    ni = 6
+    ip = np.array([0, 6, 8, 9], dtype=np.int64)
+    ix = np.array([0, 1, 2, 3, 4, 5, 1, 4, 2], dtype=np.int32)
+    e = Engine("bpr", 3, ni, 8, n_neg=1, reg=0.05, seed=2)
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, seed=1)
+    loss = e.step(np.array([[1, 1], [2, 2]], np.int32), np.array([[0], [5]], np.int32))
+    assert np.isfinite(loss)
+    with pytest.raises(N.NativeError, match="every item"):
+        e.train_steps(2, 1)
+    e.close()
