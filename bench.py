@@ -317,12 +317,17 @@ def main():
                     help="cf_set_option hot_replicas (0 = engine default)")
     ap.add_argument("--zipf", type=float, default=-1.0,
                     help="override the item popularity exponent (experiments; 0 = uniform)")
-    ap.add_argument("--item-exchange", default=os.environ.get("CF_ITEM_EXCHANGE", "allreduce"),
-                    choices=["allreduce", "rs_ag"],
+    ap.add_argument("--item-exchange", default=os.environ.get("CF_ITEM_EXCHANGE", "auto"),
+                    choices=["auto", "allreduce", "rs_ag"],
                     help="multi-GPU item step: RCCL all-reduce + replicated Adagrad, or "
-                         "reduce-scatter -> owner Adagrad -> all-gather")
+                         "reduce-scatter -> owner Adagrad -> all-gather; auto = rs_ag from 4 ranks "
+                         "(DESIGN 5)")
     ap.add_argument("--secondary-batch", type=int, default=65536,
                     help="also time this batch size (SURVEY 8(d)'s B); 0 = off")
+    ap.add_argument("--bias-slots", type=int, default=-1,
+                    help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
+    ap.add_argument("--deterministic", type=int, default=0,
+                    help="cf_set_option deterministic (sort-based ranks, no float atomics)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the process group, check it, print a line; no GPU work (tests)")
     args = ap.parse_args()
@@ -353,6 +358,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     check_world(world, args.gpus)
+    if args.item_exchange == "auto":
+        args.item_exchange = "rs_ag" if world >= 4 else "allreduce"
     dist = None
     torch = None
     # CF_DIST_BACKEND=gloo + CF_SHARE_DEVICE=1 rehearse the N>1 path with all
@@ -421,6 +428,10 @@ def main():
         eng.set_option("neg_check", args.neg_check)
     if args.item_reduce >= 0:
         eng.set_option("item_reduce", args.item_reduce)
+    if args.bias_slots >= 0:
+        eng.set_option("bias_slots", args.bias_slots)
+    if args.deterministic:
+        eng.set_option("deterministic", 1)
     if args.slot_max:
         eng.set_option("slot_max", args.slot_max)
     eng.set_interactions(indptr, indices)

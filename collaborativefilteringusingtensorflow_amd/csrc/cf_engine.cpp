@@ -195,6 +195,7 @@ struct cf_engine {
     int topk_path = 0;  // cf_set_option("topk_path")
     int grad_path = 0;  // cf_set_option("grad_path")
     int item_reduce = 1;  // cf_set_option("item_reduce"): dense mode counts item rows
+    int bias_slots = 0;   // cf_set_option("bias_slots"): duplicated item-bias gradients in slots (1) or atomics (0)
     int prep_side = 0;  // cf_set_option("prep_stream"): 1 = side stream (overlap), 0 = main
 
     // profiling
@@ -364,7 +365,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.rankV = e->rankV_[k];
     a.slotU = e->slotU;
     a.slotV = e->slotV;
-    a.slotVb = (has_bias(c) && e->slotV) ? e->slotVb : nullptr;
+    a.slotVb = (has_bias(c) && e->slotV && e->bias_slots) ? e->slotVb : nullptr;
     a.capU = e->capU;
     a.capV = e->capV;
     a.GVrep = e->GVrep;
@@ -1888,7 +1889,12 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "neg_check") {
+#ifdef CF_LANE_DRAW
         if (value < 0 || value > 2) return fail(CF_EINVAL, "neg_check must be 0, 1 or 2");
+#else
+        if (value < 0 || value > 1)
+            return fail(CF_EINVAL, "neg_check must be 0 or 1 (2, the one-lane-per-pair draw, needs a -DCF_LANE_DRAW build)");
+#endif
         CF_TRY(discard_pending(e));
         e->neg_check = (int)value;
         if (value >= 1 && e->pairs && !e->pos_set) CF_TRY(build_pos_set(e));
@@ -1901,6 +1907,13 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_HIP(hipStreamSynchronize(e->stream));
         e->item_reduce = (int)value;
         e->slots_ready = false;
+        return CF_OK;
+    }
+    if (n == "bias_slots") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "bias_slots must be 0 or 1");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        e->bias_slots = (int)value;
         return CF_OK;
     }
     if (n == "deterministic") {

@@ -475,8 +475,13 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
 // wave instruction serialise in the address path, and 8-lane groups keep
 // more waves -- more independent chains -- in flight.  Kept as an option.
 // ---------------------------------------------------------------------------
+// Built only with -DCF_LANE_DRAW (its registers would otherwise count against
+// every launch that carries a draw branch)
+#ifndef CF_LANE_DRAW
+#define CF_LANE_DRAW 0
+#endif
 __host__ __device__ __forceinline__ bool lane_prep(const StepArgs& a) {
-    return a.lane_draw != 0 && (!a.sample || a.pos_set != nullptr);
+    return CF_LANE_DRAW && a.lane_draw != 0 && (!a.sample || a.pos_set != nullptr);
 }
 
 template <int MODEL, int WT>
@@ -579,13 +584,15 @@ __device__ __forceinline__ void prep_lane_body(const StepArgs& a, int block) {
 // row scan is needed (lane_prep), else the 8-lane cooperative row scan
 template <int MODEL>
 __device__ __forceinline__ void prep_any(const StepArgs& a, int block) {
+#if CF_LANE_DRAW
     if (lane_prep(a)) {
         if (a.W == 1) prep_lane_body<MODEL, 1>(a, block);
         else if (a.W == 5) prep_lane_body<MODEL, 5>(a, block);
         else prep_lane_body<MODEL, 0>(a, block);
-    } else {
-        prep_body<MODEL>(a, block);
+        return;
     }
+#endif
+    prep_body<MODEL>(a, block);
 }
 
 __host__ __device__ __forceinline__ int prep_pairs_per_block(const StepArgs& a) {
@@ -943,10 +950,12 @@ __device__ __forceinline__ bool minor_block(int b, int nmajor, int nminor, int& 
     return hi > lo;
 }
 
-template <int MODEL, int EPL, int WT>
+// DRAW: the launch also carries the draw blocks of the next step (pipeline
+// 2); without it the draw's registers do not count against the gradient
+template <int MODEL, int EPL, int WT, bool DRAW>
 __global__ __launch_bounds__(kBlock) void grad_kernel(StepArgs a, StepArgs nx, int ng, int np) {
-    int idx;
-    if (minor_block(blockIdx.x, ng, np, idx))
+    int idx = blockIdx.x;
+    if (DRAW && minor_block(blockIdx.x, ng, np, idx))
         prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
         grad_body<MODEL, EPL, WT>(a, idx);
@@ -1277,15 +1286,15 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     }
 }
 
-template <int MODEL, int EPL, int WT, int P>
+template <int MODEL, int EPL, int WT, int P, bool DRAW>
 #ifdef CF_GRAD_WAVES_PER_EU
 #define CF_GRAD_ATTR __attribute__((amdgpu_waves_per_eu(CF_GRAD_WAVES_PER_EU, 8)))
 #else
 #define CF_GRAD_ATTR
 #endif
 __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
-    int idx;
-    if (minor_block(blockIdx.x, ng, np, idx))
+    int idx = blockIdx.x;
+    if (DRAW && minor_block(blockIdx.x, ng, np, idx))
         prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
         grad_fast_body<MODEL, EPL, WT, P>(a, idx);
@@ -1372,10 +1381,11 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     // atomics left in Gb
     float gbias = 0.f;
     const bool bias_row = !isU && a.slotVb != nullptr && a.Gb != nullptr;
-    if (bias_row && gl == 0) {
+    if (bias_row) {   // the group's 16 lanes load the slots, a fixed-order butterfly sums them
         const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
-        for (int t = 0; t < ns; ++t) gbias += a.slotVb[s0 + t];
-        gbias += a.Gb[r];
+        float t = 0.f;
+        for (int q = gl; q < ns; q += kGL) t += a.slotVb[s0 + q];
+        gbias = gsum(t) + a.Gb[r];
     }
     if (reduce_only) {
         row_st<EPL>(G + r * (int64_t)a.d, a.d, gl, g);
@@ -1803,6 +1813,12 @@ static int epl_for(int d) {
 #ifndef CF_FAST_PAIRS_W5
 #define CF_FAST_PAIRS_W5 1
 #endif
+// GBPR at d <= 64 (EPL <= 4): two pairs per 16-lane group keep more rows of
+// the 10M-user / 1M-item tables in flight (cfg4 grad 164.9 -> 157.6 us); at
+// d = 128 the second pair's registers cost occupancy (cfg5 AMF 148 -> 253 us)
+#ifndef CF_FAST_PAIRS_GBPR_W5
+#define CF_FAST_PAIRS_GBPR_W5 2
+#endif
 
 // which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
 // fast, 0 = generic
@@ -1825,8 +1841,9 @@ int grad_blocks(const StepArgs& a, bool with_draw) {
     const int fw = fast_w(a);
     const int B = a.B;
     const int gpb = (CF_GRAD_WAVE_BLOCKS && !with_draw) ? kWave / kGL : kGroupsPerBlock;
+    const int p5 = (a.model == GBPR && epl_for(a.d) <= 4) ? CF_FAST_PAIRS_GBPR_W5 : CF_FAST_PAIRS_W5;
     const int ppb = fw == 1 ? CF_FAST_PAIRS_W1 * gpb
-                  : fw == 5 ? CF_FAST_PAIRS_W5 * gpb : kPairsPerBlock;
+                  : fw == 5 ? p5 * gpb : kPairsPerBlock;
     return (B + ppb - 1) / ppb;
 }
 
@@ -1849,19 +1866,25 @@ static int prep_blocks(const StepArgs* nx) {
     return (nx->B + ppb - 1) / ppb;
 }
 
+template <int MODEL, int WT, bool DRAW>
+static hipError_t launch_grad_w_d(const StepArgs& a, const StepArgs& n, int ng, int np, hipStream_t s) {
+    const dim3 grid(ng + np), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4, WT, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8, WT, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16, WT, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+    }
+    return hipGetLastError();
+}
+
 template <int MODEL, int WT>
 static hipError_t launch_grad_w(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     const int ng = (a.B + kPairsPerBlock - 1) / kPairsPerBlock, np = prep_blocks(nx);
     const StepArgs n = nx ? *nx : a;
-    const dim3 grid(ng + np), block(kBlock);
-    switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((grad_kernel<MODEL, 1, WT>), grid, block, 0, s, a, n, ng, np); break;
-        case 2: hipLaunchKernelGGL((grad_kernel<MODEL, 2, WT>), grid, block, 0, s, a, n, ng, np); break;
-        case 4: hipLaunchKernelGGL((grad_kernel<MODEL, 4, WT>), grid, block, 0, s, a, n, ng, np); break;
-        case 8: hipLaunchKernelGGL((grad_kernel<MODEL, 8, WT>), grid, block, 0, s, a, n, ng, np); break;
-        default: hipLaunchKernelGGL((grad_kernel<MODEL, 16, WT>), grid, block, 0, s, a, n, ng, np); break;
-    }
-    return hipGetLastError();
+    return np > 0 ? launch_grad_w_d<MODEL, WT, true>(a, n, ng, np, s)
+                  : launch_grad_w_d<MODEL, WT, false>(a, n, ng, 0, s);
 }
 
 template <int MODEL, int WT, int P>
@@ -1882,11 +1905,20 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
     const int ng = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock), np = prep_blocks(nx);
     const StepArgs n = nx ? *nx : a;
     const dim3 grid(ng + np), block(kBlock);
-    switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P>), grid, block, 0, s, a, n, ng, np); break;
-        case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P>), grid, block, 0, s, a, n, ng, np); break;
-        case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P>), grid, block, 0, s, a, n, ng, np); break;
-        default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P>), grid, block, 0, s, a, n, ng, np); break;
+    if (np > 0) {
+        switch (epl_for(a.d)) {
+            case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
+            case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
+            case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
+            default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
+        }
+    } else {
+        switch (epl_for(a.d)) {
+            case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
+            case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
+            case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
+            default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
+        }
     }
     return hipGetLastError();
 }
@@ -1905,6 +1937,7 @@ static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream
     const int e = epl_for(a.d);
     const int fw = fast_w(a);
     if (fw == 1) return launch_grad_fast<MODEL, 1, CF_FAST_PAIRS_W1>(a, nx, s);
+    if (fw == 5 && MODEL == GBPR && e <= 4) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_GBPR_W5>(a, nx, s);
     if (fw == 5) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_W5>(a, nx, s);
     if (a.W == 1) return launch_grad_w<MODEL, 1>(a, nx, s);
     if (a.W == 5 && e <= 8) return launch_grad_w<MODEL, 5>(a, nx, s);

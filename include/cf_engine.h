@@ -388,6 +388,11 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                set probed by one lane per pair (measured slower, DESIGN).
  *                The same batches every way: each negative takes its first
  *                attempt outside Pos(u) in the same draw sequence.
+ *   "bias_slots" GBPR / CPLR item bias of a duplicated row: 1 = stored in a
+ *                bias slot beside the row's gradient slot and summed by the
+ *                apply, 0 = one float atomic per occurrence (default: at
+ *                cfg4 the atomics cost the gradient launch nothing measurable,
+ *                165.1 vs 164.9 us, and the slot sums cost the apply 4 us).
  *   "deterministic" 1 = bitwise-reproducible steps: occurrence ranks from a
  *                stable sort of the batch's row ids, every occurrence of a
  *                duplicated row stored in its own compact slot and summed in

@@ -119,13 +119,18 @@ def test_amf_across_phase_switch(fold1, streams):
         assert rel(g, o) <= RTOL, (t, rel(g, o))
 
 
+@pytest.mark.parametrize("bias_slots", [0, 1], ids=["bias-atomics", "bias-slots"])
 @pytest.mark.parametrize("name,d,rho,reg", [("gbpr_b100_g1_w5", 16, 0.4, 0.01),
                                             ("gbpr_b100_g3_w2", 24, 0.5, 0.02)])
-def test_gbpr_steps_match_oracle(fold1, streams, name, d, rho, reg):
+def test_gbpr_steps_match_oracle(fold1, streams, name, d, rho, reg, bias_slots):
+    _OPTS["bias_slots"] = bias_slots
     st = get_stream(streams, name)
     W, G = st["negs"].shape[2], st["groups"].shape[2]
     U, V, b = init_tables(fold1, d, 5, bias=True)
-    e = make_engine("gbpr", fold1, d, W, G=G, rho=rho, reg=reg)
+    try:
+        e = make_engine("gbpr", fold1, d, W, G=G, rho=rho, reg=reg)
+    finally:
+        _OPTS.clear()
     e.set_table("user", U)
     e.set_table("item", V)
     e.set_table("bias", b)
