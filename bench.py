@@ -320,8 +320,8 @@ def main():
     ap.add_argument("--item-exchange", default=os.environ.get("CF_ITEM_EXCHANGE", "auto"),
                     choices=["auto", "allreduce", "rs_ag"],
                     help="multi-GPU item step: RCCL all-reduce + replicated Adagrad, or "
-                         "reduce-scatter -> owner Adagrad -> all-gather; auto = rs_ag from 4 ranks "
-                         "(DESIGN 5)")
+                         "reduce-scatter -> owner Adagrad -> all-gather; auto = rs_ag when "
+                         "n_items * d >= 2^24 (DESIGN 5.1)")
     ap.add_argument("--secondary-batch", type=int, default=65536,
                     help="also time this batch size (SURVEY 8(d)'s B); 0 = off")
     ap.add_argument("--bias-slots", type=int, default=-1,
@@ -359,7 +359,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     check_world(world, args.gpus)
     if args.item_exchange == "auto":
-        args.item_exchange = "rs_ag" if world >= 4 else "allreduce"
+        # the all-reduce hides under the fused user apply + draw at
+        # cfg2/3/5; item-range ownership pays off where the dense item Adagrad
+        # itself is large (cfg4: 1M x 64 floats)
+        args.item_exchange = "rs_ag" if cfg["n_items"] * cfg["d"] >= (1 << 24) else "allreduce"
     dist = None
     torch = None
     # CF_DIST_BACKEND=gloo + CF_SHARE_DEVICE=1 rehearse the N>1 path with all
