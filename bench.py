@@ -324,6 +324,8 @@ def main():
                          "n_items * d >= 2^24 (DESIGN 5.1)")
     ap.add_argument("--secondary-batch", type=int, default=65536,
                     help="also time this batch size (SURVEY 8(d)'s B); 0 = off")
+    ap.add_argument("--item-slots", type=int, default=-1,
+                    help="cf_set_option item_slots (duplicated item rows: 1 records, 0 gradient rows; -1 default)")
     ap.add_argument("--bias-slots", type=int, default=-1,
                     help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
     ap.add_argument("--deterministic", type=int, default=0,
@@ -433,6 +435,8 @@ def main():
         eng.set_option("item_reduce", args.item_reduce)
     if args.bias_slots >= 0:
         eng.set_option("bias_slots", args.bias_slots)
+    if args.item_slots >= 0:
+        eng.set_option("item_slots", args.item_slots)
     if args.deterministic:
         eng.set_option("deterministic", 1)
     if args.slot_max:

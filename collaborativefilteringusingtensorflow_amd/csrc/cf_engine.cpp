@@ -89,6 +89,14 @@ struct cf_engine {
     float* slotV = nullptr;   // [n_items * capV, d]
     float* slotVb = nullptr;  // [n_items * capV] item-bias gradient beside each slot row (GBPR / PLR)
     int capU = 2, capV = 32;
+    // item records instead of item slot rows (cf_set_option "item_slots" 1):
+    // 16 B per duplicated item occurrence + each pair's pre-update user row
+    // (GBPR: its group blend row) stashed once (StepArgs::recV)
+    int item_recs = 0;
+    int4* recV = nullptr;     // [n_items * capV]
+    int4* recVc = nullptr;    // deterministic mode: [B*(1+W)]
+    float *stashU = nullptr, *stashB = nullptr;   // [stash_cap, d]
+    int stash_cap = 0;
     // hot item rows (occurrences past capV) spread their float atomics over
     // GV and hot_rep - 1 extra copies (cf_set_option "hot_replicas")
     float* GVrep = nullptr;   // [hot_rep - 1][n_items, d]
@@ -256,10 +264,14 @@ int ensure_slots(cf_engine* e) {
     dfree(e->slotU);
     dfree(e->slotV);
     dfree(e->slotVb);
+    dfree(e->recV);
     dfree(e->GVrep);
     CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
     if (!c.dense_item_apply || e->item_reduce == 1) {
-        CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
+        if (e->item_recs)
+            CF_TRY(dalloc(&e->recV, (size_t)c.n_items * e->capV));
+        else
+            CF_TRY(dalloc(&e->slotV, (size_t)c.n_items * e->capV * c.n_factors));
         if (has_bias(c)) CF_TRY(dalloc(&e->slotVb, (size_t)c.n_items * e->capV));
     }
     if (!c.dense_item_apply) {
@@ -282,6 +294,7 @@ int ensure_det(cf_engine* e, int B) {
     CF_HIP(hipStreamSynchronize(e->side));
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc);
+    dfree(e->recVc);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     e->det_tmp = nullptr;
     e->det_cap = 0;
@@ -290,7 +303,10 @@ int ensure_det(cf_engine* e, int B) {
     CF_TRY(dalloc(&e->det_vals, (size_t)(2 * n)));
     CF_TRY(dalloc(&e->det_off, (size_t)rows));
     CF_TRY(dalloc(&e->slotUc, (size_t)nU * c.n_factors));
-    CF_TRY(dalloc(&e->slotVc, (size_t)nV * c.n_factors));
+    if (e->item_recs)
+        CF_TRY(dalloc(&e->recVc, (size_t)nV));
+    else
+        CF_TRY(dalloc(&e->slotVc, (size_t)nV * c.n_factors));
     if (has_bias(c)) CF_TRY(dalloc(&e->slotVbc, (size_t)nV));
     e->det_tmp_bytes = det_ranks_scratch(n, rows);
     if (e->det_tmp_bytes) {
@@ -301,9 +317,23 @@ int ensure_det(cf_engine* e, int B) {
     return CF_OK;
 }
 
+int ensure_stash(cf_engine* e, int B) {
+    if (!e->item_recs || B <= e->stash_cap) return CF_OK;
+    const cf_config& c = e->cfg;
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipStreamSynchronize(e->side));
+    dfree(e->stashU);
+    dfree(e->stashB);
+    CF_TRY(dalloc(&e->stashU, (size_t)B * c.n_factors));
+    if (c.model == CF_GBPR) CF_TRY(dalloc(&e->stashB, (size_t)B * c.n_factors));
+    e->stash_cap = B;
+    return CF_OK;
+}
+
 int ensure_batch(cf_engine* e, int B) {
     CF_TRY(ensure_slots(e));
     if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap)));
+    CF_TRY(ensure_stash(e, std::max(B, e->Bcap)));
     if (B <= e->Bcap) return CF_OK;
     CF_HIP(hipStreamSynchronize(e->stream));
     CF_HIP(hipStreamSynchronize(e->side));
@@ -365,7 +395,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.rankV = e->rankV_[k];
     a.slotU = e->slotU;
     a.slotV = e->slotV;
-    a.slotVb = (has_bias(c) && e->slotV && e->bias_slots) ? e->slotVb : nullptr;
+    a.slotVb = (has_bias(c) && (e->slotV || e->recV) && e->bias_slots) ? e->slotVb : nullptr;
     a.capU = e->capU;
     a.capV = e->capV;
     a.GVrep = e->GVrep;
@@ -388,6 +418,11 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
             a.count_items = 1;
             a.items_grad_only = 1;
         }
+    }
+    if (e->item_recs && a.count_items && a.capV > 0) {
+        a.recV = e->det ? e->recVc : e->recV;
+        a.stashU = e->stashU;
+        a.stashB = e->stashB;
     }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
@@ -570,6 +605,9 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.offU = a.offU;
     p.offV = a.offV;
     p.slotVb = a.slotVb;
+    p.recV = a.recV;
+    p.stashU = a.stashU;
+    p.stashB = a.stashB;
     p.n_items = c.n_items;
     p.count_users = a.count_users;
     p.count_items = a.count_items;
@@ -912,6 +950,11 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     cf_engine* e = new (std::nothrow) cf_engine();
     if (!e) return fail(CF_ENOMEM, "host allocation failed");
     e->cfg = c;
+    // item records by default for rows of >= 512 B: A/B on MI355X (ms/step,
+    // rows -> records) cfg3 0.256 -> 0.230, cfg5 0.258 -> 0.227 (d 128, W 5);
+    // cfg2 0.497 -> 0.519, cfg4 0.241 -> 0.254 (d 64: the apply's record ->
+    // stash gather chain costs more than the smaller slot stores save)
+    e->item_recs = c.n_factors >= 128 ? 1 : 0;
     int r = CF_OK;
     auto bail = [&](int code) {
         cf_destroy(e);
@@ -1000,7 +1043,7 @@ int cf_destroy(cf_engine* e) {
     dfree(e->slotU); dfree(e->slotV); dfree(e->slotVb); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
-    dfree(e->slotVbc);
+    dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -1914,6 +1957,23 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
         e->bias_slots = (int)value;
+        return CF_OK;
+    }
+    if (n == "item_slots") {   // 0: gradient rows, 1: (pair, alpha, beta) records + user-row stash
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "item_slots must be 0 or 1");
+        if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        CF_HIP(hipStreamSynchronize(e->side));
+        if (e->item_recs == (int)value) return CF_OK;
+        e->item_recs = (int)value;
+        e->slots_ready = false;      // slot rows <-> records
+        e->det_cap = 0;              // deterministic buffers likewise
+        if (e->Bcap > 0) {
+            CF_TRY(ensure_slots(e));
+            if (e->det) CF_TRY(ensure_det(e, e->Bcap));
+            CF_TRY(ensure_stash(e, e->Bcap));
+        }
         return CF_OK;
     }
     if (n == "deterministic") {

@@ -94,6 +94,14 @@ struct StepArgs {
     const int32_t* __restrict__ offU;   // [n_users] first sorted position of each touched row
     const int32_t* __restrict__ offV;   // [n_items]
     float* __restrict__ slotVb;         // [B*(1+W)] bias gradient per item occurrence
+    // item records (cf_set_option "item_slots" 1): a duplicated item
+    // occurrence in its slot range stores (pair, alpha, beta, which) -- its
+    // gradient is alpha * X + beta * V_row, X = stashU[pair] (which 0) or
+    // stashB[pair] (GBPR's group blend, which 1) -- instead of a slot row;
+    // null = slot rows
+    int4* __restrict__ recV;            // [n_items * capV] (deterministic mode: [B*(1+W)])
+    float* __restrict__ stashU;         // [B, d] each pair's pre-update user row
+    float* __restrict__ stashB;         // [B, d] GBPR blend rows
     double* __restrict__ loss_partial;  // [grad grid]
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
@@ -150,6 +158,9 @@ struct ApplyArgs {
     const int32_t* __restrict__ offU;    // deterministic mode (StepArgs)
     const int32_t* __restrict__ offV;
     const float* __restrict__ slotVb;
+    const int4* __restrict__ recV;       // item records (StepArgs)
+    const float* __restrict__ stashU;
+    const float* __restrict__ stashB;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;

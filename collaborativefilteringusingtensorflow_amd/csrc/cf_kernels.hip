@@ -243,6 +243,24 @@ __device__ __forceinline__ void gfinish(float* __restrict__ X, float* __restrict
     }
 }
 
+// A duplicated item row's gradient from one pair is alpha * X + beta * V_row,
+// X the pair's pre-update user row (stashU) or, for GBPR's positive, its
+// group blend rho/G sum U_g + (1-rho) U_u (stashB): with item records
+// (cf_set_option "item_slots" 1) the slot gets the 16-B record
+// (pair, alpha, beta, which) instead of the 4d-B gradient row, and the apply
+// sums alpha * X from the stash + (sum of beta) * V_row.  Rows seen once and
+// hot rows past their slot range take gfinish with g in registers.
+template <int EPL>
+__device__ __forceinline__ void ifinish(const StepArgs& a, int64_t r, int count, int64_t slot, int p,
+                                        float alpha, float beta, int which, int gl,
+                                        const float (&x0)[EPL], const float (&g)[EPL]) {
+    if (a.recV != nullptr && count >= 2 && slot >= 0) {
+        if (gl == 0) a.recV[slot] = make_int4(p, __float_as_int(alpha), __float_as_int(beta), which);
+        return;
+    }
+    gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, r, count, slot, a.d, gl, x0, g, a);
+}
+
 __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int count, float g,
                                             int64_t slot) {
     // GBPR / CPLR item bias: one scalar per row, summed like the row itself
@@ -676,6 +694,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
         float uu[EPL], vi[EPL];
         gload<EPL>(a.U, u, d, gl, uu);
         gload<EPL>(a.V, i, d, gl, vi);
+        if (a.recV != nullptr) gstore<EPL>(a.stashU, p, d, gl, uu);   // item records' X
 
         if (MODEL == BPR || MODEL == AMF) {
             // x = <u,i> - <u,j>;  c = dL/dx = sigmoid(x) - 1   (A.1, A.4)
@@ -708,7 +727,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gj[s] = -c * uu[s] + a.reg * J.v[sl][s];
                     sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
                 }
-                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                ifinish<EPL>(a, J.j[sl], J.c[sl], J.sl[sl], p, -c, a.reg, 0, gl, J.v[sl], gj);
             }
             float gi[EPL];
 #pragma unroll
@@ -719,7 +738,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 sq = fmaf(vi[s], vi[s], sq);
             }
             gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            ifinish<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, vi, gi);
         } else if (MODEL == GBPR) {
             // ui = rho*mean_k<g_k,i> + (1-rho)<u,i> + b_i ; uj = <u,j> + b_j   (A.2)
             const float bi = a.b[i];
@@ -759,17 +778,19 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     gj[s] = -c * uu[s];  // no L2 on V[j] (gbprmf.py:59-64)
                 }
                 if (gl == 0) bias_finish(a, j, J.c[sl], -c + a.reg * bj, J.sl[sl]);
-                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j, J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                ifinish<EPL>(a, j, J.c[sl], J.sl[sl], p, -c, 0.f, 0, gl, J.v[sl], gj);
             }
             const float rg = a.rho / Gf;
-            float gi[EPL];
+            float gi[EPL], bl[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) {
                 gu[s] += (1.f - a.rho) * sc * vi[s] + a.reg * uu[s];
-                gi[s] = sc * (rg * sg[s] + (1.f - a.rho) * uu[s]) + a.reg * vi[s];
+                bl[s] = rg * sg[s] + (1.f - a.rho) * uu[s];
+                gi[s] = sc * bl[s] + a.reg * vi[s];
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
             }
+            if (a.recV != nullptr) gstore<EPL>(a.stashB, p, d, gl, bl);
             gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
             for (int k2 = 0; k2 < G; ++k2) {
                 const int g = a.occU[B + p * G + k2];
@@ -786,7 +807,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g, cg, sg_, d, gl, gk, gg, a);
             }
             if (gl == 0) bias_finish(a, i, ci, sc, si);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            ifinish<EPL>(a, i, ci, si, p, sc, a.reg, 1, gl, vi, gi);
         } else if (MODEL == PLR) {
             // tuple ranking: s_x = <u, v_x> + b_x over the tuple's items
             // (x0 = i, x1.. = J); weighted -log sigmoid(coef (s_a - s_b)) terms
@@ -837,7 +858,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     sq = fmaf(J.v[w][s], J.v[w][s], sq);
                 }
                 if (a.train_bias && gl == 0) bias_finish(a, J.j[w], J.c[w], ds[w + 1] + a.reg * bx[w + 1], J.sl[w]);
-                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[w], J.c[w], J.sl[w], d, gl, J.v[w], gj, a);
+                ifinish<EPL>(a, J.j[w], J.c[w], J.sl[w], p, ds[w + 1], a.reg, 0, gl, J.v[w], gj);
             }
             float gi[EPL];
 #pragma unroll
@@ -848,7 +869,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
             }
             gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
             if (a.train_bias && gl == 0) bias_finish(a, i, ci, ds[0] + a.reg * bx[0], si);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            ifinish<EPL>(a, i, ci, si, p, ds[0], a.reg, 0, gl, vi, gi);
         } else {  // CML (A.3); W <= 16 so lane w keeps dn_w
             float du[EPL];
 #pragma unroll
@@ -900,7 +921,8 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                     }
                 }
                 // a touched row with a zero gradient is still clipped (cml.py:128-129)
-                gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, J.j[sl], J.c[sl], J.sl[sl], d, gl, J.v[sl], gj, a);
+                ifinish<EPL>(a, J.j[sl], J.c[sl], J.sl[sl], p, coef, (l2 ? a.reg_cov : 0.f) - coef, 0, gl,
+                             J.v[sl], gj);
             }
             if (l2) {
 #pragma unroll
@@ -912,7 +934,7 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
                 }
             }
             gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
-            gfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, gi, a);
+            ifinish<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), 0, gl, vi, gi);
         }
     }
 
@@ -1034,11 +1056,24 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
     }
 }
 
+// gfinish_pre with ifinish's item records (see there)
+template <int EPL>
+__device__ __forceinline__ void ifinish_pre(const StepArgs& a, int64_t r, int count, int64_t slot, int p,
+                                            float alpha, float beta, int which, int gl,
+                                            const float (&x0)[EPL], const float (&acc0)[EPL],
+                                            const float (&g)[EPL]) {
+    if (a.recV != nullptr && count >= 2 && slot >= 0) {
+        if (gl == 0) a.recV[slot] = make_int4(p, __float_as_int(alpha), __float_as_int(beta), which);
+        return;
+    }
+    gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, r, count, slot, a.d, gl, x0, acc0, g, a);
+}
+
 template <int MODEL, int EPL, int WT>
 struct PairRows {
     static constexpr int NG = (MODEL == GBPR) ? 1 : 0;
     static constexpr int NGA = NG > 0 ? NG : 1;
-    int u, i, cu, ci, ru, ri;
+    int p, u, i, cu, ci, ru, ri;
     int j[WT], cj[WT], rj[WT];
     int g[NGA], cg[NGA], rg[NGA];
     int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
@@ -1047,7 +1082,8 @@ struct PairRows {
     float ug[NGA][EPL], ag[NGA][EPL];
     float bi, bj[WT];
 
-    __device__ __forceinline__ void load_idx(const StepArgs& a, int p) {
+    __device__ __forceinline__ void load_idx(const StepArgs& a, int pair) {
+        p = pair;
         u = a.occU[p];
         i = a.occV[p];
         ru = a.count_users ? a.rankU[p] : 0;
@@ -1101,6 +1137,12 @@ struct PairRows {
 
     __device__ __forceinline__ void update(const StepArgs& a, int gl, float& loss_g, float& sq) {
         const int d = a.d;
+        if (a.recV != nullptr) {   // item records' X: only pairs that leave one
+            bool need = MODEL != GBPR && ci >= 2 && si >= 0;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) need |= cj[w] >= 2 && sj[w] >= 0;
+            if (need) gstore<EPL>(a.stashU, p, d, gl, uu);
+        }
         if (MODEL == BPR || MODEL == AMF) {
             const float ui = gdot<EPL>(uu, vi);
             float gu[EPL];
@@ -1129,7 +1171,7 @@ struct PairRows {
                     gj[s] = -c * uu[s] + a.reg * vj[w][s];
                     sq = fmaf(vj[w][s], vj[w][s], sq);
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                ifinish_pre<EPL>(a, j[w], cj[w], sj[w], p, -c, a.reg, 0, gl, vj[w], aj[w], gj);
             }
             float gi[EPL];
 #pragma unroll
@@ -1140,7 +1182,7 @@ struct PairRows {
                 sq = fmaf(vi[s], vi[s], sq);
             }
             gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            ifinish_pre<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, vi, ai, gi);
         } else if (MODEL == GBPR) {  // G == 1
             const float ui_u = gdot<EPL>(uu, vi);
 #pragma unroll
@@ -1163,14 +1205,15 @@ struct PairRows {
                     gj[s] = -c * uu[s];
                 }
                 if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w], sj[w]);
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                ifinish_pre<EPL>(a, j[w], cj[w], sj[w], p, -c, 0.f, 0, gl, vj[w], aj[w], gj);
             }
             const float rg = a.rho;  // rho / G with G == 1
-            float gi[EPL], gg[EPL];
+            float gi[EPL], gg[EPL], bl[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) {
                 gu[s] += (1.f - a.rho) * sc * vi[s] + a.reg * uu[s];
-                gi[s] = sc * (rg * ug[0][s] + (1.f - a.rho) * uu[s]) + a.reg * vi[s];
+                bl[s] = rg * ug[0][s] + (1.f - a.rho) * uu[s];
+                gi[s] = sc * bl[s] + a.reg * vi[s];
                 gg[s] = rg * sc * vi[s] + a.reg * ug[0][s];
                 sq = fmaf(uu[s], uu[s], sq);
                 sq = fmaf(vi[s], vi[s], sq);
@@ -1181,7 +1224,8 @@ struct PairRows {
             else  // another rank's user: its gradient row goes back to the owner
                 gstore<EPL>(a.xgrads, -1 - g[0], d, gl, gg);
             if (gl == 0) bias_finish(a, i, ci, sc, si);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            if (a.recV != nullptr && ci >= 2 && si >= 0) gstore<EPL>(a.stashB, p, d, gl, bl);
+            ifinish_pre<EPL>(a, i, ci, si, p, sc, a.reg, 1, gl, vi, ai, gi);
         } else {  // CML
             float du[EPL];
 #pragma unroll
@@ -1229,7 +1273,8 @@ struct PairRows {
                         sq = fmaf(vj[w][s], vj[w][s], sq);
                     }
                 }
-                gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, j[w], cj[w], sj[w], d, gl, vj[w], aj[w], gj, a);
+                ifinish_pre<EPL>(a, j[w], cj[w], sj[w], p, coef, (l2 ? a.reg_cov : 0.f) - coef, 0, gl,
+                                 vj[w], aj[w], gj);
             }
             if (l2) {
 #pragma unroll
@@ -1241,7 +1286,7 @@ struct PairRows {
                 }
             }
             gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            gfinish_pre<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, i, ci, si, d, gl, vi, ai, gi, a);
+            ifinish_pre<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), 0, gl, vi, ai, gi);
         }
     }
 };
@@ -1342,13 +1387,39 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     const int ns = flagged ? 0 : (off != nullptr || local < cap) ? local : cap;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
-    {
-        const float* S = isU ? a.slotU : a.slotV;
-        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
 #ifndef CF_APPLY_NF
 #define CF_APPLY_NF 4
 #endif
-        constexpr int NF = CF_APPLY_NF;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
+    constexpr int NF = CF_APPLY_NF;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
+    if (!isU && a.recV != nullptr) {
+        // item records in rank order: g = sum alpha_k X_k + (sum beta_k) V_r,
+        // V_r still the pre-step row (a duplicated row is only written here)
+        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
+        float bsum = 0.f;
+        for (int t0 = 0; t0 < ns; t0 += NF) {
+            int4 rc[NF];
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < ns) rc[q] = a.recV[s0 + t0 + q];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < ns) gload<EPL>(rc[q].w ? a.stashB : a.stashU, rc[q].x, a.d, gl, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < ns) {
+                    const float al = __int_as_float(rc[q].y);
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) g[s] = fmaf(al, h[q][s], g[s]);
+                    bsum += __int_as_float(rc[q].z);
+                }
+        }
+        if (reduce_only) gload<EPL>(X, r, a.d, gl, x);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] = fmaf(bsum, x[s], g[s]);
+    } else {
+        const float* S = isU ? a.slotU : a.slotV;
+        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
         for (int t0 = 0; t0 < ns; t0 += NF) {
             float h[NF][EPL];
 #pragma unroll

@@ -393,6 +393,15 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                apply, 0 = one float atomic per occurrence (default: at
  *                cfg4 the atomics cost the gradient launch nothing measurable,
  *                165.1 vs 164.9 us, and the slot sums cost the apply 4 us).
+ *   "item_slots" what a duplicated item occurrence stores for the apply:
+ *                0 = its gradient row (4d B), 1 = a 16-B record (pair, alpha,
+ *                beta, which) -- every item gradient is alpha * X + beta *
+ *                V_row with X the pair's pre-update user row (or GBPR's group
+ *                blend), which the pair stashes once -- so the apply sums
+ *                alpha * X from the stash plus (sum of beta) * V_row.  Same
+ *                results up to fp32 summation order.  Default: 1 when
+ *                n_factors >= 128 (measured 10-12 % faster steps at cfg3 /
+ *                cfg5), else 0 (4-5 % slower at cfg2 / cfg4, d = 64).
  *   "deterministic" 1 = bitwise-reproducible steps: occurrence ranks from a
  *                stable sort of the batch's row ids, every occurrence of a
  *                duplicated row stored in its own compact slot and summed in

@@ -52,11 +52,12 @@ HP = {"cml": dict(margin=1.0, reg_cov=1.0, clip_norm=1.0),   # testcml.py:26-34
       "amf": dict(reg=0.05, reg_adv=1.0)}                     # testamf.py:23-33
 
 
-def _engine(model, fold1, d, W, grad_path, seed=41):
+def _engine(model, fold1, d, W, grad_path, seed=41, item_slots=0):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=1, seed=seed,
                **HP[model])
     e.set_option("grad_path", grad_path)
+    e.set_option("item_slots", item_slots)
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=6)
     return e
@@ -84,9 +85,10 @@ TABLES = {"cml": ("user", "item", "acc_user", "acc_item"),
     ("gbpr", 64, 0, None),    # cfg4: auto = phased grad_fast_kernel<GBPR, EPL 4, W 5>
     ("amf", 128, 0, 14),      # cfg5 across the phase switch (fresh accumulators)
 ], ids=["cml-d128-generic", "cml-d128-phased", "gbpr-d64-w5-g1", "amf-d128-switch"])
-def test_bench_shape_pipeline_trajectory(fold1, model, d, grad_path, switch):
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+def test_bench_shape_pipeline_trajectory(fold1, model, d, grad_path, switch, item_slots):
     W, B, K = 5, 100, 28
-    dev = _engine(model, fold1, d, W, grad_path)
+    dev = _engine(model, fold1, d, W, grad_path, item_slots=item_slots)
     rep = _engine(model, fold1, d, W, grad_path)       # same seed: the same batch stream
     T = {t: dev.get_table(t).astype(np.float64) for t in TABLES[model]}
     batches = [rep.sample(B) for _ in range(K)]
@@ -116,14 +118,16 @@ def _cfg2_graph():
     return synth_graph(1_000_000, 100_000, 50.0, 0.8, 20261015, n_threads=16)
 
 
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
 @pytest.mark.parametrize("model", ["cml", "amf"], ids=["cfg3-cml", "cfg5-amf-phase2"])
-def test_full_size_step(model):
+def test_full_size_step(model, item_slots):
     """One step at full cfg3 / cfg5 size (1M users x 100K items, d=128, W=5,
     B=65,536), after three pipelined steps, against the float64 oracle."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni, d, W, B = 1_000_000, 100_000, 128, 5, 65536
     ip, ix = _cfg2_graph()
     e = Engine(model, nu, ni, d, n_neg=W, seed=78, **HP[model])
+    e.set_option("item_slots", item_slots)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=1)
     if model == "amf":
@@ -139,7 +143,8 @@ def test_full_size_step(model):
     e.close()
 
 
-def test_cfg4_full_size_step_touched_rows():
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+def test_cfg4_full_size_step_touched_rows(item_slots):
     """cfg4 (GBPR, 10M users x 1M items, d=64, W=5, G=1, B=65,536): one step
     after two pipelined ones.  The oracle steps a compact copy of the rows the
     batch touches (ids re-indexed), which is the whole step: Adagrad leaves
@@ -148,6 +153,7 @@ def test_cfg4_full_size_step_touched_rows():
     nu, ni, d, W, B = 10_000_000, 1_000_000, 64, 5, 65536
     ip, ix = synth_graph(nu, ni, 20.0, 0.8, 20261015, n_threads=16)
     e = Engine("gbpr", nu, ni, d, n_neg=W, gsize=1, seed=79, **HP["gbpr"])
+    e.set_option("item_slots", item_slots)
     e.set_interactions(ip, ix)
     del ip, ix
     e.init_params(0.0, 0.1, truncated=True, seed=1)

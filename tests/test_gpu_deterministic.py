@@ -31,12 +31,13 @@ def skewed_graph():
     return synth_graph(40_000, 4_000, 30.0, 0.8, 20261015, n_threads=8)
 
 
-def _run(model, graph, d, W, B, steps, det, dense=False, phase=False):
+def _run(model, graph, d, W, B, steps, det, dense=False, phase=False, item_slots=0):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     ip, ix = graph
     e = Engine(model, len(ip) - 1, 4_000, d, n_neg=W, gsize=1, seed=17, dense_item_apply=dense,
                **HP[model])
     e.set_option("deterministic", 1 if det else 0)
+    e.set_option("item_slots", item_slots)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=3)
     if phase:
@@ -51,9 +52,11 @@ def _run(model, graph, d, W, B, steps, det, dense=False, phase=False):
                                              ("cml", 32, 5, False), ("amf", 32, 5, False),
                                              ("bpr", 32, 1, True)],
                          ids=["bpr", "gbpr", "cml", "amf-adv", "bpr-dense-items"])
-def test_two_runs_bitwise_identical(skewed_graph, model, d, W, dense):
-    a = _run(model, skewed_graph, d, W, 16384, 6, det=True, dense=dense, phase=(model == "amf"))
-    b = _run(model, skewed_graph, d, W, 16384, 6, det=True, dense=dense, phase=(model == "amf"))
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+def test_two_runs_bitwise_identical(skewed_graph, model, d, W, dense, item_slots):
+    kw = dict(dense=dense, phase=(model == "amf"), item_slots=item_slots)
+    a = _run(model, skewed_graph, d, W, 16384, 6, det=True, **kw)
+    b = _run(model, skewed_graph, d, W, 16384, 6, det=True, **kw)
     assert a[0] == b[0]                                   # the loss, bit for bit
     for t in TABLES[model]:
         assert np.array_equal(a[1][t], b[1][t]), t
@@ -62,15 +65,16 @@ def test_two_runs_bitwise_identical(skewed_graph, model, d, W, dense):
     # last-bit difference can flip a term (its oracle check is below)
     if model == "cml":
         return
-    c = _run(model, skewed_graph, d, W, 16384, 6, det=False, dense=dense, phase=(model == "amf"))
+    c = _run(model, skewed_graph, d, W, 16384, 6, det=False, **kw)
     assert abs(c[0] - a[0]) <= 1e-5 * abs(a[0])
     for t in TABLES[model]:
         ref = a[1][t].astype(np.float64)
         assert np.abs(c[1][t] - ref).max() <= 1e-5 * np.abs(ref).max(), t
 
 
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
 @pytest.mark.parametrize("model", ["bpr", "gbpr", "cml"])
-def test_deterministic_steps_match_oracle(skewed_graph, model):
+def test_deterministic_steps_match_oracle(skewed_graph, model, item_slots):
     """Host-fed deterministic steps on device-drawn batches with hot rows
     (hundreds of occurrences of the Zipf head) against the float64 oracle."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine
@@ -78,6 +82,7 @@ def test_deterministic_steps_match_oracle(skewed_graph, model):
     nu, ni, d, W, B = len(ip) - 1, 4_000, 32, (1 if model == "bpr" else 5), 8192
     e = Engine(model, nu, ni, d, n_neg=W, gsize=1, seed=23, **HP[model])
     e.set_option("deterministic", 1)
+    e.set_option("item_slots", item_slots)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=4)
     T = {t: e.get_table(t).astype(np.float64) for t in TABLES[model]}

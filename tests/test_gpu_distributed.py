@@ -27,7 +27,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q, exchange="allreduce",
-            backend="gloo"):
+            backend="gloo", item_slots=0):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -49,6 +49,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q, exc
     e = Engine(model, u1 - u0, 1682, U0.shape[1], n_neg=W, dense_item_apply=True,
                seed=10 + rank, **kw)
     e.set_option("item_reduce", item_reduce)
+    e.set_option("item_slots", item_slots)
     e.set_interactions(lip, lix)
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
@@ -90,9 +91,10 @@ def _check_elementwise(got, ref, rtol=1e-5, atol=1e-6):
     assert not bad.any(), (int(bad.sum()), float(err.max()))
 
 
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
 @pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
 @pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
-def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange):
+def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange, item_slots):
     """The RCCL path itself (nccl backend, world size 1 on device 0): the
     asynchronous collectives, the user apply beside them and the stream
     ordering of cf_step_local_apply / cf_step_items(_range) against them."""
@@ -105,7 +107,7 @@ def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), fold1, batches, U0, V0, model, 1, q,
-                                          exchange, "nccl"))
+                                          exchange, "nccl", item_slots))
     p.start()
     rank, u0, u1, Ul, Vr, AVr = q.get(timeout=300)
     p.join(timeout=120)

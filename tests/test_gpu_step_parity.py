@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
 _GRAD_PATH = [0]
+_ITEM_SLOTS = [0]
 _OPTS = {}   # extra cf_set_option values for make_engine
 
 
@@ -27,6 +28,15 @@ def grad_path(request):
     _GRAD_PATH[0] = request.param
     yield request.param
     _GRAD_PATH[0] = 0
+
+
+@pytest.fixture(autouse=True, params=[0, 1], ids=["rows", "records"])
+def item_slots(request):
+    """... and both item slot forms (cf_set_option item_slots): gradient rows,
+    or (pair, alpha, beta) records over the stashed user rows."""
+    _ITEM_SLOTS[0] = request.param
+    yield request.param
+    _ITEM_SLOTS[0] = 0
 
 
 def rel(a, b):
@@ -40,6 +50,7 @@ def make_engine(model, fold1, d, W, G=1, dense=False, **kw):
     e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, gsize=G,
                dense_item_apply=dense, seed=7, **kw)
     e.set_option("grad_path", _GRAD_PATH[0])
+    e.set_option("item_slots", _ITEM_SLOTS[0])
     for k, v in _OPTS.items():
         e.set_option(k, v)
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
