@@ -191,6 +191,7 @@ struct cf_engine {
     void* det_tmp = nullptr;
     size_t det_tmp_bytes = 0;
     float *slotUc = nullptr, *slotVc = nullptr, *slotVbc = nullptr;
+    float *hotP = nullptr, *hotPb = nullptr;   // sums of the 64-slot tiles inside one row
 
     // model state
     int phase = 0;
@@ -295,6 +296,8 @@ int ensure_det(cf_engine* e, int B) {
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc);
     dfree(e->recVc);
+    dfree(e->hotP);
+    dfree(e->hotPb);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     e->det_tmp = nullptr;
     e->det_cap = 0;
@@ -308,6 +311,8 @@ int ensure_det(cf_engine* e, int B) {
     else
         CF_TRY(dalloc(&e->slotVc, (size_t)nV * c.n_factors));
     if (has_bias(c)) CF_TRY(dalloc(&e->slotVbc, (size_t)nV));
+    CF_TRY(dalloc(&e->hotP, (size_t)(n / kDetTile + 1) * c.n_factors));
+    CF_TRY(dalloc(&e->hotPb, (size_t)(n / kDetTile + 1)));
     e->det_tmp_bytes = det_ranks_scratch(n, rows);
     if (e->det_tmp_bytes) {
         hipError_t he = hipMalloc(&e->det_tmp, e->det_tmp_bytes);
@@ -608,6 +613,10 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.recV = a.recV;
     p.stashU = a.stashU;
     p.stashB = a.stashB;
+    if (e->det) {
+        p.hotP = e->hotP;
+        p.hotPb = e->hotPb;
+    }
     p.n_items = c.n_items;
     p.count_users = a.count_users;
     p.count_items = a.count_items;
@@ -661,6 +670,28 @@ int det_ranks(cf_engine* e, const StepArgs& a) {
     return CF_OK;
 }
 
+// deterministic mode, after the gradient launch: the sums of the sorted
+// occurrence list's 64-slot tiles that lie inside one row, for the apply
+int det_hot(cf_engine* e, const StepArgs& a) {
+    if (!e->det) return CF_OK;
+    const cf_config& c = e->cfg;
+    HotArgs h{};
+    h.d = c.n_factors;
+    h.nU = (int64_t)a.B * users_per_pair(c);
+    h.n = h.nU + (int64_t)a.B * items_per_pair(c);
+    h.n_users = c.n_users;
+    h.skeys = e->det_keys + h.n;   // the sort's output half
+    h.slotU = a.slotU;
+    h.slotV = a.recV ? nullptr : a.slotV;
+    h.recV = a.recV;
+    h.stashU = a.stashU;
+    h.stashB = a.stashB;
+    h.P = e->hotP;
+    h.Pb = e->hotPb;
+    CF_HIP(launch_det_hot(h, e->stream));
+    return CF_OK;
+}
+
 int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
     CF_TRY(det_ranks(e, a));
@@ -673,6 +704,7 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
             ProfScope ps(e, CF_K_GRAD_PREP);
             CF_HIP(launch_grad(a, e->stream, next));
         }
+        CF_TRY(det_hot(e, a));
         ProfScope ps(e, CF_K_APPLY);
         CF_HIP(launch_apply(p, e->stream));
         if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
@@ -682,6 +714,7 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
+    CF_TRY(det_hot(e, a));
     if (next) {
         ProfScope ps(e, CF_K_APPLY_PREP);
         CF_HIP(launch_apply_prep(p, *next, e->stream));
@@ -1044,6 +1077,7 @@ int cf_destroy(cf_engine* e) {
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
+    dfree(e->hotP); dfree(e->hotPb);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -1380,6 +1414,7 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));
     }
+    CF_TRY(det_hot(e, a));
     e->last_occV = a.occV;
     e->last_nV = (int64_t)B * items_per_pair(e->cfg);
     if (a.items_grad_only && a.capV > 0) {

@@ -161,6 +161,11 @@ struct ApplyArgs {
     const int4* __restrict__ recV;       // item records (StepArgs)
     const float* __restrict__ stashU;
     const float* __restrict__ stashB;
+    // deterministic mode: sums of the 64-slot tiles that lie inside one row
+    // (det_hot_kernel); a row with >= 2 x 64 slots adds them in tile order
+    // between its head and tail slots
+    const float* __restrict__ hotP;      // [tiles, d]
+    const float* __restrict__ hotPb;     // [tiles] records: the tile's beta sum
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -171,6 +176,23 @@ struct ApplyArgs {
     int n_partial;
     double* __restrict__ loss_acc;
 };
+
+// deterministic mode: the slot sums of every 64-position tile of the sorted
+// occurrence list (users [0, nU), then items) that lies inside one row
+constexpr int kDetTile = 64;
+struct HotArgs {
+    int d;
+    int64_t n, nU, n_users;
+    const int32_t* __restrict__ skeys;   // sorted row keys (items offset by n_users)
+    const float* __restrict__ slotU;     // compact user slot rows
+    const float* __restrict__ slotV;     // compact item slot rows (null with records)
+    const int4* __restrict__ recV;       // compact item records (null with slot rows)
+    const float* __restrict__ stashU;
+    const float* __restrict__ stashB;
+    float* __restrict__ P;               // [n / kDetTile, d]
+    float* __restrict__ Pb;              // [n / kDetTile]
+};
+hipError_t launch_det_hot(const HotArgs& h, hipStream_t s);
 
 struct DenseArgs {
     int d;

@@ -1364,7 +1364,50 @@ __global__ __launch_bounds__(kWave) void grad_fast_wave_kernel(StepArgs a) {
 // atomic sum in G for a hot row (G re-zeroed); Adagrad; the count reset.
 // Block 0 also folds the grad kernel's loss partials.
 // ---------------------------------------------------------------------------
-template <int EPL>
+// a duplicated row's slots [lo, hi) (base s0) added to g in rank order:
+// gradient rows, or item records (alpha X from the stash into g, beta into bsum)
+template <int EPL, int NF>
+__device__ __forceinline__ void slot_sum(const ApplyArgs& a, bool isU, int64_t s0, int lo, int hi, int gl,
+                                         float (&g)[EPL], float& bsum) {
+    if (!isU && a.recV != nullptr) {
+        for (int t0 = lo; t0 < hi; t0 += NF) {
+            int4 rc[NF];
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < hi) rc[q] = a.recV[s0 + t0 + q];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < hi) gload<EPL>(rc[q].w ? a.stashB : a.stashU, rc[q].x, a.d, gl, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < hi) {
+                    const float al = __int_as_float(rc[q].y);
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) g[s] = fmaf(al, h[q][s], g[s]);
+                    bsum += __int_as_float(rc[q].z);
+                }
+        }
+    } else {
+        const float* S = isU ? a.slotU : a.slotV;
+        for (int t0 = lo; t0 < hi; t0 += NF) {
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < hi) gload<EPL>(S, s0 + t0 + q, a.d, gl, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < hi) {
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+                }
+        }
+    }
+}
+
+// HOT: the deterministic-mode launch that adds whole-tile sums (its own
+// instantiation: the tile path's registers would slow every fast-path apply)
+template <int EPL, bool HOT = false>
 __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool isU, int c, int gl) {
     int32_t* cnt = isU ? a.cntU : a.cntV;
     float* X = isU ? a.U : a.V;
@@ -1391,47 +1434,36 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
 #define CF_APPLY_NF 4
 #endif
     constexpr int NF = CF_APPLY_NF;  // slot rows in flight, summed in rank order (8: occupancy 5, slower)
-    if (!isU && a.recV != nullptr) {
-        // item records in rank order: g = sum alpha_k X_k + (sum beta_k) V_r,
-        // V_r still the pre-step row (a duplicated row is only written here)
-        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
-        float bsum = 0.f;
-        for (int t0 = 0; t0 < ns; t0 += NF) {
-            int4 rc[NF];
+    // slots [0, ns) in rank order -- or, in deterministic mode for a row of
+    // >= 2 whole 64-slot tiles, the head before its first whole tile, the
+    // tiles' sums (det_hot_kernel) in tile order, then the tail
+    const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
+    float bsum = 0.f;
+    if (HOT && off != nullptr && ns >= 2 * kDetTile) {
+        const int64_t gs = (isU ? 0 : a.nU) + off[r], ge = gs + ns;
+        const int64_t qa = (gs + kDetTile - 1) / kDetTile, qb = ge / kDetTile;
+        slot_sum<EPL, NF>(a, isU, s0, 0, (int)(qa * kDetTile - gs), gl, g, bsum);
+        for (int64_t q0 = qa; q0 < qb; q0 += NF) {
             float h[NF][EPL];
 #pragma unroll
             for (int q = 0; q < NF; ++q)
-                if (t0 + q < ns) rc[q] = a.recV[s0 + t0 + q];
+                if (q0 + q < qb) gload<EPL>(a.hotP, q0 + q, a.d, gl, h[q]);
 #pragma unroll
             for (int q = 0; q < NF; ++q)
-                if (t0 + q < ns) gload<EPL>(rc[q].w ? a.stashB : a.stashU, rc[q].x, a.d, gl, h[q]);
+                if (q0 + q < qb) {
 #pragma unroll
-            for (int q = 0; q < NF; ++q)
-                if (t0 + q < ns) {
-                    const float al = __int_as_float(rc[q].y);
-#pragma unroll
-                    for (int s = 0; s < EPL; ++s) g[s] = fmaf(al, h[q][s], g[s]);
-                    bsum += __int_as_float(rc[q].z);
+                    for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+                    if (!isU && a.recV != nullptr) bsum += a.hotPb[q0 + q];
                 }
         }
+        slot_sum<EPL, NF>(a, isU, s0, (int)(qb * kDetTile - gs), ns, gl, g, bsum);
+    } else {
+        slot_sum<EPL, NF>(a, isU, s0, 0, ns, gl, g, bsum);
+    }
+    if (!isU && a.recV != nullptr) {
         if (reduce_only) gload<EPL>(X, r, a.d, gl, x);
 #pragma unroll
         for (int s = 0; s < EPL; ++s) g[s] = fmaf(bsum, x[s], g[s]);
-    } else {
-        const float* S = isU ? a.slotU : a.slotV;
-        const int64_t s0 = off != nullptr ? (int64_t)off[r] : r * (int64_t)cap;
-        for (int t0 = 0; t0 < ns; t0 += NF) {
-            float h[NF][EPL];
-#pragma unroll
-            for (int q = 0; q < NF; ++q)
-                if (t0 + q < ns) gload<EPL>(S, s0 + t0 + q, a.d, gl, h[q]);
-#pragma unroll
-            for (int q = 0; q < NF; ++q)
-                if (t0 + q < ns) {
-#pragma unroll
-                    for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
-                }
-        }
     }
     if (off == nullptr && (flagged || local > cap)) {  // the atomic sums: G, and for items the copies in use
         const int nrep = isU ? 0 : a.repV;   // copies 1..repV (unused ones are zero)
@@ -1479,6 +1511,78 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     }
 }
 
+// Deterministic mode: one block per 64-position tile of the sorted occurrence
+// list.  A tile whose first and last positions hold the same row lies inside
+// that row: its 16 groups sum four slots each (rows, or item records over the
+// stash), group 0 adds the 16 partials in group order -- a fixed tree, so the
+// row's sum stays bitwise reproducible -- and stores the tile's sum.
+template <int EPL>
+__global__ __launch_bounds__(kBlock) void det_hot_kernel(HotArgs h) {
+    __shared__ float s_p[kGroupsPerBlock][kGL * EPL];
+    __shared__ float s_b[kGroupsPerBlock];
+    const int gl = threadIdx.x & (kGL - 1);
+    const int grp = threadIdx.x >> 4;
+    const int64_t ntiles = h.n / kDetTile;
+    for (int64_t q = blockIdx.x; q < ntiles; q += gridDim.x) {
+        const int64_t p0 = q * kDetTile;
+        const int32_t k0 = h.skeys[p0];
+        if (k0 != h.skeys[p0 + kDetTile - 1]) continue;   // block-uniform
+        const bool isU = k0 < h.n_users;
+        float g[EPL], t[4][EPL];
+        float bs = 0.f;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] = 0.f;
+        constexpr int PER = kDetTile / kGroupsPerBlock;   // 4
+        const int64_t pos = p0 + grp * PER;
+        if (isU) {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) gload<EPL>(h.slotU, pos + k, h.d, gl, t[k]);
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] += t[k][s];
+        } else if (h.recV != nullptr) {
+            int4 rc[PER];
+#pragma unroll
+            for (int k = 0; k < PER; ++k) rc[k] = h.recV[pos + k - h.nU];
+#pragma unroll
+            for (int k = 0; k < PER; ++k) gload<EPL>(rc[k].w ? h.stashB : h.stashU, rc[k].x, h.d, gl, t[k]);
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const float al = __int_as_float(rc[k].y);
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] = fmaf(al, t[k][s], g[s]);
+                bs += __int_as_float(rc[k].z);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) gload<EPL>(h.slotV, pos + k - h.nU, h.d, gl, t[k]);
+#pragma unroll
+            for (int k = 0; k < PER; ++k)
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] += t[k][s];
+        }
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) s_p[grp][gl * EPL + s] = g[s];
+        if (gl == 0) s_b[grp] = bs;
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) g[s] = s_p[0][gl * EPL + s];
+            bs = s_b[0];
+            for (int k = 1; k < kGroupsPerBlock; ++k) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] += s_p[k][gl * EPL + s];
+                bs += s_b[k];
+            }
+            gstore<EPL>(h.P, q, h.d, gl, g);
+            if (gl == 0) h.Pb[q] = bs;
+        }
+        __syncthreads();   // s_p reused by the next tile
+    }
+}
+
+
 #ifndef CF_APPLY_DETECT_WAVES
 #define CF_APPLY_DETECT_WAVES 1   // 4 measured slower: ~46 owners per block, ~3 per group in series
 #endif
@@ -1494,7 +1598,7 @@ constexpr int kApplyDetectWaves = CF_APPLY_DETECT_WAVES;
 constexpr int kApplyChunk = CF_APPLY_CHUNK;
 
 // BS = workgroup size (256, or 64 for one-wave apply blocks)
-template <int EPL, int BS = kBlock>
+template <int EPL, int BS = kBlock, bool HOT = false>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     constexpr int NWV = BS / kWave, NGR = BS / kGL;
     __shared__ double s_red[NWV];
@@ -1586,15 +1690,15 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 rem -= c;
             }
             if (src < 0) break;  // group-uniform
-            apply_row<EPL>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
+            apply_row<EPL, HOT>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
         }
         __syncthreads();  // s_* reused by the next chunk
     }
 }
 
-template <int EPL>
+template <int EPL, bool HOT>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
-    apply_body<EPL>(a, blockIdx.x, gridDim.x);
+    apply_body<EPL, kBlock, HOT>(a, blockIdx.x, gridDim.x);
 }
 
 // one-wave apply blocks: the detecting wave's own four groups apply its owners
@@ -1606,7 +1710,7 @@ __global__ __launch_bounds__(kWave) void apply_wave_kernel(ApplyArgs a) {
 // horizontal fusion on the device-sampler path: apply of step s (blocks
 // [0, napply)) beside the draw + count of step s+1 (the rest) -- independent
 // work (other buffer set), one launch instead of two
-template <int EPL, int MODEL>
+template <int EPL, int MODEL, bool HOT>
 #ifndef CF_APPLY_PREP_ORDER
 #define CF_APPLY_PREP_ORDER 0  // 0: apply blocks first, 1: draw blocks first, 2: interleaved
 #endif
@@ -1619,15 +1723,15 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
     if (minor_block(blockIdx.x, napply, nprep, idx))
         prep_any<MODEL>(a, idx);
     else
-        apply_body<EPL>(p, idx, napply);
+        apply_body<EPL, kBlock, HOT>(p, idx, napply);
 #elif CF_APPLY_PREP_ORDER == 1
     if ((int)blockIdx.x < nprep)
         prep_any<MODEL>(a, blockIdx.x);
     else
-        apply_body<EPL>(p, blockIdx.x - nprep, napply);
+        apply_body<EPL, kBlock, HOT>(p, blockIdx.x - nprep, napply);
 #else
     if ((int)blockIdx.x < napply)
-        apply_body<EPL>(p, blockIdx.x, napply);
+        apply_body<EPL, kBlock, HOT>(p, blockIdx.x, napply);
     else
         prep_any<MODEL>(a, blockIdx.x - napply);
 #endif
@@ -2042,6 +2146,19 @@ static int apply_grid(const ApplyArgs& a) {
 #define CF_APPLY_WAVE_BLOCKS 0
 #endif
 
+template <bool HOT>
+static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
+    const dim3 grid(apply_grid(a)), block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL((apply_kernel<1, HOT>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((apply_kernel<2, HOT>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((apply_kernel<4, HOT>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((apply_kernel<8, HOT>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((apply_kernel<16, HOT>), grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
     if (CF_APPLY_WAVE_BLOCKS) {
         const dim3 grid(apply_grid(a)), block(kWave);
@@ -2054,35 +2171,29 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    const dim3 grid(apply_grid(a)), block(kBlock);
-    switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL(apply_kernel<1>, grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL(apply_kernel<2>, grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL(apply_kernel<4>, grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL(apply_kernel<8>, grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL(apply_kernel<16>, grid, block, 0, s, a); break;
-    }
-    return hipGetLastError();
+    return a.hotP != nullptr ? launch_apply_h<true>(a, s) : launch_apply_h<false>(a, s);
 }
 
-template <int MODEL>
+template <int MODEL, bool HOT>
 static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     const int na = apply_grid(p);
     const int np = prep_blocks(&a);
     const dim3 grid(na + np), block(kBlock);
     switch (epl_for(p.d)) {
-        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL>), grid, block, 0, s, p, a, na); break;
-        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL>), grid, block, 0, s, p, a, na); break;
-        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL>), grid, block, 0, s, p, a, na); break;
-        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL>), grid, block, 0, s, p, a, na); break;
-        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL>), grid, block, 0, s, p, a, na); break;
+        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return launch_apply(p, s);
-    return a.model == GBPR ? launch_apply_prep_m<GBPR>(p, a, s) : launch_apply_prep_m<BPR>(p, a, s);
+    if (p.hotP != nullptr)
+        return a.model == GBPR ? launch_apply_prep_m<GBPR, true>(p, a, s) : launch_apply_prep_m<BPR, true>(p, a, s);
+    return a.model == GBPR ? launch_apply_prep_m<GBPR, false>(p, a, s) : launch_apply_prep_m<BPR, false>(p, a, s);
 }
 
 static int row_grid(int64_t n_rows) {
@@ -2274,6 +2385,20 @@ PermKey make_perm_key(uint64_t n, uint64_t seed, uint64_t epoch) {
         p.m[r] = (mix64(h ^ 0xA0761D6478BD642Full) | 1ull);
     }
     return p;
+}
+
+hipError_t launch_det_hot(const HotArgs& h, hipStream_t s) {
+    const int64_t ntiles = h.n / kDetTile;
+    if (ntiles <= 0) return hipSuccess;
+    const dim3 grid((unsigned)(ntiles < 16384 ? ntiles : 16384)), block(kBlock);
+    switch (epl_for(h.d)) {
+        case 1: hipLaunchKernelGGL(det_hot_kernel<1>, grid, block, 0, s, h); break;
+        case 2: hipLaunchKernelGGL(det_hot_kernel<2>, grid, block, 0, s, h); break;
+        case 4: hipLaunchKernelGGL(det_hot_kernel<4>, grid, block, 0, s, h); break;
+        case 8: hipLaunchKernelGGL(det_hot_kernel<8>, grid, block, 0, s, h); break;
+        default: hipLaunchKernelGGL(det_hot_kernel<16>, grid, block, 0, s, h); break;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace cfk

@@ -1,0 +1,29 @@
+#!/bin/bash
+# Round-2 deterministic-mode tile sums: det tests, then det / fast benches.
+set -o pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/r02j
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_deterministic.py tests/test_gpu_step_parity.py > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $OUT/pytest.log; exit 1; }
+tail -3 $OUT/pytest.log
+Q="--steps 60 --warmup 10 --no-cpu-baseline --no-ndcg --secondary-batch 0"
+summ() {
+python - "$1" <<'PY'
+import json, sys
+r = json.loads(open(sys.argv[1]).read())
+k = r["kernels"]
+print(sys.argv[1].split("/")[-1], "ms/step %.4f" % r["ms_per_step"], {n: round(v["avg_us"], 1) for n, v in k.items() if isinstance(v, dict) and v["launches"] > 1})
+PY
+}
+run() { # name args
+  local n=$1; shift
+  timeout -k 10 300 python bench.py $Q "$@" > $OUT/$n.json 2> $OUT/$n.err || { echo "$n failed"; tail -5 $OUT/$n.err; exit 1; }
+  summ $OUT/$n.json
+}
+run cfg2_fast --config cfg2
+run cfg2_det --config cfg2 --deterministic 1
+run cfg4_det --config cfg4 --deterministic 1
+run cfg3_det --config cfg3 --deterministic 1
+run cfg5_fast --config cfg5
+echo ALL DONE
