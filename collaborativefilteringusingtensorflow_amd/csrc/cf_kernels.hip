@@ -279,6 +279,19 @@ __device__ __forceinline__ void bias_finish(const StepArgs& a, int64_t r, int co
     }
 }
 
+// bias_finish with the row's bias and accumulator already in registers (the
+// phased kernel loads them with the rows): no load at the end of the pair
+__device__ __forceinline__ void bias_finish_pre(const StepArgs& a, int64_t r, int count, float g,
+                                                int64_t slot, float b0, float ab0) {
+    if (count == 1 && !a.items_grad_only) {
+        const float acc = fmaf(g, g, ab0);
+        a.Ab[r] = acc;
+        a.b[r] = b0 - adagrad_delta(a.lr, g, acc);
+    } else {
+        bias_finish(a, r, count, g, slot);
+    }
+}
+
 __device__ __forceinline__ float neg_log_sigmoid(float x) {
     // literal -log(sigmoid(x)) as in bprmf.py:70 / gbprmf.py:88
     return -logf(rcp_1p(expf(-x)));
@@ -1081,6 +1094,7 @@ struct PairRows {
     float vj[WT][EPL], aj[WT][EPL];
     float ug[NGA][EPL], ag[NGA][EPL];
     float bi, bj[WT];
+    float abi, abj[WT];   // GBPR: bias accumulators of rows seen once
 
     __device__ __forceinline__ void load_idx(const StepArgs& a, int pair) {
         p = pair;
@@ -1133,6 +1147,11 @@ struct PairRows {
         for (int w = 0; w < WT; ++w) gload_acc<EPL>(a.AV, j[w], a.d, gl, item_acc && cj[w] == 1, aj[w]);
 #pragma unroll
         for (int k = 0; k < NG; ++k) gload_acc<EPL>(a.AU, g[k], a.d, gl, cg[k] == 1, ag[k]);
+        if (MODEL == GBPR) {
+            abi = (item_acc && ci == 1) ? a.Ab[i] : 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) abj[w] = (item_acc && cj[w] == 1) ? a.Ab[j[w]] : 0.f;
+        }
     }
 
     __device__ __forceinline__ void update(const StepArgs& a, int gl, float& loss_g, float& sq) {
@@ -1204,7 +1223,7 @@ struct PairRows {
                     gu[s] = fmaf(-c, vj[w][s], gu[s]);
                     gj[s] = -c * uu[s];
                 }
-                if (gl == 0) bias_finish(a, j[w], cj[w], -c + a.reg * bj[w], sj[w]);
+                if (gl == 0) bias_finish_pre(a, j[w], cj[w], -c + a.reg * bj[w], sj[w], bj[w], abj[w]);
                 ifinish_pre<EPL>(a, j[w], cj[w], sj[w], p, -c, 0.f, 0, gl, vj[w], aj[w], gj);
             }
             const float rg = a.rho;  // rho / G with G == 1
@@ -1223,7 +1242,7 @@ struct PairRows {
                 gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g[0], cg[0], sg[0], d, gl, ug[0], ag[0], gg, a);
             else  // another rank's user: its gradient row goes back to the owner
                 gstore<EPL>(a.xgrads, -1 - g[0], d, gl, gg);
-            if (gl == 0) bias_finish(a, i, ci, sc, si);
+            if (gl == 0) bias_finish_pre(a, i, ci, sc, si, bi, abi);
             if (a.recV != nullptr && ci >= 2 && si >= 0) gstore<EPL>(a.stashB, p, d, gl, bl);
             ifinish_pre<EPL>(a, i, ci, si, p, sc, a.reg, 1, gl, vi, ai, gi);
         } else {  // CML
