@@ -328,6 +328,8 @@ def main():
                     help="cf_set_option item_slots (duplicated item rows: 1 records, 0 gradient rows; -1 default)")
     ap.add_argument("--bias-slots", type=int, default=-1,
                     help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
+    ap.add_argument("--pos-sort", type=int, default=-1,
+                    help="cf_set_option pos_sort (gradient pairs in positive-item order; -1 default)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="cf_set_option deterministic (sort-based ranks, no float atomics)")
     ap.add_argument("--dry-run", action="store_true",
@@ -437,6 +439,8 @@ def main():
         eng.set_option("bias_slots", args.bias_slots)
     if args.item_slots >= 0:
         eng.set_option("item_slots", args.item_slots)
+    if args.pos_sort >= 0:
+        eng.set_option("pos_sort", args.pos_sort)
     if args.deterministic:
         eng.set_option("deterministic", 1)
     if args.slot_max:
@@ -516,7 +520,7 @@ def main():
         sync()
         eng.profile(False)
         for kname in ("sample", "slot", "step", "grad_prep", "apply", "apply_prep", "apply_slot", "item_reduce",
-                      "apply_dense", "clip"):
+                      "apply_dense", "clip", "psort"):
             ms, n = eng.profile_read(kname)
             if n:
                 kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}

@@ -71,7 +71,66 @@ int grid_of(int64_t n) {
     return (int)(b < 1 ? 1 : b > 4096 ? 4096 : b);
 }
 
+// positive-sorted gradient: pair p goes to position offP[i_p] + its rank
+// among the batch's positives of i_p (counting sort by positive item), as
+// one record (u, rank_u, i, p, (j_w, rank_j_w)...) of psort_stride(W) ints
+__device__ __forceinline__ int32_t rank16(int32_t r) { return r < 0xFFFF ? r : 0xFFFF; }
+
+template <int W>
+__global__ void psort_scatter_kernel(const int32_t* __restrict__ occU, const int32_t* __restrict__ rankU,
+                                     const int32_t* __restrict__ occV, const int32_t* __restrict__ rankV,
+                                     int B, const int32_t* __restrict__ offP, int32_t* __restrict__ srec) {
+    constexpr int RS = psort_stride(W);
+    const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nt = gridDim.x * blockDim.x;
+    for (int p = t0; p < B; p += nt) {
+        const int32_t i = occV[p];
+        int32_t v[RS], rk[W + 2];
+        v[0] = occU[p];
+        v[1] = i;
+        rk[0] = rank16(rankU[p]);
+        rk[W + 1] = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const int64_t q = (int64_t)B + (int64_t)p * W + w;
+            v[2 + w] = occV[q];
+            rk[1 + w] = rank16(rankV[q]);
+        }
+#pragma unroll
+        for (int k = 0; k < (W + 2) / 2; ++k) v[2 + W + k] = rk[2 * k] | (rk[2 * k + 1] << 16);
+#pragma unroll
+        for (int k = 2 + W + (W + 2) / 2; k < RS; ++k) v[k] = 0;
+        int4* r = reinterpret_cast<int4*>(srec + (int64_t)(offP[i] + rankV[p]) * RS);
+#pragma unroll
+        for (int k = 0; k < RS / 4; ++k) r[k] = make_int4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+}
+
 }  // namespace
+
+size_t psort_scratch(int64_t n_items) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                           (int)n_items);
+    return bytes;
+}
+
+hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
+                        int B, int W, const int32_t* cntP, int32_t* offP, int32_t* srec, int64_t n_items,
+                        void* tmp, size_t tmp_bytes, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    size_t bytes = tmp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cntP, offP, (int)n_items, s);
+    if (e != hipSuccess) return e;
+    switch (W) {
+        case 1: hipLaunchKernelGGL(psort_scatter_kernel<1>, dim3(grid_of(B)), dim3(256), 0, s, occU, rankU, occV,
+                                   rankV, B, offP, srec); break;
+        case 5: hipLaunchKernelGGL(psort_scatter_kernel<5>, dim3(grid_of(B)), dim3(256), 0, s, occU, rankU, occV,
+                                   rankV, B, offP, srec); break;
+        default: return hipErrorInvalidValue;   // pos_sort runs at W in {1, 5}
+    }
+    return hipGetLastError();
+}
 
 size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows) {
     size_t bytes = 0;

@@ -101,6 +101,18 @@ struct cf_engine {
     // GV and hot_rep - 1 extra copies (cf_set_option "hot_replicas")
     float* GVrep = nullptr;   // [hot_rep - 1][n_items, d]
     int hot_rep = 1;
+    // positive-sorted gradient (cf_set_option "pos_sort"): positives counted
+    // in cntP, pairs visited in positive-item order, one partial row per
+    // (gradient block, positive item) in slotP (StepArgs::cntP)
+    int pos_sort = 2;                 // 0 off, 1 on, 2 auto: on for B >= kPsortAutoB
+    int capP = 8;
+    int32_t* cntP_[2] = {nullptr, nullptr};
+    int32_t* offP = nullptr;          // [n_items]
+    int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
+    int order_cap = 0;
+    float* slotP = nullptr;           // [n_items * capP, d]
+    void* psort_tmp = nullptr;
+    size_t psort_tmp_bytes = 0;
     bool slots_ready = false;
     // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
     // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches);
@@ -258,6 +270,32 @@ int users_per_pair(const cf_config& c) { return c.model == CF_GBPR ? 1 + c.gsize
 int items_per_pair(const cf_config& c) { return 1 + c.n_neg; }
 int group_count(const cf_config& c) { return c.model == CF_GBPR ? c.gsize : 0; }
 
+// pos_sort applies: BPR / AMF / CML steps on the phased gradient kernel
+// (must agree with fast_w() in cf_kernels.hip) and none of the modes it does
+// not combine with
+// auto pos_sort from this batch size up: below it the sort launches cost more
+// than the fewer duplicate rows save (cfg2 A/B: -7 % at 2^19, -3.5 % at 2^18,
+// even at 2^17)
+constexpr int kPsortAutoB = 1 << 18;
+
+// the engine's model / shape / slot form can take pos_sort (its buffers are
+// allocated only then)
+bool psort_possible(const cf_engine* e) {
+    const cf_config& c = e->cfg;
+    if (!e->pos_sort || c.dense_item_apply || e->item_recs) return false;
+    if (c.model != CF_BPR && c.model != CF_AMF && c.model != CF_CML) return false;
+    return c.n_factors <= 128 && (c.n_neg == 1 || c.n_neg == 5);
+}
+
+bool psort_active(const cf_engine* e, int B) {
+    const cf_config& c = e->cfg;
+    if (!psort_possible(e) || (e->pos_sort == 2 && B < kPsortAutoB) || e->det || e->hot_rep > 1 ||
+        e->neg_check == 2 || e->pipeline == 2)
+        return false;
+    if (e->grad_path == 1 || (e->grad_path == 0 && c.model == CF_CML && c.n_neg == 5)) return false;
+    return true;
+}
+
 int ensure_slots(cf_engine* e) {
     if (e->slots_ready) return CF_OK;
     const cf_config& c = e->cfg;
@@ -267,6 +305,24 @@ int ensure_slots(cf_engine* e) {
     dfree(e->slotVb);
     dfree(e->recV);
     dfree(e->GVrep);
+    dfree(e->slotP);
+    dfree(e->offP);
+    for (int k = 0; k < 2; ++k) dfree(e->cntP_[k]);
+    if (e->psort_tmp) (void)hipFree(e->psort_tmp);
+    e->psort_tmp = nullptr;
+    if (psort_possible(e)) {
+        CF_TRY(dalloc(&e->slotP, (size_t)c.n_items * e->capP * c.n_factors));
+        CF_TRY(dalloc(&e->offP, (size_t)c.n_items));
+        for (int k = 0; k < 2; ++k) {
+            CF_TRY(dalloc(&e->cntP_[k], (size_t)c.n_items));
+            CF_HIP(hipMemsetAsync(e->cntP_[k], 0, (size_t)c.n_items * 4, e->stream));
+        }
+        e->psort_tmp_bytes = psort_scratch(c.n_items);
+        if (e->psort_tmp_bytes) {
+            hipError_t he = hipMalloc(&e->psort_tmp, e->psort_tmp_bytes);
+            if (he != hipSuccess) return fail(CF_ENOMEM, std::string("hipMalloc (psort scratch): ") + hipGetErrorString(he));
+        }
+    }
     CF_TRY(dalloc(&e->slotU, (size_t)c.n_users * e->capU * c.n_factors));
     if (!c.dense_item_apply || e->item_reduce == 1) {
         if (e->item_recs)
@@ -335,8 +391,11 @@ int ensure_stash(cf_engine* e, int B) {
     return CF_OK;
 }
 
+int ensure_order(cf_engine* e, int B);
+
 int ensure_batch(cf_engine* e, int B) {
     CF_TRY(ensure_slots(e));
+    CF_TRY(ensure_order(e, B));
     if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap)));
     CF_TRY(ensure_stash(e, std::max(B, e->Bcap)));
     if (B <= e->Bcap) return CF_OK;
@@ -357,6 +416,16 @@ int ensure_batch(cf_engine* e, int B) {
     }
     CF_TRY(dalloc(&e->loss_partial, (size_t)grad_blocks_max(B)));
     e->Bcap = B;
+    return CF_OK;
+}
+
+int ensure_order(cf_engine* e, int B) {
+    if (!psort_possible(e) || (e->srec && B <= e->order_cap)) return CF_OK;
+    CF_HIP(hipStreamSynchronize(e->stream));
+    CF_HIP(hipStreamSynchronize(e->side));
+    dfree(e->srec);
+    CF_TRY(dalloc(&e->srec, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg)));
+    e->order_cap = std::max(B, e->Bcap);
     return CF_OK;
 }
 
@@ -428,6 +497,13 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.recV = e->det ? e->recVc : e->recV;
         a.stashU = e->stashU;
         a.stashB = e->stashB;
+    }
+    if (psort_active(e, B) && e->cntP_[k] && e->srec && e->order_cap >= B) {
+        a.cntP = e->cntP_[k];
+        a.offP = e->offP;
+        a.srec = e->srec;
+        a.slotP = e->slotP;
+        a.capP = e->capP;
     }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
@@ -613,6 +689,13 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.recV = a.recV;
     p.stashU = a.stashU;
     p.stashB = a.stashB;
+    if (a.cntP != nullptr && a.count_items) {
+        p.cntP = a.cntP;
+        p.offP = a.offP;
+        p.slotP = a.slotP;
+        p.capP = a.capP;
+        p.nPos = B;
+    }
     if (e->det) {
         p.hotP = e->hotP;
         p.hotPb = e->hotPb;
@@ -692,9 +775,19 @@ int det_hot(cf_engine* e, const StepArgs& a) {
     return CF_OK;
 }
 
+// pos_sort: order the batch's pairs by positive item before its gradient launch
+int psort(cf_engine* e, const StepArgs& a) {
+    if (a.srec == nullptr) return CF_OK;
+    ProfScope ps(e, CF_K_PSORT);
+    CF_HIP(launch_psort(a.occU, a.rankU, a.occV, a.rankV, a.B, a.W, a.cntP, e->offP, e->srec, e->cfg.n_items,
+                        e->psort_tmp, e->psort_tmp_bytes, e->stream));
+    return CF_OK;
+}
+
 int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
                 const StepArgs* next) {
     CF_TRY(det_ranks(e, a));
+    CF_TRY(psort(e, a));
     ApplyArgs p = apply_args(e, a, B, k, loss_acc);
     if (next && e->pipeline == 2) {
         p.n_partial = grad_blocks(a, true);   // the launch with draw blocks keeps 256-lane groups
@@ -811,6 +904,7 @@ int discard_pending(cf_engine* e) {
         const int64_t nU = (int64_t)e->x_pend_B * users_per_pair(c), nV = (int64_t)e->x_pend_B * items_per_pair(c);
         if (a.count_users) CF_HIP(launch_uncount(a.occU, nU, a.cntU, e->stream));
         if (a.count_items) CF_HIP(launch_uncount(a.occV, nV, a.cntV, e->stream));
+        if (a.count_items && a.cntP) CF_HIP(launch_uncount(a.occV, e->x_pend_B, a.cntP, e->stream));
         e->epoch = e->x_pend_epoch;
         e->batch = e->x_pend_batch;
         e->sampler_B = e->x_pend_sampler_B;
@@ -823,6 +917,7 @@ int discard_pending(cf_engine* e) {
     const int64_t nU = (int64_t)e->pend_B * users_per_pair(c), nV = (int64_t)e->pend_B * items_per_pair(c);
     if (a.count_users) CF_HIP(launch_uncount(a.occU, nU, a.cntU, e->stream));
     if (a.count_items) CF_HIP(launch_uncount(a.occV, nV, a.cntV, e->stream));
+    if (a.count_items && a.cntP) CF_HIP(launch_uncount(a.occV, e->pend_B, a.cntP, e->stream));
     e->epoch = e->pend_epoch;
     e->batch = e->pend_batch;
     e->sampler_B = e->pend_sampler_B;
@@ -1078,6 +1173,8 @@ int cf_destroy(cf_engine* e) {
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
     dfree(e->hotP); dfree(e->hotPb);
+    dfree(e->slotP); dfree(e->offP); dfree(e->srec); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
+    if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
@@ -1946,6 +2043,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     }
     if (n == "pipeline") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "pipeline must be 0, 1 or 2");
+        CF_TRY(discard_pending(e));
         e->pipeline = (int)value;
         return CF_OK;
     }
@@ -2022,7 +2120,24 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     }
     if (n == "grad_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "grad_path must be 0, 1 or 2");
+        CF_TRY(discard_pending(e));   // a drawn-ahead batch was counted for the old path (pos_sort)
         e->grad_path = (int)value;
+        return CF_OK;
+    }
+    if (n == "pos_sort" || n == "slot_max_pos") {
+        if (n == "pos_sort" && (value < 0 || value > 2)) return fail(CF_EINVAL, "pos_sort must be 0, 1 or 2");
+        if (n == "slot_max_pos" && (value < 1 || value > 256))
+            return fail(CF_EINVAL, "slot_max_pos must be in [1, 256]");
+        if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+        CF_TRY(discard_pending(e));
+        CF_HIP(hipStreamSynchronize(e->stream));
+        CF_HIP(hipStreamSynchronize(e->side));
+        if (n == "pos_sort") e->pos_sort = (int)value; else e->capP = (int)value;
+        e->slots_ready = false;
+        if (e->Bcap > 0) {
+            CF_TRY(ensure_slots(e));
+            CF_TRY(ensure_order(e, e->Bcap));
+        }
         return CF_OK;
     }
     return fail(CF_EINVAL, "unknown option " + n);

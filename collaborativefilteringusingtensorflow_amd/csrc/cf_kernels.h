@@ -103,6 +103,23 @@ struct StepArgs {
     float* __restrict__ stashU;         // [B, d] each pair's pre-update user row
     float* __restrict__ stashB;         // [B, d] GBPR blend rows
     double* __restrict__ loss_partial;  // [grad grid]
+    // positive-sorted gradient (cf_set_option "pos_sort"; BPR / AMF / CML on
+    // the phased kernel): the draw counts a pair's positive item in cntP
+    // (rankV[p] = its rank among the batch's positives of that item) and its
+    // negatives in cntV; psort orders the pairs by positive item (order), so
+    // the pairs of one gradient block that share a positive item sum its
+    // gradient in LDS and store ONE partial row per (block, item): partial k =
+    // block - offP[i] / kPsortPPB of item i goes to slotP[i * capP + k] (k <
+    // capP) or float atomics into GV.  null cntP = off
+    int32_t* __restrict__ cntP;         // [n_items] positives per item (0 between steps)
+    const int32_t* __restrict__ offP;   // [n_items] exclusive scan of cntP
+    // [B, psort_stride(W)] the pair at each positive-sorted position as one
+    // contiguous record (u, i, j_0 .. j_{W-1}, then the ranks of u, j_0, ..
+    // as 16-bit halves, clamped to 0xFFFF -- a rank only matters below the
+    // slot caps, <= 256), so the gradient launch reads its ids coalesced
+    const int32_t* __restrict__ srec;
+    float* __restrict__ slotP;          // [n_items * capP, d]
+    int capP;
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
     // occU until the exchange recodes it -1 - (its row in xrows / xgrads)
@@ -119,6 +136,12 @@ struct StepArgs {
 // a row of this rank's user table that other ranks' batches touch: its count
 // word carries this flag, so it takes the summed (float-atomic) path
 constexpr int32_t kRemoteFlag = 1 << 24;
+// positive-sorted positions per gradient block (the phased kernel at one pair
+// per 16-lane group): partial k of an item covers the positions of block
+// offP[i] / kPsortPPB + k
+constexpr int kPsortPPB = kGroupsPerBlock;
+// ints per record, int4-aligned: W = 1 -> 4 (16 B), W = 5 -> 12 (48 B)
+__host__ __device__ constexpr int psort_stride(int W) { return (2 + W + (2 + W) / 2 + 3) & ~3; }
 
 struct XchgArgs {
     int n;                        // group occurrences (B * G)
@@ -166,6 +189,12 @@ struct ApplyArgs {
     // between its head and tail slots
     const float* __restrict__ hotP;      // [tiles, d]
     const float* __restrict__ hotPb;     // [tiles] records: the tile's beta sum
+    // positive-sorted gradient (StepArgs): positives are occV[0, nPos)
+    int32_t* __restrict__ cntP;
+    const int32_t* __restrict__ offP;
+    const float* __restrict__ slotP;
+    int capP;
+    int64_t nPos;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -301,6 +330,12 @@ hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
                             hipStream_t s);
+// positive-sorted gradient: offP = exclusive scan of cntP (hipCUB), then
+// order[offP[i_p] + rankV[p]] = p for the B pairs; tmp sized by psort_scratch
+size_t psort_scratch(int64_t n_items);
+hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
+                        int B, int W, const int32_t* cntP, int32_t* offP, int32_t* srec, int64_t n_items,
+                        void* tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
                                 uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,

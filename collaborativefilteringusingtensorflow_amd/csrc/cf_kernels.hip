@@ -457,7 +457,11 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         } else if (gl < nw) {
             j = a.occV[B + p * W + w];
         }
+#ifdef CF_EXP_NORET_ALL   // attribution: every count atomic non-returning, no ranks (wrong results)
+        if (a.count_items && gl < nw) { atomicAdd(&a.cntV[j], 1); a.rankV[B + p * W + w] = 0; }
+#else
         if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
+#endif
     }
     if (MODEL == GBPR) {
         for (int k = gl; k < G; k += PGL) {
@@ -483,13 +487,21 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             a.occU[p] = u;
             a.occV[p] = i;
         }
+#ifdef CF_EXP_NORET_ALL
+        if (a.count_users) { atomicAdd(&a.cntU[u], 1); a.rankU[p] = 0; }
+        if (a.count_items) { atomicAdd(&a.cntV[i], 1); a.rankV[p] = 0; }
+#else
         if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
-#if defined(CF_EXP_NORET)
+#endif
+#if defined(CF_EXP_NORET_ALL)
+#elif defined(CF_EXP_NORET)
         if (a.count_items) { atomicAdd(&a.cntV[i], 1); a.rankV[p] = 0; }
 #elif defined(CF_EXP_NO_ICOUNT)
         if (a.count_items) a.rankV[p] = 0;
 #else
-        if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
+        // pos_sort: the positive's rank among the batch's positives of i (the
+        // negatives count in cntV), the key of psort's counting sort
+        if (a.count_items) a.rankV[p] = atomicAdd(a.cntP != nullptr ? &a.cntP[i] : &a.cntV[i], 1);
 #endif
     }
 }
@@ -1087,6 +1099,7 @@ struct PairRows {
     static constexpr int NG = (MODEL == GBPR) ? 1 : 0;
     static constexpr int NGA = NG > 0 ? NG : 1;
     int p, u, i, cu, ci, ru, ri;
+    int oi;   // pos_sort: offP[i], the item's first positive-sorted position
     int j[WT], cj[WT], rj[WT];
     int g[NGA], cg[NGA], rg[NGA];
     int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
@@ -1096,6 +1109,28 @@ struct PairRows {
     float bi, bj[WT];
     float abi, abj[WT];   // GBPR: bias accumulators of rows seen once
 
+    // pos_sort: the ids of the pair at positive-sorted position pos, from its
+    // contiguous record (coalesced across the wave's groups)
+    __device__ __forceinline__ void load_idx_sorted(const StepArgs& a, int pos) {
+        constexpr int RS = psort_stride(WT);
+        const int4* r = reinterpret_cast<const int4*>(a.srec + (int64_t)pos * RS);
+        int32_t v[RS];
+#pragma unroll
+        for (int k = 0; k < RS / 4; ++k) {
+            const int4 q = r[k];
+            v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+        }
+        u = v[0];
+        i = v[1];
+        p = pos;   // (the pair index itself is not needed on this path)
+        ri = 0;
+        ru = v[2 + WT] & 0xFFFF;
+#pragma unroll
+        for (int w = 0; w < WT; ++w) {
+            j[w] = v[2 + w];
+            rj[w] = (v[2 + WT + (w + 1) / 2] >> (16 * ((w + 1) & 1))) & 0xFFFF;
+        }
+    }
     __device__ __forceinline__ void load_idx(const StepArgs& a, int pair) {
         p = pair;
         u = a.occU[p];
@@ -1113,11 +1148,19 @@ struct PairRows {
             rg[k] = a.count_users ? a.rankU[a.B + p + k] : 0;
         }
     }
+    template <bool SORT = false>
     __device__ __forceinline__ void load_rows(const StepArgs& a, int gl) {
         cu = a.count_users ? a.cntU[u] : 0;
-        ci = a.count_items ? a.cntV[i] : 0;
+        if constexpr (SORT) {   // an item's count = its positives (cntP) + its negatives (cntV)
+            ci = a.cntV[i] + a.cntP[i];
+            oi = a.offP[i];
 #pragma unroll
-        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+            for (int w = 0; w < WT; ++w) cj[w] = a.cntV[j[w]] + a.cntP[j[w]];
+        } else {
+            ci = a.count_items ? a.cntV[i] : 0;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+        }
 #pragma unroll
         for (int k = 0; k < NG; ++k) cg[k] = (a.count_users && g[k] >= 0) ? a.cntU[g[k]] : 0;
         gload<EPL>(a.U, u, a.d, gl, uu);
@@ -1154,7 +1197,12 @@ struct PairRows {
         }
     }
 
-    __device__ __forceinline__ void update(const StepArgs& a, int gl, float& loss_g, float& sq) {
+    // SORT: the positive item's gradient row goes to the group's LDS row
+    // srow (summed over the block's run of pairs sharing the item by
+    // psort_head) instead of being finished here
+    template <bool SORT = false>
+    __device__ __forceinline__ void update(const StepArgs& a, int gl, float& loss_g, float& sq,
+                                           float* srow = nullptr) {
         const int d = a.d;
         if (a.recV != nullptr) {   // item records' X: only pairs that leave one
             bool need = MODEL != GBPR && ci >= 2 && si >= 0;
@@ -1201,7 +1249,12 @@ struct PairRows {
                 sq = fmaf(vi[s], vi[s], sq);
             }
             gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            ifinish_pre<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, vi, ai, gi);
+            if constexpr (SORT) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) srow[s * kGL + gl] = gi[s];
+            } else {
+                ifinish_pre<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, vi, ai, gi);
+            }
         } else if (MODEL == GBPR) {  // G == 1
             const float ui_u = gdot<EPL>(uu, vi);
 #pragma unroll
@@ -1305,14 +1358,50 @@ struct PairRows {
                 }
             }
             gfinish_pre<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, au, gu, a);
-            ifinish_pre<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), 0, gl, vi, ai, gi);
+            if constexpr (SORT) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) srow[s * kGL + gl] = gi[s];
+            } else {
+                ifinish_pre<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), 0, gl, vi, ai, gi);
+            }
         }
     }
 };
 
-template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock>
+// pos_sort: the first group of a run of the block's pairs that share the
+// positive item i sums the run's gradient rows (LDS, in position order) and
+// finishes the item once for the whole run: Adagrad now if the run is the
+// item's only occurrence in the batch, else the block's partial row -> slot
+// (partial k = block - offP[i] / kPsortPPB) or, past capP, float atomics
+template <int MODEL, int EPL, int WT, int GPB>
+__device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MODEL, EPL, WT>& r, int block,
+                                           int grp, int gl, const float (*s_gi)[kGL * EPL],
+                                           const int* s_item) {
+    float g[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) g[s] = s_gi[grp][s * kGL + gl];
+    for (int q = grp + 1; q < GPB && s_item[q] == r.i; ++q) {
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] += s_gi[q][s * kGL + gl];
+    }
+    if (r.ci == 1) {
+        gapply_pre<EPL>(a.V, a.AV, r.i, a.d, gl, r.vi, r.ai, g, a.lr, a.clip != 0, a.clip_norm);
+        if (gl == 0) a.cntP[r.i] = 0;
+    } else {
+        const int k = block - r.oi / kPsortPPB;
+        if (k < a.capP)
+            gstore<EPL>(a.slotP, (int64_t)r.i * a.capP + k, a.d, gl, g);
+        else
+            gatomic<EPL>(a.GV, r.i, a.d, gl, g);
+    }
+}
+
+template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock, bool SORT = false>
 __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
+    static_assert(!SORT || (P == 1 && MODEL != GBPR && GPB == kPsortPPB), "pos_sort: one pair per group");
     __shared__ double s_loss[GPB];
+    __shared__ float s_gi[SORT ? GPB : 1][SORT ? kGL * EPL : 1];
+    __shared__ int s_item[SORT ? GPB : 1];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
     float loss_g = 0.f;
@@ -1327,16 +1416,27 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     }
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        if (ok[k]) pr[k].load_idx(a, pp[k]);
+        if (ok[k]) {
+            if constexpr (SORT)
+                pr[k].load_idx_sorted(a, pp[k]);   // pp = positive-sorted position
+            else
+                pr[k].load_idx(a, pp[k]);
+        }
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        if (ok[k]) pr[k].load_rows(a, gl);
+        if (ok[k]) pr[k].template load_rows<SORT>(a, gl);
 #pragma unroll
     for (int k = 0; k < P; ++k)
         if (ok[k]) pr[k].load_acc(a, gl);
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        if (ok[k]) pr[k].update(a, gl, loss_g, sq);
+        if (ok[k]) pr[k].template update<SORT>(a, gl, loss_g, sq, SORT ? &s_gi[grp][0] : nullptr);
+    if constexpr (SORT) {
+        if (gl == 0) s_item[grp] = ok[0] ? pr[0].i : -1;
+        __syncthreads();
+        if (ok[0] && (grp == 0 || s_item[grp - 1] != pr[0].i))
+            psort_head<MODEL, EPL, WT, GPB>(a, pr[0], block, grp, gl, s_gi, s_item);
+    }
 
     const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
     const float sq_g = gsum(sq);
@@ -1350,7 +1450,7 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     }
 }
 
-template <int MODEL, int EPL, int WT, int P, bool DRAW>
+template <int MODEL, int EPL, int WT, int P, bool DRAW, bool SORT = false>
 #ifdef CF_GRAD_WAVES_PER_EU
 #define CF_GRAD_ATTR __attribute__((amdgpu_waves_per_eu(CF_GRAD_WAVES_PER_EU, 8)))
 #else
@@ -1361,7 +1461,7 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
     if (DRAW && minor_block(blockIdx.x, ng, np, idx))
         prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
     else
-        grad_fast_body<MODEL, EPL, WT, P>(a, idx);
+        grad_fast_body<MODEL, EPL, WT, P, kGroupsPerBlock, SORT>(a, idx);
 }
 
 // the same gradient blocks at one wave per workgroup (no draw blocks): a
@@ -1530,6 +1630,53 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
     }
 }
 
+// pos_sort: a duplicated item row's gradient = its negatives' slot rows
+// (rank order) + its positive partials (block order) + the float-atomic sum
+// of what overflowed either range; Adagrad; both counts reset
+template <int EPL>
+__device__ __forceinline__ void rows_sum(const float* __restrict__ S, int64_t s0, int n, int d, int gl,
+                                         float (&g)[EPL]) {
+    constexpr int NF = CF_APPLY_NF;
+    for (int t0 = 0; t0 < n; t0 += NF) {
+        float h[NF][EPL];
+#pragma unroll
+        for (int q = 0; q < NF; ++q)
+            if (t0 + q < n) gload<EPL>(S, s0 + t0 + q, d, gl, h[q]);
+#pragma unroll
+        for (int q = 0; q < NF; ++q)
+            if (t0 + q < n) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+            }
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int gl) {
+    float x[EPL], acc[EPL], g[EPL];
+    gload<EPL>(a.V, r, a.d, gl, x);
+    gload_acc<EPL>(a.AV, r, a.d, gl, true, acc);
+    const int cn = a.cntV[r], cp = a.cntP[r];
+    const int o = a.offP[r];
+    const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) g[s] = 0.f;
+    rows_sum<EPL>(a.slotV, r * (int64_t)a.capV, cn < a.capV ? cn : a.capV, a.d, gl, g);
+    rows_sum<EPL>(a.slotP, r * (int64_t)a.capP, np < a.capP ? np : a.capP, a.d, gl, g);
+    if (cn > a.capV || np > a.capP) {
+        float h[EPL];
+        gload<EPL>(a.GV, r, a.d, gl, h);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] += h[s];
+        row_zero<EPL>(a.GV + r * a.d, a.d, gl);
+    }
+    gapply_pre<EPL>(a.V, a.AV, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
+    if (gl == 0) {
+        a.cntV[r] = 0;
+        a.cntP[r] = 0;
+    }
+}
+
 // Deterministic mode: one block per 64-position tile of the sorted occurrence
 // list.  A tile whose first and last positions hold the same row lies inside
 // that row: its 16 groups sum four slots each (rows, or item records over the
@@ -1617,7 +1764,7 @@ constexpr int kApplyDetectWaves = CF_APPLY_DETECT_WAVES;
 constexpr int kApplyChunk = CF_APPLY_CHUNK;
 
 // BS = workgroup size (256, or 64 for one-wave apply blocks)
-template <int EPL, int BS = kBlock, bool HOT = false>
+template <int EPL, int BS = kBlock, bool HOT = false, bool PS = false>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     constexpr int NWV = BS / kWave, NGR = BS / kGL;
     __shared__ double s_red[NWV];
@@ -1676,8 +1823,16 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 const int64_t k = q - nU;
                 if (a.rankV[k] == 0) {
                     const int32_t r = a.occV[k];
-                    c = a.cntV[r];
-                    if (c >= 2) row = r;
+                    if constexpr (PS) {
+                        // owner: the rank-0 negative, or the rank-0 positive
+                        // of an item drawn as no pair's negative
+                        const int cn = a.cntV[r], cp = a.cntP[r];
+                        c = cn + cp;
+                        if (c >= 2 && (k >= a.nPos || cn == 0)) row = r;
+                    } else {
+                        c = a.cntV[r];
+                        if (c >= 2) row = r;
+                    }
                 }
             } else if (q < total) {
                 const int64_t k = q - nU - nV;
@@ -1709,15 +1864,18 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 rem -= c;
             }
             if (src < 0) break;  // group-uniform
-            apply_row<EPL, HOT>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
+            if (PS && s_isU[src] == 0)
+                apply_item_ps<EPL>(a, s_row[src], gl);
+            else
+                apply_row<EPL, HOT>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
         }
         __syncthreads();  // s_* reused by the next chunk
     }
 }
 
-template <int EPL, bool HOT>
+template <int EPL, bool HOT, bool PS = false>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
-    apply_body<EPL, kBlock, HOT>(a, blockIdx.x, gridDim.x);
+    apply_body<EPL, kBlock, HOT, PS>(a, blockIdx.x, gridDim.x);
 }
 
 // one-wave apply blocks: the detecting wave's own four groups apply its owners
@@ -1729,7 +1887,7 @@ __global__ __launch_bounds__(kWave) void apply_wave_kernel(ApplyArgs a) {
 // horizontal fusion on the device-sampler path: apply of step s (blocks
 // [0, napply)) beside the draw + count of step s+1 (the rest) -- independent
 // work (other buffer set), one launch instead of two
-template <int EPL, int MODEL, bool HOT>
+template <int EPL, int MODEL, bool HOT, bool PS = false>
 #ifndef CF_APPLY_PREP_ORDER
 #define CF_APPLY_PREP_ORDER 0  // 0: apply blocks first, 1: draw blocks first, 2: interleaved
 #endif
@@ -1750,7 +1908,7 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
         apply_body<EPL, kBlock, HOT>(p, blockIdx.x - nprep, napply);
 #else
     if ((int)blockIdx.x < napply)
-        apply_body<EPL, kBlock, HOT>(p, blockIdx.x, napply);
+        apply_body<EPL, kBlock, HOT, PS>(p, blockIdx.x, napply);
     else
         prep_any<MODEL>(a, blockIdx.x - napply);
 #endif
@@ -2099,6 +2257,19 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
     const int ng = (a.B + P * kGroupsPerBlock - 1) / (P * kGroupsPerBlock), np = prep_blocks(nx);
     const StepArgs n = nx ? *nx : a;
     const dim3 grid(ng + np), block(kBlock);
+    if constexpr (MODEL != GBPR && P == 1) {
+        if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
+            if (np > 0) return hipErrorInvalidValue;
+            switch (epl_for(a.d)) {
+                case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
+                case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
+                case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
+                default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
+            }
+            return hipGetLastError();
+        }
+    }
+    if (a.srec != nullptr) return hipErrorInvalidValue;
     if (np > 0) {
         switch (epl_for(a.d)) {
             case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
@@ -2141,6 +2312,7 @@ static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
     if (a.B <= 0) return next ? launch_prep(*next, s) : hipSuccess;
     if (next && next->model != a.model) return hipErrorInvalidValue;
+    if (a.srec != nullptr && fast_w(a) == 0) return hipErrorInvalidValue;   // pos_sort: phased kernel only
     switch (a.model) {
         case BPR: return launch_grad_m<BPR>(a, next, s);
         case GBPR: return launch_grad_m<GBPR>(a, next, s);
@@ -2165,15 +2337,15 @@ static int apply_grid(const ApplyArgs& a) {
 #define CF_APPLY_WAVE_BLOCKS 0
 #endif
 
-template <bool HOT>
+template <bool HOT, bool PS = false>
 static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
     const dim3 grid(apply_grid(a)), block(kBlock);
     switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((apply_kernel<1, HOT>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((apply_kernel<2, HOT>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((apply_kernel<4, HOT>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((apply_kernel<8, HOT>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((apply_kernel<16, HOT>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((apply_kernel<1, HOT, PS>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((apply_kernel<2, HOT, PS>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((apply_kernel<4, HOT, PS>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((apply_kernel<8, HOT, PS>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((apply_kernel<16, HOT, PS>), grid, block, 0, s, a); break;
     }
     return hipGetLastError();
 }
@@ -2190,26 +2362,30 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
         }
         return hipGetLastError();
     }
+    if (a.cntP != nullptr) return a.hotP != nullptr ? hipErrorInvalidValue : launch_apply_h<false, true>(a, s);
     return a.hotP != nullptr ? launch_apply_h<true>(a, s) : launch_apply_h<false>(a, s);
 }
 
-template <int MODEL, bool HOT>
+template <int MODEL, bool HOT, bool PS = false>
 static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     const int na = apply_grid(p);
     const int np = prep_blocks(&a);
     const dim3 grid(na + np), block(kBlock);
     switch (epl_for(p.d)) {
-        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
-        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
-        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
-        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
-        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
+        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
+        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
+        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
+        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
     }
     return hipGetLastError();
 }
 
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return launch_apply(p, s);
+    if (p.cntP != nullptr)   // pos_sort: BPR / AMF / CML (their draw is prep_body<BPR>)
+        return (p.hotP != nullptr || a.model == GBPR) ? hipErrorInvalidValue
+                                                      : launch_apply_prep_m<BPR, false, true>(p, a, s);
     if (p.hotP != nullptr)
         return a.model == GBPR ? launch_apply_prep_m<GBPR, true>(p, a, s) : launch_apply_prep_m<BPR, true>(p, a, s);
     return a.model == GBPR ? launch_apply_prep_m<GBPR, false>(p, a, s) : launch_apply_prep_m<BPR, false>(p, a, s);

@@ -88,7 +88,9 @@ enum cf_kernel_id {
     CF_K_APPLY_SLOT = 10,/* (retired pipeline 2)                               */
     CF_K_ITEM_REDUCE = 11,/* multi-rank: duplicated item rows' summed gradient
                             into the bound buffer, before the all-reduce    */
-    CF_K_COUNT = 12
+    CF_K_PSORT = 12,     /* pos_sort: scan of the positive counts + scatter of
+                            the pairs into positive-item order               */
+    CF_K_COUNT = 13
 };
 
 /*
@@ -409,6 +411,21 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                exchange is excluded); 0 = the fast path (default), whose
  *                rank order -- and so the last bits of duplicate sums --
  *                follows the order the count atomics land.
+ *   "pos_sort"   1 = the gradient launch visits the batch's pairs in
+ *                positive-item order (a counting sort by the draw's positive
+ *                counts, two short launches before it), so the pairs of one
+ *                gradient block that share a positive item sum that item's
+ *                gradient in LDS and store one partial row per block instead
+ *                of one slot row (or float atomics) per occurrence; the apply
+ *                adds the partials to the negatives' slot rows.  BPR / AMF /
+ *                CML on the phased kernel (W in {1, 5}, d <= 128), not with
+ *                deterministic, item_slots 1, hot_replicas > 1, pipeline 2 or
+ *                a dense item apply (the option is ignored there).  Same
+ *                results up to fp32 summation order.  0 = off; 2 = auto
+ *                (default): on for batches of >= 2^18 pairs (cfg2: 7 %
+ *                faster steps at 2^19, 3.5 % at 2^18, even at 2^17).
+ *   "slot_max_pos" positive partial rows per item row under pos_sort (default
+ *                8; later partials of a hot item add with float atomics).
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
  *                item occurrences are counted like user ones, a row seen
  *                once stores its gradient row into the bound buffer, a

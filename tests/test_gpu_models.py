@@ -204,6 +204,58 @@ def test_fold_parallel_driver_replicas(fold1, tmp_path):
     assert np.all(stds <= 0.03), stds
 
 
+def test_fold_parallel_replicas_match_oracle(fold1, tmp_path):
+    """Each spawned replica of run_folds(parallel=True) against the oracle:
+    three folds (copies of ml-100k fold 1 written as text) train
+    concurrently in spawned processes with the deterministic cfg1 worker
+    (reference sampler stream for seed 11, seeded init); every replica's five
+    ranking metrics must equal the oracle's committed cfg1 metrics
+    (tests/golden/cfg1_oracle_metrics.json) within the north star's 0.2 %,
+    and the replicas must agree with each other (testbprmf.py:113-125)."""
+    from collaborativefilteringusingtensorflow_amd.drivers._common import run_folds
+    from _replica_worker import cfg1_config, seeded_worker
+    folds = 3
+    for fold in range(1, folds + 1):
+        for tag in ("train", "test"):
+            ip, ix = fold1[tag + "_indptr"], fold1[tag + "_indices"]
+            name = "ratings__%d_%s.txt" % (fold, "tra" if tag == "train" else "tst")
+            with open(tmp_path / name, "w") as f:
+                for u in range(943):
+                    for it in ix[ip[u]:ip[u + 1]]:
+                        f.write("%d\t%d\t4.0\n" % (u, it))
+    g = cfg1_config()
+    ref = np.array([g["metrics"][m] for m in g["config"]["metrics"]])
+    import multiprocessing
+    ctx = multiprocessing.get_context("spawn")
+    # run_folds collects the replicas' score vectors through its queue; call
+    # the entry the same way so the per-replica scores are visible here
+    q = ctx.Queue()
+    from collaborativefilteringusingtensorflow_amd.drivers._common import _fold_entry
+    procs = [ctx.Process(target=_fold_entry, args=(seeded_worker, f, 0, 943, 1682,
+                                                   str(tmp_path) + "/", q)) for f in range(folds)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(folds):
+        f, sc, err = q.get(timeout=100)
+        assert err is None, (f, err)
+        got[f] = np.array(sc)
+    for p in procs:
+        p.join()
+    for f in range(folds):
+        rel = np.abs(got[f] - ref) / np.abs(ref)
+        print("replica", f, got[f], "max rel vs oracle", rel.max())
+        assert np.all(rel <= 2e-3), (f, got[f], ref)
+        # same data and stream: the replicas differ only by the order of the
+        # hot rows' float atomics (fast path), far inside the tolerance
+        assert np.all(np.abs(got[f] - got[0]) <= 1e-3 * np.abs(ref)), (got[f], got[0])
+    # and the driver's own ave@N / std@N path over the same replicas
+    aves, stds = run_folds(seeded_worker, 943, 1682, str(tmp_path) + "/", folds, 10,
+                           g["config"]["metrics"], parallel=True)
+    assert np.all(np.abs(aves - ref) <= 2e-3 * np.abs(ref)), (aves, ref)
+    assert np.all(stds <= 1e-3 * np.abs(ref)), stds
+
+
 @pytest.mark.parametrize("name", ["prigp", "cplr"])
 def test_tuple_models_train(fold1, name):
     """PRIGP / CPLR drop-ins (prigp.py:172-228, cplr_u.py:179-291): similarity

@@ -1,0 +1,237 @@
+"""GPU parity of the positive-sorted gradient (cf_set_option "pos_sort").
+
+The draw counts each pair's positive item apart from the negatives, psort
+orders the pairs by positive item, and the gradient launch sums the pairs of
+one block that share a positive item in LDS: one partial row per (block,
+item) instead of one slot row (or float atomics) per occurrence.  The step is
+still TF1's dedup-sum + SparseApplyAdagrad (bprmf.py:74-88), so every case is
+checked against the float64 oracle at the north star's 1e-5 (max-relative per
+table and per-step loss) on the reference's captured batches, plus hot items
+whose partials overflow their slot range, items seen only as positives, and
+the device-sampled pipeline (draw fused into the apply launch).
+"""
+import numpy as np
+import pytest
+
+from conftest import get_stream
+from oracle import cf_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def make(model, fold1, d, W, opts, **kw):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, seed=7, **kw)
+    e.set_option("item_slots", 0)
+    for k, v in opts.items():
+        e.set_option(k, v)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    return e
+
+
+def tables(fold1, d, seed, truncated=True):
+    rng = np.random.RandomState(seed)
+    U = O.init_table(rng, (int(fold1["n_users"]), d), truncated=truncated)
+    V = O.init_table(rng, (int(fold1["n_items"]), d), truncated=truncated)
+    return U, V
+
+
+def psort_launches(e):
+    return e.profile_read("psort")[1]
+
+
+def run_steps(model, fold1, batches, d, opts, amf_switch=None, **kw):
+    W = batches[0][1].shape[1]
+    U, V = tables(fold1, d, 3, truncated=(model != "cml"))
+    e = make(model, fold1, d, W, opts, **kw)
+    e.set_table("user", U)
+    e.set_table("item", V)
+    e.profile_reset()
+    e.profile(True)
+    U64, V64 = U.astype(np.float64), V.astype(np.float64)
+    AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
+    adv = False
+    for s, (pairs, negs) in enumerate(batches):
+        if amf_switch is not None and s == amf_switch:
+            e.begin_phase(1)
+            adv = True
+            AU[...] = 0.1
+            AV[...] = 0.1
+        lg = e.step(pairs, negs)
+        if model == "bpr":
+            lo = O.bpr_step(U64, V64, AU, AV, pairs, negs, kw["reg"])
+        elif model == "amf":
+            lo = O.amf_step(U64, V64, AU, AV, pairs, negs, kw["reg"], adv, reg_adv=kw.get("reg_adv", 1.0))
+        else:
+            lo = O.cml_step(U64, V64, AU, AV, pairs, negs, kw["margin"], kw["reg_cov"], kw["clip_norm"],
+                            use_rank_weight=kw["use_rank_weight"])
+        assert abs(lg - lo) <= RTOL * abs(lo) + 1e-6, (s, lg, lo)
+    e.profile(False)
+    n_ps = psort_launches(e)
+    for t, o in (("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV)):
+        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+    e.close()
+    return n_ps
+
+
+def stream_batches(streams, name, K):
+    st = get_stream(streams, name)
+    return [(st["pairs"][s], st["negs"][s]) for s in range(K)]
+
+
+@pytest.mark.parametrize("cap", [1, 8])
+@pytest.mark.parametrize("name,d,reg", [("rank_b100_w1", 32, 0.1), ("rank_b100_w5", 64, 0.05),
+                                        ("uij_b100", 16, 0.02)])
+def test_bpr_pos_sort_matches_oracle(fold1, streams, name, d, reg, cap):
+    n = run_steps("bpr", fold1, stream_batches(streams, name, 40), d,
+                  {"pos_sort": 1, "slot_max_pos": cap}, reg=reg)
+    assert n == 40   # the sorted kernel ran every step
+
+
+def test_amf_pos_sort_across_phase_switch(fold1, streams):
+    n = run_steps("amf", fold1, stream_batches(streams, "rank_b100_w5", 40), 128,
+                  {"pos_sort": 1}, amf_switch=20, reg=0.05, reg_adv=1.0)
+    assert n == 40
+
+
+def test_cml_pos_sort_phased(fold1, streams):
+    """CML at W=5 on the phased kernel (grad_path 2; auto keeps the generic
+    one, where pos_sort does not apply) with the clip in every update."""
+    n = run_steps("cml", fold1, stream_batches(streams, "rank_b50_w5", 40), 50,
+                  {"pos_sort": 1, "grad_path": 2}, margin=1.0, reg_cov=1.0, clip_norm=1.0,
+                  use_rank_weight=True)
+    assert n == 40
+
+
+def test_pos_sort_inactive_paths_unchanged(fold1, streams):
+    """Where pos_sort does not apply (generic kernel, CML auto at W=5) the
+    option is ignored and the step is the plain one."""
+    n = run_steps("bpr", fold1, stream_batches(streams, "rank_b100_w1", 10), 32,
+                  {"pos_sort": 1, "grad_path": 1}, reg=0.1)
+    assert n == 0
+    n = run_steps("cml", fold1, stream_batches(streams, "rank_b50_w5", 10), 50,
+                  {"pos_sort": 1}, margin=1.0, reg_cov=1.0, clip_norm=1.0, use_rank_weight=True)
+    assert n == 0
+
+
+def hot_batch(fold1, rng, n_pos, n_neg_hot, hot=49, B=900):
+    """Item `hot` as the positive of the first n_pos pairs (users who rated
+    it) and the negative of n_neg_hot more; other pairs ordinary."""
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    raters = [u for u in range(943) if hot in set(ix[ip[u]:ip[u + 1]].tolist())]
+    pairs, negs = [], []
+    for r in range(B):
+        if r < n_pos:
+            u = raters[rng.randint(len(raters))]
+            row = set(ix[ip[u]:ip[u + 1]].tolist())
+            pairs.append([u, hot])
+        else:
+            u = int(rng.randint(943))
+            while ip[u + 1] == ip[u] or hot in set(ix[ip[u]:ip[u + 1]].tolist()):
+                u = int(rng.randint(943))
+            row = set(ix[ip[u]:ip[u + 1]].tolist())
+            pairs.append([u, int(ix[ip[u] + rng.randint(ip[u + 1] - ip[u])])])
+        if n_pos <= r < n_pos + n_neg_hot:
+            negs.append([hot])
+        else:
+            negs.append([next(int(x) for x in rng.randint(0, 1682, 64) if x not in row and x != hot)])
+    return np.array(pairs, np.int32), np.array(negs, np.int32)
+
+
+@pytest.mark.parametrize("cap,slot_max", [(1, 3), (8, 32), (64, 32)])
+@pytest.mark.parametrize("n_pos,n_neg_hot", [(600, 300), (600, 0), (5, 0)])
+def test_pos_sort_hot_item(fold1, cap, slot_max, n_pos, n_neg_hot):
+    """A hot positive spanning ~38 gradient blocks: partials 0..cap-1 in
+    slots, the rest float atomics; with n_neg_hot 0 the item is no pair's
+    negative, so its rank-0 positive owns the apply."""
+    rng = np.random.RandomState(n_pos + n_neg_hot + cap)
+    batches = [hot_batch(fold1, rng, n_pos, n_neg_hot) for _ in range(3)]
+    n = run_steps("bpr", fold1, batches, 16, {"pos_sort": 1, "slot_max_pos": cap, "slot_max": slot_max},
+                  reg=0.02)
+    assert n == 3
+
+
+def test_pos_sort_device_pipeline_equals_plain(fold1):
+    """cf_train_steps (device draw fused into the apply launch, the psort
+    launches between) trains the same model as the plain path from the same
+    state and sampler seed: same batches, sums equal up to fp32 order."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    out = []
+    for ps in (0, 1):
+        e = Engine("bpr", 943, 1682, 64, n_neg=1, reg=0.05, seed=21)
+        e.set_option("item_slots", 0)
+        e.set_option("pos_sort", ps)
+        e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+        e.init_params(0.0, 0.1, truncated=True, seed=1)
+        e.profile_reset()
+        e.profile(True)
+        loss = e.train_steps(2048, 30)
+        e.profile(False)
+        out.append((loss, e.get_table("user"), e.get_table("item"), e.get_table("acc_item"),
+                    psort_launches(e)))
+        e.close()
+    (l0, U0, V0, A0, n0), (l1, U1, V1, A1, n1) = out
+    assert n0 == 0 and n1 == 30
+    assert abs(l1 - l0) <= 1e-5 * abs(l0)
+    for a, b in ((U1, U0), (V1, V0), (A1, A0)):
+        assert rel(a, b) <= 1e-5, rel(a, b)
+
+
+def test_pos_sort_device_pipeline_matches_oracle(fold1):
+    """The same path against the oracle replaying the engine's own draws."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    d, reg, B = 32, 0.05, 1024
+    e = Engine("bpr", 943, 1682, d, n_neg=1, reg=reg, seed=33)
+    e.set_option("pos_sort", 1)
+    e.set_option("item_slots", 0)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    U, V = tables(fold1, d, 5)
+    e.set_table("user", U)
+    e.set_table("item", V)
+    # the sampler stream: draw K batches, rewind, train the same K on the device
+    st = e.sampler_state()
+    batches = [e.sample(B)[:2] for _ in range(12)]
+    e.set_sampler_state(*st)
+    e.train_steps(B, 12)
+    U64, V64 = U.astype(np.float64), V.astype(np.float64)
+    AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
+    for pairs, negs in batches:
+        O.bpr_step(U64, V64, AU, AV, pairs, negs, reg)
+    for t, o in (("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV)):
+        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+    e.close()
+
+
+def test_pos_sort_auto_by_batch_size():
+    """Default (auto): on from 2^18 pairs per step, off below; the auto path
+    trains the same model as pos_sort 0 on a synthetic Zipf graph."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+    nu, ni, d = 60_000, 8_000, 64
+    ip, ix = synth_graph(nu, ni, 30.0, 0.8, 7, n_threads=8)
+    out = []
+    for ps in (None, 0):
+        e = Engine("bpr", nu, ni, d, n_neg=1, reg=0.02, seed=3)
+        if ps is not None:
+            e.set_option("pos_sort", ps)
+        e.set_interactions(ip, ix)
+        e.init_params(0.0, 0.1, truncated=True, seed=1)
+        e.profile_reset()
+        e.profile(True)
+        e.train_steps(1 << 16, 2)          # below the auto threshold
+        n_small = psort_launches(e)
+        loss = e.train_steps(1 << 18, 3)
+        e.profile(False)
+        out.append((loss, e.get_table("user"), e.get_table("item"), psort_launches(e) - n_small, n_small))
+        e.close()
+    (l_auto, U_a, V_a, n_auto, s_auto), (l_off, U_o, V_o, n_off, s_off) = out
+    assert s_auto == 0 and s_off == 0 and n_off == 0 and n_auto == 3
+    assert abs(l_auto - l_off) <= 1e-5 * abs(l_off)
+    assert rel(U_a, U_o) <= 1e-5 and rel(V_a, V_o) <= 1e-5

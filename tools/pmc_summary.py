@@ -22,7 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"grad_fast_kernel": "step", "grad_kernel": "step", "apply_prep_kernel": "apply_prep",
          "prep_kernel": "sample", "slot_kernel": "slot", "apply_kernel": "apply",
          "apply_dense_kernel": "apply_dense", "clip_full_kernel": "clip",
-         "fused_topk_kernel": "fused_topk", "score_kernel": "score", "topk_kernel": "topk"}
+         "fused_topk_kernel": "fused_topk", "score_kernel": "score", "topk_kernel": "topk",
+         "psort_scatter_kernel": "psort_scatter", "psort_scan_kernel": "psort_scan",
+         "scan_impl": "psort_scan", "init_lookback_scan_state": "psort_scan_init"}
 
 
 def short(name):
