@@ -282,7 +282,8 @@ constexpr int kPsortAutoB = 1 << 18;
 // allocated only then)
 bool psort_possible(const cf_engine* e) {
     const cf_config& c = e->cfg;
-    if (!e->pos_sort || c.dense_item_apply || e->item_recs) return false;
+    if (!e->pos_sort || e->item_recs) return false;
+    if (c.dense_item_apply && e->item_reduce != 1) return false;   // the multi-rank item reduce: slot rows only
     if (c.model != CF_BPR && c.model != CF_AMF && c.model != CF_CML) return false;
     return c.n_factors <= 128 && (c.n_neg == 1 || c.n_neg == 5);
 }
@@ -1507,6 +1508,7 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
         CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
     }
     CF_TRY(det_ranks(e, a));
+    CF_TRY(psort(e, a));
     {
         ProfScope ps(e, CF_K_STEP);
         CF_HIP(launch_grad(a, e->stream));

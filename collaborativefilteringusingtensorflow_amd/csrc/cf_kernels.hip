@@ -1385,7 +1385,10 @@ __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MOD
         for (int s = 0; s < EPL; ++s) g[s] += s_gi[q][s * kGL + gl];
     }
     if (r.ci == 1) {
-        gapply_pre<EPL>(a.V, a.AV, r.i, a.d, gl, r.vi, r.ai, g, a.lr, a.clip != 0, a.clip_norm);
+        if (a.items_grad_only)   // multi-rank item reduce: the sole writer of the zeroed dense row
+            gstore<EPL>(a.GV, r.i, a.d, gl, g);
+        else
+            gapply_pre<EPL>(a.V, a.AV, r.i, a.d, gl, r.vi, r.ai, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) a.cntP[r.i] = 0;
     } else {
         const int k = block - r.oi / kPsortPPB;
@@ -1653,9 +1656,13 @@ __device__ __forceinline__ void rows_sum(const float* __restrict__ S, int64_t s0
 
 template <int EPL>
 __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int gl) {
+    // multi-rank item reduce: the summed row goes to GV for the exchange
+    const bool reduce_only = a.items_grad_only;
     float x[EPL], acc[EPL], g[EPL];
-    gload<EPL>(a.V, r, a.d, gl, x);
-    gload_acc<EPL>(a.AV, r, a.d, gl, true, acc);
+    if (!reduce_only) {
+        gload<EPL>(a.V, r, a.d, gl, x);
+        gload_acc<EPL>(a.AV, r, a.d, gl, true, acc);
+    }
     const int cn = a.cntV[r], cp = a.cntP[r];
     const int o = a.offP[r];
     const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
@@ -1668,9 +1675,12 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
         gload<EPL>(a.GV, r, a.d, gl, h);
 #pragma unroll
         for (int s = 0; s < EPL; ++s) g[s] += h[s];
-        row_zero<EPL>(a.GV + r * a.d, a.d, gl);
+        if (!reduce_only) row_zero<EPL>(a.GV + r * a.d, a.d, gl);
     }
-    gapply_pre<EPL>(a.V, a.AV, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
+    if (reduce_only)
+        row_st<EPL>(a.GV + r * (int64_t)a.d, a.d, gl, g);
+    else
+        gapply_pre<EPL>(a.V, a.AV, r, a.d, gl, x, acc, g, a.lr, a.clip != 0, a.clip_norm);
     if (gl == 0) {
         a.cntV[r] = 0;
         a.cntP[r] = 0;

@@ -27,7 +27,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q, exchange="allreduce",
-            backend="gloo", item_slots=0):
+            backend="gloo", item_slots=0, opts=None):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -50,6 +50,8 @@ def _worker(rank, world, port, fold, batches, U0, V0, model, item_reduce, q, exc
                seed=10 + rank, **kw)
     e.set_option("item_reduce", item_reduce)
     e.set_option("item_slots", item_slots)
+    for k, v in (opts or {}).items():
+        e.set_option(k, v)
     e.set_interactions(lip, lix)
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
@@ -91,7 +93,7 @@ def _check_elementwise(got, ref, rtol=1e-5, atol=1e-6):
     assert not bad.any(), (int(bad.sum()), float(err.max()))
 
 
-@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+@pytest.mark.parametrize("item_slots", [0, 1, 2], ids=["rows", "records", "rows-pos-sort"])
 @pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
 @pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
 def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange, item_slots):
@@ -106,8 +108,12 @@ def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange, ite
     batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s]) for s in range(8)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
+    # rows-pos-sort: slot rows + positive-sorted gradients (the item reduce sums
+    # the positive partials; CML forced onto the phased kernel where it applies)
+    opts = {"pos_sort": 1, "grad_path": 2} if item_slots == 2 else {"pos_sort": 0}
     p = ctx.Process(target=_worker, args=(0, 1, _free_port(), fold1, batches, U0, V0, model, 1, q,
-                                          exchange, "nccl", item_slots))
+                                          exchange, "nccl", min(item_slots, 1) if item_slots < 2 else 0,
+                                          opts))
     p.start()
     rank, u0, u1, Ul, Vr, AVr = q.get(timeout=300)
     p.join(timeout=120)
@@ -119,12 +125,14 @@ def test_one_rank_rccl_sharded_step(fold1, streams, model, stream, exchange, ite
     _check_elementwise(AVr, AV, **tol)
 
 
-@pytest.mark.parametrize("item_reduce,exchange", [(1, "allreduce"), (2, "allreduce"), (0, "allreduce"),
-                                                  (1, "rs_ag")],
-                         ids=["reduce", "store-singletons", "atomic", "reduce-scatter"])
+@pytest.mark.parametrize("item_reduce,exchange,psort", [(1, "allreduce", 0), (2, "allreduce", 0),
+                                                        (0, "allreduce", 0), (1, "rs_ag", 0),
+                                                        (1, "allreduce", 1), (1, "rs_ag", 1)],
+                         ids=["reduce", "store-singletons", "atomic", "reduce-scatter", "reduce-pos-sort",
+                              "reduce-scatter-pos-sort"])
 @pytest.mark.parametrize("model,stream", [("bpr", "rank_b100_w5"), ("cml", "rank_b50_w5")])
 def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, stream, item_reduce,
-                                                    exchange):
+                                                    exchange, psort):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(8)
     d = 24
@@ -134,8 +142,9 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    opts = {"pos_sort": 1, "grad_path": 2} if psort else {"pos_sort": 0}
     procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, model, item_reduce, q,
-                                               exchange))
+                                               exchange, "gloo", 0, opts))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -154,7 +163,7 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
     assert np.array_equal(res[0][4], res[1][4])   # replicas bit-identical
 
 
-def _draw_ahead_worker(port, fold, q, exchange="allreduce"):
+def _draw_ahead_worker(port, fold, q, exchange="allreduce", W=2, opts=None):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -164,7 +173,9 @@ def _draw_ahead_worker(port, fold, q, exchange="allreduce"):
     ip, ix = fold["train_indptr"], fold["train_indices"]
     out = []
     for ahead in (True, False):
-        e = Engine("bpr", 943, 1682, 16, n_neg=2, reg=0.05, dense_item_apply=True, seed=77)
+        e = Engine("bpr", 943, 1682, 16, n_neg=W, reg=0.05, dense_item_apply=True, seed=77)
+        for k, v in (opts or {}).items():
+            e.set_option(k, v)
         e.set_interactions(ip, ix)
         e.init_params(0.0, 0.1, seed=5)
         step, _ = make_gpu_sharded(e, 1682, 16, False, torch.device("cuda", 0), exchange=exchange)
@@ -174,21 +185,29 @@ def _draw_ahead_worker(port, fold, q, exchange="allreduce"):
         torch.cuda.synchronize()
         state = e.sampler_state()
         nxt = e.sample(120)           # drops a drawn-ahead batch, rewinds the sampler
+        loss = e.take_loss()
+        for _ in range(2):            # steps after the drop see clean counts
+            step(batch_size=120)
+        torch.cuda.synchronize()
         out.append((e.get_table("user"), e.get_table("item"), e.get_table("acc_user"), state,
-                    nxt[0], nxt[1], e.take_loss()))
+                    nxt[0], nxt[1], loss))
         e.close()
     q.put(out)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
-def test_draw_ahead_split_step_equals_plain_split_step(fold1, exchange):
+@pytest.mark.parametrize("exchange,W,psort", [("allreduce", 2, 0), ("rs_ag", 2, 0), ("allreduce", 5, 1),
+                                             ("rs_ag", 1, 1)])
+def test_draw_ahead_split_step_equals_plain_split_step(fold1, exchange, W, psort):
     """cf_step_local_grad / cf_step_local_apply(next_B) (all-reduce) or
     cf_step_local_draw (reduce-scatter): the batch drawn ahead is the one the
     sampler would draw next; dropping it rewinds."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_draw_ahead_worker, args=(_free_port(), fold1, q, exchange))
+    # psort: the drawn-ahead batch's positives are counted in cntP, and the
+    # drop (cf_sample) must clear them too
+    p = ctx.Process(target=_draw_ahead_worker, args=(_free_port(), fold1, q, exchange, W,
+                                                     {"pos_sort": psort}))
     p.start()
     a, b = q.get(timeout=300)
     p.join(timeout=120)
