@@ -2054,6 +2054,7 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
 
 int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (!e || !name) return fail(CF_EINVAL, "null argument");
+    CF_TRY(set_dev(e));   // some options (re)allocate device buffers
     const std::string n(name);
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
