@@ -330,8 +330,6 @@ def main():
                     help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
     ap.add_argument("--pos-sort", type=int, default=-1,
                     help="cf_set_option pos_sort (gradient pairs in positive-item order; -1 default)")
-    ap.add_argument("--psort-fused", type=int, default=-1,
-                    help="cf_set_option psort_fused (1 one-launch sort, 0 hipCUB scan + scatter; -1 default)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="cf_set_option deterministic (sort-based ranks, no float atomics)")
     ap.add_argument("--dry-run", action="store_true",
@@ -443,8 +441,6 @@ def main():
         eng.set_option("item_slots", args.item_slots)
     if args.pos_sort >= 0:
         eng.set_option("pos_sort", args.pos_sort)
-    if args.psort_fused >= 0:
-        eng.set_option("psort_fused", args.psort_fused)
     if args.deterministic:
         eng.set_option("deterministic", 1)
     if args.slot_max:

@@ -113,13 +113,6 @@ struct cf_engine {
     float* slotP = nullptr;           // [n_items * capP, d]
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
-    // 0: hipCUB scan, then the scatter (default); 1: both in one launch --
-    // measured 65 us against 22.6 at cfg2: cross-XCD visibility of offP costs
-    // an L2 write-back per tile and uncached agent-scope loads
-    int psort_fused = 0;
-    uint64_t* ps_state = nullptr;     // [tiles] look-back words
-    uint32_t* ps_ctr = nullptr;       // [4] tickets, tiles done
-    uint32_t ps_gen = 0;              // launches so far (the first is generation 1)
     bool slots_ready = false;
     // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
     // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches);
@@ -318,15 +311,7 @@ int ensure_slots(cf_engine* e) {
     for (int k = 0; k < 2; ++k) dfree(e->cntP_[k]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     e->psort_tmp = nullptr;
-    dfree(e->ps_state);
-    dfree(e->ps_ctr);
-    e->ps_gen = 0;
     if (psort_possible(e)) {
-        const size_t tiles = psort_state_words(c.n_items);
-        CF_TRY(dalloc(&e->ps_state, tiles));
-        CF_TRY(dalloc(&e->ps_ctr, (size_t)4));
-        CF_HIP(hipMemsetAsync(e->ps_state, 0, tiles * 8, e->stream));
-        CF_HIP(hipMemsetAsync(e->ps_ctr, 0, 16, e->stream));
         CF_TRY(dalloc(&e->slotP, (size_t)c.n_items * e->capP * c.n_factors));
         CF_TRY(dalloc(&e->offP, (size_t)c.n_items));
         for (int k = 0; k < 2; ++k) {
@@ -797,21 +782,6 @@ int det_hot(cf_engine* e, const StepArgs& a) {
 int psort(cf_engine* e, const StepArgs& a) {
     if (a.srec == nullptr) return CF_OK;
     ProfScope ps(e, CF_K_PSORT);
-    if (e->psort_fused) {
-        PsortArgs p{};
-        p.occU = a.occU; p.rankU = a.rankU; p.occV = a.occV; p.rankV = a.rankV;
-        p.B = a.B;
-        p.n_items = e->cfg.n_items;
-        p.cntP = a.cntP;
-        p.offP = e->offP;
-        p.srec = e->srec;
-        p.state = e->ps_state;
-        p.ctr = e->ps_ctr;
-        if (++e->ps_gen == 0 || (e->ps_gen & 0x3FFFFFFFu) == 0) e->ps_gen = 1;   // 0 = never published
-        p.gen = e->ps_gen;
-        CF_HIP(launch_psort_fused(p, a.W, e->stream));
-        return CF_OK;
-    }
     CF_HIP(launch_psort(a.occU, a.rankU, a.occV, a.rankV, a.B, a.W, a.cntP, e->offP, e->srec, e->cfg.n_items,
                         e->psort_tmp, e->psort_tmp_bytes, e->stream));
     return CF_OK;
@@ -1207,7 +1177,6 @@ int cf_destroy(cf_engine* e) {
     dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
     dfree(e->hotP); dfree(e->hotPb);
     dfree(e->slotP); dfree(e->offP); dfree(e->srec); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
-    dfree(e->ps_state); dfree(e->ps_ctr);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
@@ -2158,12 +2127,6 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "grad_path must be 0, 1 or 2");
         CF_TRY(discard_pending(e));   // a drawn-ahead batch was counted for the old path (pos_sort)
         e->grad_path = (int)value;
-        return CF_OK;
-    }
-    if (n == "psort_fused") {   // 0: hipCUB scan + scatter (default), 1: the one-launch sort (A/B)
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "psort_fused must be 0 or 1");
-        CF_HIP(hipStreamSynchronize(e->stream));
-        e->psort_fused = (int)value;
         return CF_OK;
     }
     if (n == "pos_sort" || n == "slot_max_pos") {

@@ -333,25 +333,6 @@ hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV
 // positive-sorted gradient: offP = exclusive scan of cntP (hipCUB), then
 // order[offP[i_p] + rankV[p]] = p for the B pairs; tmp sized by psort_scratch
 size_t psort_scratch(int64_t n_items);
-// ... or both in one launch (decoupled look-back scan + scatter in the same
-// blocks): state words sized by psort_state_words, ctr[4] zeroed once; gen =
-// a per-engine call counter
-struct PsortArgs {
-    const int32_t* __restrict__ occU;
-    const int32_t* __restrict__ rankU;
-    const int32_t* __restrict__ occV;
-    const int32_t* __restrict__ rankV;
-    int B;
-    int64_t n_items;
-    const int32_t* __restrict__ cntP;
-    int32_t* __restrict__ offP;
-    int32_t* __restrict__ srec;
-    uint64_t* __restrict__ state;   // [tiles] (generation, flag, value)
-    uint32_t* __restrict__ ctr;     // [4] tile tickets [2], tiles done [2] (by generation parity)
-    uint32_t gen;
-};
-size_t psort_state_words(int64_t n_items);
-hipError_t launch_psort_fused(const PsortArgs& a, int W, hipStream_t s);
 hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
                         int B, int W, const int32_t* cntP, int32_t* offP, int32_t* srec, int64_t n_items,
                         void* tmp, size_t tmp_bytes, hipStream_t s);

@@ -312,14 +312,20 @@ __device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t
 // The draw runs 8 lanes per pair (32 pairs per block): one wave generation
 // covers a 65,536-pair batch at full occupancy, and a user's row (~51 ids at
 // cfg2) is tested in one batch of up to 8 independent 32-B loads.
-constexpr int kPrepGL = 8;
+#ifndef CF_PREP_GL
+#define CF_PREP_GL 8       // lanes per pair in the draw (a power of two, 2..16)
+#endif
+#ifndef CF_PREP_CHUNKS
+#define CF_PREP_CHUNKS 8   // row chunks in flight per candidate test
+#endif
+constexpr int kPrepGL = CF_PREP_GL;
 constexpr int kPrepPairsPerBlock = kBlock / kPrepGL;
-constexpr int kPrepChunks = 8;   // row chunks in flight per candidate test
+constexpr int kPrepChunks = CF_PREP_CHUNKS;
 
+// OR over the kPrepGL lanes of a draw group
 __device__ __forceinline__ uint32_t gor8(uint32_t v) {
-    v |= (uint32_t)__shfl_xor((int)v, 4, 64);
-    v |= (uint32_t)__shfl_xor((int)v, 2, 64);
-    v |= (uint32_t)__shfl_xor((int)v, 1, 64);
+#pragma unroll
+    for (int o = kPrepGL / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
     return v;
 }
 

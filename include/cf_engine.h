@@ -424,9 +424,6 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                results up to fp32 summation order.  0 = off; 2 = auto
  *                (default): on for batches of >= 2^18 pairs (cfg2: 7 %
  *                faster steps at 2^19, 3.5 % at 2^18, even at 2^17).
- *   "psort_fused" 1 = pos_sort's scan and scatter in one launch (decoupled
- *                look-back; measured 65 vs 22.6 us at cfg2),
- *                0 = hipCUB scan, then the scatter (default).  Same results.
  *   "slot_max_pos" positive partial rows per item row under pos_sort (default
  *                8; later partials of a hot item add with float atomics).
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =

@@ -19,16 +19,6 @@ from oracle import cf_oracle as O
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
-_FUSED = [1]
-
-
-@pytest.fixture(autouse=True, params=[1, 0], ids=["fused", "cub"])
-def psort_fused(request):
-    """Every case runs with the one-launch sort (decoupled look-back scan +
-    scatter, the default) and with the hipCUB scan + separate scatter."""
-    _FUSED[0] = request.param
-    yield request.param
-    _FUSED[0] = 1
 
 
 def rel(a, b):
@@ -41,7 +31,6 @@ def make(model, fold1, d, W, opts, **kw):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=W, seed=7, **kw)
     e.set_option("item_slots", 0)
-    e.set_option("psort_fused", _FUSED[0])
     for k, v in opts.items():
         e.set_option(k, v)
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
@@ -179,7 +168,6 @@ def test_pos_sort_device_pipeline_equals_plain(fold1):
     for ps in (0, 1):
         e = Engine("bpr", 943, 1682, 64, n_neg=1, reg=0.05, seed=21)
         e.set_option("item_slots", 0)
-        e.set_option("psort_fused", _FUSED[0])
         e.set_option("pos_sort", ps)
         e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
         e.init_params(0.0, 0.1, truncated=True, seed=1)
@@ -203,7 +191,6 @@ def test_pos_sort_device_pipeline_matches_oracle(fold1):
     d, reg, B = 32, 0.05, 1024
     e = Engine("bpr", 943, 1682, d, n_neg=1, reg=reg, seed=33)
     e.set_option("pos_sort", 1)
-    e.set_option("psort_fused", _FUSED[0])
     e.set_option("item_slots", 0)
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     U, V = tables(fold1, d, 5)
@@ -232,7 +219,6 @@ def test_pos_sort_auto_by_batch_size():
     out = []
     for ps in (None, 0):
         e = Engine("bpr", nu, ni, d, n_neg=1, reg=0.02, seed=3)
-        e.set_option("psort_fused", _FUSED[0])
         if ps is not None:
             e.set_option("pos_sort", ps)
         e.set_interactions(ip, ix)
