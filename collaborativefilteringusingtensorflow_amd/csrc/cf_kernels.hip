@@ -1840,11 +1840,18 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 if (a.rankV[k] == 0) {
                     const int32_t r = a.occV[k];
                     if constexpr (PS) {
-                        // owner: the rank-0 negative, or the rank-0 positive
-                        // of an item drawn as no pair's negative
-                        const int cn = a.cntV[r], cp = a.cntP[r];
-                        c = cn + cp;
-                        if (c >= 2 && (k >= a.nPos || cn == 0)) row = r;
+                        // owner: the rank-0 positive of an item with positives
+                        // in the batch, else its rank-0 negative.  Which class
+                        // owns comes from offP (offP[r+1] - offP[r] = the
+                        // item's positives), never from a count: an owner
+                        // resets cntV / cntP while other waves still detect,
+                        // so a rule on cntV == 0 could crown a second owner
+                        const int64_t o0 = a.offP[r];
+                        const int64_t o1 = (int64_t)r + 1 < a.n_items ? (int64_t)a.offP[r + 1] : a.nPos;
+                        if ((k < a.nPos) == (o1 > o0)) {
+                            c = a.cntV[r] + a.cntP[r];
+                            if (c >= 2) row = r;
+                        }
                     } else {
                         c = a.cntV[r];
                         if (c >= 2) row = r;
