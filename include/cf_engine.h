@@ -420,7 +420,9 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                adds the partials to the negatives' slot rows.  BPR / AMF /
  *                CML on the phased kernel (W in {1, 5}, d <= 128), not with
  *                deterministic, item_slots 1, hot_replicas > 1, pipeline 2 or
- *                a dense item apply (the option is ignored there).  Same
+ *                a dense item apply other than item_reduce 1 (the option is
+ *                ignored there; with item_reduce 1 the multi-rank item reduce
+ *                sums the partials into the bound gradient).  Same
  *                results up to fp32 summation order.  0 = off; 2 = auto
  *                (default): on for batches of >= 2^18 pairs (cfg2: 7 %
  *                faster steps at 2^19, 3.5 % at 2^18, even at 2^17).
