@@ -98,13 +98,35 @@ def draw_bytes_per_pair(W, G, mean_row):
     return 8 + 16 + 4 * mean_row + 12 * occ + ((16 + 4 * G) if G else 0)
 
 
-def load_pmc(workload, n_gpus):
+def lib_digest():
+    """First 12 hex digits of sha1(libcf_engine.so): the build the committed
+    counters were collected on."""
+    import hashlib
+    from collaborativefilteringusingtensorflow_amd import _native
+    try:
+        with open(_native.LIB_PATH, "rb") as f:
+            return hashlib.sha1(f.read()).hexdigest()[:12]
+    except OSError:
+        return "nolib"
+
+
+def pmc_key(config, B, world, path_flags, exchange=None):
+    """Key of profiles/pmc_traffic.json: workload, batch, ranks, the kernel
+    path the step takes (cf_step_path flags) and the engine build -- counters
+    collected on another build, path or world size do not apply to this line."""
+    k = "%s_b%d_n%d_p%x_%s" % (config, B, world, path_flags, lib_digest())
+    return k + ("_" + exchange if exchange else "")
+
+
+def load_pmc(key):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py) for
+    exactly this key, else None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             rec = json.load(f)
-        r = rec.get(workload, {})
-        return r.get("step_hbm_bytes_per_launch")
+        return rec.get(key, {}).get("step_hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -564,7 +586,9 @@ def main():
     mean_row = float((deg * deg).sum() / max(deg.sum(), 1.0))
     db = draw_bytes_per_pair(W, Gm, mean_row) * B if dom == "grad_prep" else 0.0
     achieved = (gb + db) / step_avg_s / 1e9 if step_avg_s == step_avg_s and step_avg_s > 0 else None
-    traffic = load_pmc("%s_b%d" % (args.config, B), world)
+    path_flags, path = eng.step_path(B)
+    key = pmc_key(args.config, B, world, path_flags, args.item_exchange if sharded else None)
+    traffic = load_pmc(key)
     if dom == "grad_prep":
         kdesc = ("grad_fast_kernel: gather + loss + grads + singleton-row Adagrad of step s, "
                  "fused with the device draw + count of step s+1")
@@ -578,6 +602,8 @@ def main():
                 "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBPS) if achieved else None,
                 "traffic": traffic,
+                "pmc_key": key,
+                "step_path": path,
                 "bytes_per_launch": gb + db,
                 "gather_bytes_per_launch": gb,
                 "gather_only_GBps": gb / step_avg_s / 1e9 if achieved else None,

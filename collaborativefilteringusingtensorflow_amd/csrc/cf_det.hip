@@ -73,7 +73,10 @@ int grid_of(int64_t n) {
 
 // positive-sorted gradient: pair p goes to position offP[i_p] + its rank
 // among the batch's positives of i_p (counting sort by positive item), as
-// one record (u, rank_u, i, p, (j_w, rank_j_w)...) of psort_stride(W) ints
+// one record of psort_stride(W) ints:
+//   [u, i, j_0 .. j_{W-1}, (ru | rj0 << 16), (rj1 | rj2 << 16), .., 0 padding]
+// -- the ranks of u and of the negatives as 16-bit halves (clamped to
+// 0xFFFF), ru in the low half of the first rank word (load_idx_sorted)
 __device__ __forceinline__ int32_t rank16(int32_t r) { return r < 0xFFFF ? r : 0xFFFF; }
 
 template <int W>

@@ -1884,9 +1884,15 @@ int cf_xchg_draw(cf_engine* e, int32_t B, void* send_counts_dev, int32_t* half_o
     return CF_OK;
 }
 
-int cf_xchg_adopt(cf_engine* e) {
+int cf_xchg_adopt(cf_engine* e, int32_t B) {
     CF_TRY(check_xchg(e, 0));
-    if (!e->x_pend) return fail(CF_ESTATE, "no exchange batch drawn ahead (cf_xchg_draw)");
+    if (!e->x_pend) return fail(CF_EAGAIN, "no exchange batch drawn ahead (cf_xchg_draw)");
+    if (e->x_pend_B != B) {   // drawn at another batch size: drop it (uncount, rewind the sampler)
+        const int drawn = e->x_pend_B;
+        CF_TRY(discard_pending(e));
+        return fail(CF_EAGAIN, "the batch drawn ahead has B=" + std::to_string(drawn) + ", not " +
+                                   std::to_string(B) + ": discarded, draw again");
+    }
     e->x_args = e->x_pend_args;
     e->x_set = e->x_pend_set;
     e->x_B = e->x_pend_B;
@@ -2146,6 +2152,27 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     return fail(CF_EINVAL, "unknown option " + n);
+}
+
+int cf_step_path(cf_engine* e, int32_t B, int32_t* flags_out) {
+    if (!e || !flags_out) return fail(CF_EINVAL, "null argument");
+    if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
+    const cf_config& c = e->cfg;
+    StepArgs a{};
+    a.model = c.model;
+    a.d = c.n_factors;
+    a.W = c.n_neg;
+    a.G = group_count(c);
+    a.grad_path = e->grad_path;
+    int f = 0;
+    if (grad_fast_w(a) != 0) f |= CF_PATH_PHASED;
+    if (psort_active(e, B)) f |= CF_PATH_POS_SORT;
+    if (e->item_recs && (!c.dense_item_apply || e->item_reduce)) f |= CF_PATH_ITEM_RECORDS;
+    if (e->det) f |= CF_PATH_DETERMINISTIC;
+    if (c.dense_item_apply) f |= CF_PATH_DENSE_ITEMS;
+    f |= (e->pipeline & 3) << 8;
+    *flags_out = f;
+    return CF_OK;
 }
 
 int cf_profile_enable(cf_engine* e, int32_t on) {

@@ -287,6 +287,8 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + cou
 // gather, loss, grads, singleton apply; with `next`, the same launch also
 // draws and counts the next step's batch (other buffer set)
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
+// the phased gradient kernel's compile-time W (1 or 5) a step takes, 0 = generic
+int grad_fast_w(const StepArgs& a);
 // blocks (= loss partials) of the grad launch for this step shape
 int grad_blocks(const StepArgs& a, bool with_draw = false);
 int grad_blocks_max(int B);  // upper bound over every grad variant

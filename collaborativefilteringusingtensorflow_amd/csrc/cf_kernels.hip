@@ -1923,12 +1923,12 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
     if (minor_block(blockIdx.x, napply, nprep, idx))
         prep_any<MODEL>(a, idx);
     else
-        apply_body<EPL, kBlock, HOT>(p, idx, napply);
+        apply_body<EPL, kBlock, HOT, PS>(p, idx, napply);
 #elif CF_APPLY_PREP_ORDER == 1
     if ((int)blockIdx.x < nprep)
         prep_any<MODEL>(a, blockIdx.x);
     else
-        apply_body<EPL, kBlock, HOT>(p, blockIdx.x - nprep, napply);
+        apply_body<EPL, kBlock, HOT, PS>(p, blockIdx.x - nprep, napply);
 #else
     if ((int)blockIdx.x < napply)
         apply_body<EPL, kBlock, HOT, PS>(p, blockIdx.x, napply);
@@ -2206,6 +2206,8 @@ static int fast_w(const StepArgs& a) {
     return ok && (a.W == 1 || a.W == 5) ? a.W : 0;
 }
 
+int grad_fast_w(const StepArgs& a) { return fast_w(a); }
+
 #ifndef CF_GRAD_WAVE_BLOCKS
 // 1: fast path without draw blocks in one-wave workgroups (measured no faster
 // at cfg2: 43.9 vs 44.2 us), 0: 256-lane workgroups
@@ -2375,6 +2377,9 @@ static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
 
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
     if (CF_APPLY_WAVE_BLOCKS) {
+        // one-wave apply blocks have no pos_sort owner rule: refuse rather
+        // than skip or double-apply an item whose positives count in cntP
+        if (a.cntP != nullptr || a.hotP != nullptr) return hipErrorInvalidValue;
         const dim3 grid(apply_grid(a)), block(kWave);
         switch (epl_for(a.d)) {
             case 1: hipLaunchKernelGGL(apply_wave_kernel<1>, grid, block, 0, s, a); break;

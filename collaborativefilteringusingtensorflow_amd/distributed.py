@@ -122,6 +122,10 @@ class ReduceScatterItems(object):
         self.chunk, self.rank = int(chunk), int(rank)
         self.row0, self.row1 = self.rank * self.chunk, (self.rank + 1) * self.chunk
         self.group = group
+        # accumulators of rows other ranks own are stale after an owner
+        # update until sync_state gathers them (Engine.get_table refuses them)
+        self.stale = False
+        self.stale_tables = ("acc_item", "acc_bias")
 
     def overlap(self, dist):
         return self.grad.is_cuda and dist.get_backend(self.group) != "gloo"
@@ -155,6 +159,7 @@ class ReduceScatterItems(object):
         # step, then the owner's Adagrad on its rows
         be.clear_item_grad()
         be.step_items_range(self.row0, self.row1, self.grad_slice, self.bias_slice)
+        self.stale = True
 
     def gather(self, dist, async_op):
         return _Works([self._ag(dist, t, w, async_op) for t, w in self.tables])
@@ -164,6 +169,7 @@ class ReduceScatterItems(object):
         only the owner keeps its range current during training)."""
         for t, w in self.state:
             self._ag(dist, t, w, False)
+        self.stale = False
 
 
 def _items(items, group):
@@ -265,6 +271,7 @@ def _bind_rs_items(engine, n_items, d, with_bias, device, group=None):
     items = ReduceScatterItems(grad, z(chunk * d), tables, chunk, rank, grad_bias=gb,
                                bias_slice=z(chunk) if with_bias else None, state=state, group=group)
     items._keep = (V, AV) + ((b, Ab) if with_bias else ())
+    engine._stale_guard = items   # get_table refuses stale accumulators until sync_state
     return items
 
 
@@ -361,14 +368,16 @@ class GroupExchangeStep(object):
         """(send counts, recv counts, send_ids half) of this step."""
         be, dist, torch = self.backend, self._dist, self._torch
         if self.pipelined and pairs is None:
-            if self._next is not None:
-                try:
-                    be.xchg_adopt()
-                except Exception:          # the drawn batch was dropped by another call
-                    self._next = None
+            # the batch drawn one step ahead is adopted only at the size it
+            # was drawn at; dropped by another call or drawn at another size
+            # (the engine then discards it: counts cleared, sampler rewound),
+            # it is drawn again now
+            if self._next is not None and not be.xchg_adopt(batch_size):
+                self._next = None
             if self._next is None:
                 self._draw(batch_size)
-                be.xchg_adopt()
+                if not be.xchg_adopt(batch_size):
+                    raise RuntimeError("cf_xchg_adopt refused the batch just drawn")
             h, ev = self._next
             if ev is not None:
                 ev.synchronize()           # recorded a step ago: already complete
@@ -444,8 +453,8 @@ class EngineExchange(object):
     def xchg_draw(self, batch_size, counts_ptr):
         return self.e.xchg_draw(batch_size, counts_ptr)
 
-    def xchg_adopt(self):
-        self.e.xchg_adopt()
+    def xchg_adopt(self, batch_size):
+        return self.e.xchg_adopt(batch_size)
 
     def xchg_serve(self, n):
         self.e.xchg_serve(n)

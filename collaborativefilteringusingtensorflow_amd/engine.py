@@ -141,6 +141,12 @@ class Engine(object):
                 "cf_set_table(%s)" % name)
 
     def get_table(self, name):
+        guard = getattr(self, "_stale_guard", None)
+        if guard is not None and guard.stale and name in guard.stale_tables:
+            # rs_ag item-range ownership: only the owner keeps its accumulator
+            # rows current; the other ranks' copies are gathered by sync_state
+            raise RuntimeError("%s is stale on this rank under the rs_ag item exchange: "
+                               "call step.sync_state() before reading it" % name)
         out = np.empty(self._table_shape(name), dtype=np.float32)
         N.check(self._L.cf_get_table(self._h, N.TABLES[name], _ptr(out, ctypes.c_float), out.size),
                 "cf_get_table(%s)" % name)
@@ -336,8 +342,15 @@ class Engine(object):
                                      ctypes.byref(h)), "cf_xchg_draw")
         return int(h.value)
 
-    def xchg_adopt(self):
-        N.check(self._L.cf_xchg_adopt(self._h), "cf_xchg_adopt")
+    def xchg_adopt(self, batch_size):
+        """Take the batch drawn ahead as this step's.  False (CF_EAGAIN) when
+        none of that size is pending -- a batch drawn at another size is
+        discarded by the engine (counts cleared, sampler rewound)."""
+        st = self._L.cf_xchg_adopt(self._h, int(batch_size))
+        if st == N.CF_EAGAIN:
+            return False
+        N.check(st, "cf_xchg_adopt")
+        return True
 
     def xchg_serve(self, n_recv):
         N.check(self._L.cf_xchg_serve(self._h, int(n_recv)), "cf_xchg_serve")
@@ -376,6 +389,18 @@ class Engine(object):
                                       _ptr(val, ctypes.c_float) if return_values else None),
                 "cf_score_topk")
         return (idx, val) if return_values else idx
+
+    PATH_FLAGS = {"phased": 1, "pos_sort": 2, "item_records": 4, "deterministic": 8, "dense_items": 16}
+
+    def step_path(self, batch_size):
+        """The kernel path a step of ``batch_size`` pairs takes now
+        (cf_step_path): (flags, {name: bool, ..., "pipeline": n})."""
+        f = ctypes.c_int32(0)
+        N.check(self._L.cf_step_path(self._h, int(batch_size), ctypes.byref(f)), "cf_step_path")
+        v = int(f.value)
+        out = {k: bool(v & m) for k, m in self.PATH_FLAGS.items()}
+        out["pipeline"] = (v >> 8) & 3
+        return v, out
 
     def set_option(self, name, value):
         N.check(self._L.cf_set_option(self._h, name.encode(), int(value)), "cf_set_option(%s)" % name)

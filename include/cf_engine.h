@@ -60,7 +60,10 @@ enum cf_status {
     CF_EINVAL = -1,   /* bad argument / shape                         */
     CF_EHIP = -2,     /* HIP runtime error (message has the HIP text)  */
     CF_ESTATE = -3,   /* call out of order (e.g. no interactions set)  */
-    CF_ENOMEM = -4    /* device or host allocation failed              */
+    CF_ENOMEM = -4,   /* device or host allocation failed              */
+    CF_EAGAIN = -5    /* cf_xchg_adopt: no batch of that size drawn ahead
+                         (none drawn, dropped, or drawn at another B and
+                         now discarded): draw one (cf_xchg_draw) and retry */
 };
 
 /* parameter tables addressable by cf_set_table / cf_get_table */
@@ -298,7 +301,9 @@ int cf_bind_table(cf_engine* eng, int32_t table, void* device_ptr, int64_t n_ele
  *                    its per-owner counts to send_counts_dev[h*world ..]
  *                    (device int32 [2, world]); the caller all-to-alls the
  *                    counts and copies them to the host asynchronously
- *   cf_xchg_adopt    take the drawn batch as this step's (stage begun)
+ *   cf_xchg_adopt    take the drawn batch as this step's (stage begun); B
+ *                    must be the size it was drawn at, else it is discarded
+ *                    (counts cleared, sampler rewound) and CF_EAGAIN returned
  *   all-to-all       send_ids -> recv_ids (ids this rank serves)
  *   cf_xchg_serve    copy the served rows (pre-update) into serve_rows
  *   all-to-all       serve_rows -> rows (in send_ids order)
@@ -321,10 +326,22 @@ int cf_bind_exchange(cf_engine* eng, void* send_ids, void* rows, void* grads, in
 int cf_xchg_begin(cf_engine* eng, int32_t B, const int32_t* host_pairs, const int32_t* host_negs,
                   const int32_t* host_groups, int32_t* send_counts_out);
 int cf_xchg_draw(cf_engine* eng, int32_t B, void* send_counts_dev, int32_t* half_out);
-int cf_xchg_adopt(cf_engine* eng);
+int cf_xchg_adopt(cf_engine* eng, int32_t B);
 int cf_xchg_serve(cf_engine* eng, int64_t n_recv);
 int cf_xchg_grad(cf_engine* eng);
 int cf_xchg_finish(cf_engine* eng, int64_t n_recv);
+
+/* Which kernels a step of B pairs takes with the current options (bench
+ * keys its committed PMC counters by it; tests assert the path under test):
+ * a bitmask of cf_path_flag, plus the pipeline option in bits 8-9. */
+enum cf_path_flag {
+    CF_PATH_PHASED = 1,         /* phased gradient kernel (grad_fast_kernel), else generic */
+    CF_PATH_POS_SORT = 2,       /* positive-sorted gradient (psort + partial rows)         */
+    CF_PATH_ITEM_RECORDS = 4,   /* item records + user-row stash instead of slot rows      */
+    CF_PATH_DETERMINISTIC = 8,  /* sort-based ranks, compact slots, no float atomics       */
+    CF_PATH_DENSE_ITEMS = 16    /* multi-rank item path (dense item gradient)              */
+};
+int cf_step_path(cf_engine* eng, int32_t B, int32_t* flags_out);
 
 /* Pre-update loss accumulated since the last call (syncs), then reset. */
 int cf_take_loss(cf_engine* eng, double* loss_sum_out);

@@ -28,23 +28,12 @@ relaxed one (tests/test_oracle.py::test_fp32_oracle_drift_bounds_cml_tolerance).
 import numpy as np
 import pytest
 
+from conftest import CML_TRAJ, assert_close
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
 
 RTOL, ATOL = 1e-5, 1e-6
-
-
-CML_TRAJ = dict(rtol=5e-5, atol=3e-6)
-
-
-def assert_close(got, ref, what, rtol=RTOL, atol=ATOL):
-    got = np.asarray(got, np.float64)
-    ref = np.asarray(ref, np.float64)
-    err = np.abs(got - ref)
-    bad = err > atol + rtol * np.abs(ref)
-    worst = float(np.max(err / (atol + rtol * np.abs(ref)))) if err.size else 0.0
-    assert not bad.any(), (what, int(bad.sum()), float(err.max()), worst)
 
 
 HP = {"cml": dict(margin=1.0, reg_cov=1.0, clip_norm=1.0),   # testcml.py:26-34

@@ -153,13 +153,11 @@ def test_two_rank_sharded_engine_equals_global_step(fold1, streams, model, strea
         p.join(timeout=120)
         assert p.exitcode == 0
     U, V, AU, AV = _oracle_run(model, batches, U0, V0)
-    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
     for rank, u0, u1, Ul, Vr, AVr in res:
-        assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
-        assert rel(Vr, V) <= 1e-5 and rel(AVr, AV) <= 1e-5
         tol = dict(rtol=5e-5, atol=3e-6) if model == "cml" else {}
         _check_elementwise(Ul, U[u0:u1], **tol)
         _check_elementwise(Vr, V, **tol)
+        _check_elementwise(AVr, AV, **tol)
     assert np.array_equal(res[0][4], res[1][4])   # replicas bit-identical
 
 

@@ -11,15 +11,15 @@ with ragged B, hot rows and repeated items."""
 import numpy as np
 import pytest
 
-from conftest import get_stream
+from conftest import assert_close, get_stream
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
-RTOL = 1e-4
+# elementwise: |gpu - oracle| <= 4e-5 + 1e-4 |oracle| (the former max-relative 1e-4 at max|ref| ~ 0.4
+# allowed 4e-5 on every element; the [B, B] ensemble loss sums B^2 terms in fp32)
+RTOL, ATOL = 1e-4, 4e-5
 
 
-def rel(a, b):
-    return float(np.max(np.abs(np.asarray(a, np.float64) - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
 def make(K, nu, ni, d, reg, seed=5):
@@ -38,8 +38,7 @@ def make(K, nu, ni, d, reg, seed=5):
 def check_tables(e, U, V, H, AU, AV, AH):
     for name, o in (("user", U), ("item", V), ("h", H), ("acc_user", AU), ("acc_item", AV),
                     ("acc_h", AH)):
-        r = rel(e.get_table(name), o)
-        assert r <= RTOL, (name, r)
+        assert_close(e.get_table(name), o, name, rtol=RTOL, atol=ATOL)
 
 
 @pytest.mark.parametrize("K,d,reg", [(3, 100, 0.01), (2, 20, 0.1), (1, 16, 0.05)])

@@ -15,6 +15,8 @@ import sys
 
 import numpy as np
 import pytest
+
+from conftest import assert_close
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
@@ -58,6 +60,9 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     if sampled == "steps":           # device-sampled steps only (pipelined count exchange)
         for _ in range(7):
             step(batch_size=64)
+    elif sampled == "sizes":         # ... with the batch size changing between steps
+        for bs in SIZES:
+            step(batch_size=bs)
     elif sampled:
         for _ in range(6):
             pairs, negs, groups = e.sample(64)
@@ -78,6 +83,9 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     e.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+SIZES = (64, 64, 48, 48, 64, 32, 32, 64)
 
 
 def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True):
@@ -112,12 +120,13 @@ def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exch
     AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
     for pairs, negs, groups in batches:
         O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
-    rel = lambda a, c: np.abs(a - c).max() / np.abs(c).max()
     for rank, u0, u1, Ul, Vr, br, AUl, _, AVr, Abr in res:
-        assert rel(Ul, U[u0:u1]) <= 1e-5, (rank, rel(Ul, U[u0:u1]))
-        assert rel(AUl, AU[u0:u1]) <= 1e-5, (rank, rel(AUl, AU[u0:u1]))
-        assert rel(Vr, V) <= 1e-5 and rel(br, b) <= 1e-5
-        assert rel(AVr, AV) <= 1e-5 and rel(Abr, Ab) <= 1e-5
+        assert_close(Ul, U[u0:u1], ("user", rank))
+        assert_close(AUl, AU[u0:u1], ("acc_user", rank))
+        assert_close(Vr, V, ("item", rank))
+        assert_close(br, b, ("bias", rank))
+        assert_close(AVr, AV, ("acc_item", rank))
+        assert_close(Abr, Ab, ("acc_bias", rank))
     assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
 
 
@@ -159,7 +168,27 @@ def test_pipelined_count_exchange_equals_synchronous(fold1, exchange):
     dummy = [(np.zeros((1, 2), np.int32), np.zeros((1, 5), np.int32), np.zeros((1, 1), np.int32))]
     a = _run(fold1, dummy, U0, V0, b0, sampled="steps", exchange=exchange, pipelined=True)
     b = _run(fold1, dummy, U0, V0, b0, sampled="steps", exchange=exchange, pipelined=False)
-    rel = lambda x, y: np.abs(x - y).max() / np.abs(y).max()
     for ra, rb in zip(a, b):
         for k in (3, 4, 5, 6):      # user, item, bias, acc_user
-            assert rel(ra[k], rb[k]) <= 1e-5, (ra[0], k, rel(ra[k], rb[k]))
+            assert_close(ra[k], rb[k], (ra[0], k))
+
+
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
+def test_pipelined_exchange_batch_size_change(fold1, exchange):
+    """The batch drawn one step ahead is taken only at the size it was drawn
+    at: when the caller changes batch_size between pipelined steps, the
+    engine discards it (counts cleared, sampler rewound, CF_EAGAIN) and the
+    step draws at the new size -- so the pipelined run trains exactly what
+    the synchronous one trains over the same size sequence."""
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(15)
+    d = 16
+    U0 = O.init_table(rng, (943, d))
+    V0 = O.init_table(rng, (1682, d))
+    b0 = O.init_table(rng, (1682,))
+    dummy = [(np.zeros((1, 2), np.int32), np.zeros((1, 5), np.int32), np.zeros((1, 1), np.int32))]
+    a = _run(fold1, dummy, U0, V0, b0, sampled="sizes", exchange=exchange, pipelined=True)
+    b = _run(fold1, dummy, U0, V0, b0, sampled="sizes", exchange=exchange, pipelined=False)
+    for ra, rb in zip(a, b):
+        for k in (3, 4, 5, 6, 8, 9):      # user, item, bias, acc_user, acc_item, acc_bias
+            assert_close(ra[k], rb[k], (ra[0], k))

@@ -6,13 +6,16 @@
   sampler) and the same initial tables as the CPU oracle (oracle/cf_oracle.c,
   fp32): ranking metrics after training must agree within 0.2 % (north star).
 * the same drivers' device-sampled path trains (metrics far above random).
-* cfg2 at full size (1M users x 100K items, d=64, B=65,536): one step on a
-  device-drawn batch against the float64 oracle (1e-5 relative).
+* cfg2 at full size (1M users x 100K items, d=64): one step at B=65,536 on a
+  device-drawn batch, and two pipelined steps at the bench batch B=2^19
+  (pos_sort, partials past capP on atomics) against the float64 oracle,
+  elementwise |gpu - oracle| <= 1e-6 + 1e-5 |oracle| over the whole tables.
 """
 import numpy as np
 import pytest
 import scipy.sparse as sp
 
+from conftest import assert_close
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -132,10 +135,18 @@ def test_amf_rejects_rand():
         AMF(10, 10, adv_method="rand")
 
 
-def test_cfg2_full_size_step_parity():
-    from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+@pytest.fixture(scope="module")
+def cfg2_graph():
+    from collaborativefilteringusingtensorflow_amd.engine import synth_graph
+    return synth_graph(1_000_000, 100_000, 50.0, 0.8, 20261015, n_threads=16)
+
+
+def test_cfg2_full_size_step_parity(cfg2_graph):
+    """cfg2 at SURVEY 8(d)'s B = 65,536 (pos_sort auto: off): one host-fed
+    step on a device-drawn batch against the float64 oracle, elementwise."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni, d, B = 1_000_000, 100_000, 64, 65536
-    ip, ix = synth_graph(nu, ni, 50.0, 0.8, 20261015, n_threads=16)
+    ip, ix = cfg2_graph
     e = Engine("bpr", nu, ni, d, n_neg=1, reg=0.02, seed=77)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=True, seed=1)
@@ -155,9 +166,49 @@ def test_cfg2_full_size_step_parity():
     lo = O.bpr_step(U, V, AU, AV, pairs, negs, 0.02)
     assert abs(loss - lo) <= 1e-5 * abs(lo)
     for name, ref in (("user", U), ("item", V), ("acc_user", AU), ("acc_item", AV)):
-        got = e.get_table(name)
-        err = np.abs(got - ref).max() / np.abs(ref).max()
-        assert err <= 1e-5, (name, err)
+        assert_close(e.get_table(name), ref, name)
+    e.close()
+
+
+def test_cfg2_bench_batch_pos_sort_matches_oracle(cfg2_graph):
+    """The benched cfg2 instantiation itself: B = 2^19 pairs per step with
+    pos_sort auto (on), i.e. psort + grad_fast_kernel<BPR, d 64, W 1, SORT>
+    + the PS apply fused with the next draw (apply_prep_kernel), where the
+    Zipf-head positives' partials overflow capP into float atomics.  Three
+    pipelined steps move off the initial state; then two more pipelined
+    steps (cf_train_steps: the first one's apply launch draws the second's
+    batch) are replayed by the float64 oracle on the same drawn batches and
+    compared over the WHOLE tables, elementwise (bprmf.py:83-88: TF1's
+    dedup-sum before SparseApplyAdagrad)."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d, B, K, reg = 1_000_000, 100_000, 64, 1 << 19, 2, 0.02
+    ip, ix = cfg2_graph
+    e = Engine("bpr", nu, ni, d, n_neg=1, reg=reg, seed=78)
+    e.set_interactions(ip, ix)
+    e.init_params(0.0, 0.1, truncated=True, seed=1)
+    e.profile_reset()
+    e.profile(True)
+    e.train_steps(B, 3)
+    T = {t: e.get_table(t).astype(np.float64) for t in ("user", "item", "acc_user", "acc_item")}
+    st = e.sampler_state()
+    batches = [e.sample(B)[:2] for _ in range(K)]
+    e.set_sampler_state(*st)
+    loss = e.train_steps(B, K)
+    e.profile(False)
+    assert e.profile_read("psort")[1] == 3 + K, "pos_sort did not run at the bench batch"
+    # the drawn batches overflow the positives' partial slots (capP = 8):
+    # partial k of item i covers sorted positions of block offP[i] / 16 + k
+    for pairs, _ in batches:
+        cnt = np.bincount(pairs[:, 1], minlength=ni)
+        off = np.cumsum(cnt) - cnt
+        nparts = np.where(cnt > 0, (off + cnt - 1) // 16 - off // 16 + 1, 0)
+        assert (nparts > 8).sum() > 100, int((nparts > 8).sum())
+    lo = 0.0
+    for pairs, negs in batches:
+        lo += O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, reg)
+    assert abs(loss - lo) <= 1e-5 * abs(lo), (loss, lo)
+    for t in T:
+        assert_close(e.get_table(t), T[t], t)
     e.close()
 
 

@@ -10,15 +10,12 @@ Tolerance: 1e-5 relative (fp32 summation order of duplicated rows may differ).
 import numpy as np
 import pytest
 
+from conftest import assert_close
+
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
 
-
-def rel(a, b):
-    a = np.asarray(a, np.float64)
-    b = np.asarray(b, np.float64)
-    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
 
 
 def make(model, fold1, d, W, G, **opts):
@@ -62,7 +59,7 @@ def test_train_steps_equals_host_fed_stream(fold1, model, d, W, G, B, opts):
     assert abs(loss_d - loss_h) <= RTOL * abs(loss_h), (loss_d, loss_h)
     assert host.sampler_state() == dev.sampler_state()
     for t in TABLES[model]:
-        assert rel(dev.get_table(t), host.get_table(t)) <= RTOL, (t, rel(dev.get_table(t), host.get_table(t)))
+        assert_close(dev.get_table(t), host.get_table(t), t)
     # the pipelined engine continues correctly after a host-fed step
     pairs, negs, groups = host.sample(B)
     p2, n2, g2 = dev.sample(B)
@@ -72,6 +69,6 @@ def test_train_steps_equals_host_fed_stream(fold1, model, d, W, G, B, opts):
     host.train_steps(B, 3)
     dev.train_steps(B, 3)
     for t in TABLES[model]:
-        assert rel(dev.get_table(t), host.get_table(t)) <= RTOL, t
+        assert_close(dev.get_table(t), host.get_table(t), t)
     host.close()
     dev.close()

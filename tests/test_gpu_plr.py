@@ -7,14 +7,13 @@ the recommend step scores U.V^T + b."""
 import numpy as np
 import pytest
 
+from conftest import assert_close
+
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 
-
-def rel(a, b):
-    return float(np.max(np.abs(np.asarray(a, np.float64) - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
 def tuples_for(rng, fold1, B, width):
@@ -66,7 +65,7 @@ def test_plr_trajectory_matches_oracle(fold1, name, kind, width, hp, slot_max):
         assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
     for t, o in (("user", U64), ("item", V64), ("bias", b64), ("acc_user", AU),
                  ("acc_item", AV), ("acc_bias", Ab)):
-        assert rel(e.get_table(t), o) <= RTOL, (t, rel(e.get_table(t), o))
+        assert_close(e.get_table(t), o, t)
     if kind == 0:   # PRIGP trains U and V only (prigp.py:145)
         assert np.array_equal(e.get_table("bias"), b)
     users = np.arange(0, 943, 7, dtype=np.int32)

@@ -501,3 +501,29 @@ def test_fp32_oracle_drift_bounds_cml_tolerance(fold1):
     assert max(r[0] for r in out["cml"]) > 1.0, out          # the strict band is not fp32-attainable
     assert max(r[1] for r in out["cml"]) < 0.75, out         # the relaxed band holds it with headroom
     assert max(r[0] for r in out["bpr"]) < 0.5, out
+
+
+@pytest.mark.parametrize("reg_cov,use_rw", [(1.0, True), (0.0, True), (0.5, False)])
+def test_fp32_oracle_drift_bounds_cml_stream_tolerance(fold1, streams, reg_cov, use_rw):
+    """The same fp32-vs-float64 argument at the shape of the CML step tests
+    (tests/test_gpu_step_parity.py::test_cml_steps_match_oracle,
+    test_gpu_pos_sort.py::test_cml_pos_sort_phased): 40 steps of the
+    reference's captured sampler_ranking stream at B=50, W=5, d=50 -- the
+    oracle in float32 stays inside the relaxed CML band (conftest.CML_TRAJ)
+    with headroom, which is what those tests require of the GPU."""
+    from oracle import cf_oracle as O
+    from conftest import CML_TRAJ, get_stream
+    st = get_stream(streams, "rank_b50_w5")
+    rng = np.random.RandomState(9)
+    U = O.init_table(rng, (943, 50), truncated=False)
+    V = O.init_table(rng, (1682, 50), truncated=False)
+    res = {}
+    for dt in (np.float32, np.float64):
+        T = [U.astype(dt), V.astype(dt), np.full((943, 50), 0.1, dt), np.full((1682, 50), 0.1, dt)]
+        for s in range(40):
+            O.cml_step(T[0], T[1], T[2], T[3], st["pairs"][s], st["negs"][s], 1.0, reg_cov, 1.0,
+                       use_rank_weight=use_rw)
+        res[dt] = T
+    worst = max(float(np.max(np.abs(a.astype(np.float64) - b) / (CML_TRAJ["atol"] + CML_TRAJ["rtol"] * np.abs(b))))
+                for a, b in zip(res[np.float32], res[np.float64]))
+    assert worst < 0.75, worst

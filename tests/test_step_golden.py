@@ -13,6 +13,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import assert_close
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 import sys  # noqa: E402
 sys.path.insert(0, os.path.join(HERE, "golden"))
@@ -73,7 +75,7 @@ def test_engine_lands_on_step_golden(gold, streams, case):
     for t in ("user", "item", "acc_user", "acc_item") + (("bias", "acc_bias") if b is not None else ()):
         x = e.get_table(t)
         rows = gold[name + ("/rows_user" if t in ("user", "acc_user") else "/rows_item")]
-        assert rel(x[rows], gold["%s/f64/%s/rows" % (name, t)]) <= 1e-5, t
+        assert_close(x[rows], gold["%s/f64/%s/rows" % (name, t)], t)
         ck = gold["%s/f64/%s/checksum" % (name, t)]
         assert abs((x.astype(np.float64) ** 2).sum() - ck[1]) <= 1e-5 * ck[1], t
     e.close()
