@@ -12,6 +12,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "cf_kernels.h"
+#include "cf_device.h"
 
 namespace cfk {
 
@@ -109,22 +110,131 @@ __global__ void psort_scatter_kernel(const int32_t* __restrict__ occU, const int
     }
 }
 
-}  // namespace
+// offP = exclusive scan of cntP (positives per item) and offN = exclusive
+// scan of cntV (negatives per item) in two launches of our own: per-tile sums
+// of both arrays, then every tile adds the sums of the tiles before it (read
+// by the whole block, O(tiles) per block -- ~50 tiles at 100K items) to its
+// local scan.  No cross-block publication inside a launch (the look-back
+// forms' XCD-coherence hazards), no library scan's init launch.
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = 8;
+constexpr int kScanTile = kScanThreads * kScanPer;   // 2,048 items per block
 
-size_t psort_scratch(int64_t n_items) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                           (int)n_items);
-    return bytes;
+__global__ __launch_bounds__(kScanThreads) void psort_tile_sum_kernel(const int32_t* __restrict__ cntP,
+                                                                      const int32_t* __restrict__ cntV,
+                                                                      int64_t n, int2* __restrict__ tiles) {
+    __shared__ int s_p[kScanThreads / 64], s_n[kScanThreads / 64];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    int sp = 0, sn = 0;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+        const int64_t k = base + (int64_t)q * kScanThreads + threadIdx.x;   // coalesced
+        if (k < n) {
+            sp += cntP[k];
+            sn += cntV[k];
+        }
+    }
+    sp = wave_sum_i(sp);
+    sn = wave_sum_i(sn);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_p[w] = sp;
+        s_n[w] = sn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tp = 0, tn = 0;
+        for (int k = 0; k < kScanThreads / 64; ++k) {
+            tp += s_p[k];
+            tn += s_n[k];
+        }
+        tiles[blockIdx.x] = make_int2(tp, tn);
+    }
 }
 
+__global__ __launch_bounds__(kScanThreads) void psort_tile_scan_kernel(const int32_t* __restrict__ cntP,
+                                                                       const int32_t* __restrict__ cntV,
+                                                                       int64_t n, const int2* __restrict__ tiles,
+                                                                       int32_t* __restrict__ offP,
+                                                                       int32_t* __restrict__ offN) {
+    __shared__ int s_p[kScanThreads / 64], s_n[kScanThreads / 64];
+    __shared__ int s_bp, s_bn;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the tiles before this one, summed by the whole block
+    int bp = 0, bn = 0;
+    for (int t = threadIdx.x; t < (int)blockIdx.x; t += kScanThreads) {
+        const int2 v = tiles[t];
+        bp += v.x;
+        bn += v.y;
+    }
+    bp = wave_sum_i(bp);
+    bn = wave_sum_i(bn);
+    if (lane == 0) {
+        s_p[w] = bp;
+        s_n[w] = bn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tp = 0, tn = 0;
+        for (int k = 0; k < kScanThreads / 64; ++k) {
+            tp += s_p[k];
+            tn += s_n[k];
+        }
+        s_bp = tp;
+        s_bn = tn;
+    }
+    __syncthreads();
+    // this thread's kScanPer consecutive items, scanned locally
+    const int64_t k0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+    int vp[kScanPer], vn[kScanPer];
+    int tp = 0, tn = 0;
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+        const bool ok = k0 + q < n;
+        vp[q] = ok ? cntP[k0 + q] : 0;
+        vn[q] = ok ? cntV[k0 + q] : 0;
+        tp += vp[q];
+        tn += vn[q];
+    }
+    const int ip = wave_incl_scan(tp), in = wave_incl_scan(tn);
+    __syncthreads();   // s_p / s_n reused: wave totals
+    if (lane == 63) {
+        s_p[w] = ip;
+        s_n[w] = in;
+    }
+    __syncthreads();
+    int ep = s_bp + ip - tp, en = s_bn + in - tn;
+    for (int k = 0; k < w; ++k) {
+        ep += s_p[k];
+        en += s_n[k];
+    }
+#pragma unroll
+    for (int q = 0; q < kScanPer; ++q) {
+        if (k0 + q < n) {
+            offP[k0 + q] = ep;
+            offN[k0 + q] = en;
+        }
+        ep += vp[q];
+        en += vn[q];
+    }
+}
+
+int psort_tiles(int64_t n_items) { return (int)((n_items + kScanTile - 1) / kScanTile); }
+
+}  // namespace
+
+size_t psort_scratch(int64_t n_items) { return (size_t)psort_tiles(n_items) * sizeof(int2); }
+
 hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
-                        int B, int W, const int32_t* cntP, int32_t* offP, int32_t* srec, int64_t n_items,
-                        void* tmp, size_t tmp_bytes, hipStream_t s) {
+                        int B, int W, const int32_t* cntP, int32_t* offP, const int32_t* cntV, int32_t* offN,
+                        int32_t* srec, int64_t n_items, void* tmp, size_t tmp_bytes, hipStream_t s) {
     if (B <= 0) return hipSuccess;
-    size_t bytes = tmp_bytes;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, bytes, cntP, offP, (int)n_items, s);
-    if (e != hipSuccess) return e;
+    const int nt = psort_tiles(n_items);
+    if (tmp_bytes < (size_t)nt * sizeof(int2)) return hipErrorInvalidValue;
+    int2* tiles = reinterpret_cast<int2*>(tmp);
+    hipLaunchKernelGGL(psort_tile_sum_kernel, dim3(nt), dim3(kScanThreads), 0, s, cntP, cntV, n_items, tiles);
+    hipLaunchKernelGGL(psort_tile_scan_kernel, dim3(nt), dim3(kScanThreads), 0, s, cntP, cntV, n_items, tiles,
+                       offP, offN);
     switch (W) {
         case 1: hipLaunchKernelGGL(psort_scatter_kernel<1>, dim3(grid_of(B)), dim3(256), 0, s, occU, rankU, occV,
                                    rankV, B, offP, srec); break;

@@ -108,9 +108,11 @@ struct cf_engine {
     int capP = 8;
     int32_t* cntP_[2] = {nullptr, nullptr};
     int32_t* offP = nullptr;          // [n_items]
+    int32_t* offN = nullptr;          // [n_items] exclusive scan of the negatives' counts
     int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
     int order_cap = 0;
     float* slotP = nullptr;           // [n_items * capP, d]
+    float* slotN = nullptr;           // [order_cap * n_neg, d] compact negative slot rows (offN[j] + rank)
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
     bool slots_ready = false;
@@ -308,12 +310,14 @@ int ensure_slots(cf_engine* e) {
     dfree(e->GVrep);
     dfree(e->slotP);
     dfree(e->offP);
+    dfree(e->offN);
     for (int k = 0; k < 2; ++k) dfree(e->cntP_[k]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     e->psort_tmp = nullptr;
     if (psort_possible(e)) {
         CF_TRY(dalloc(&e->slotP, (size_t)c.n_items * e->capP * c.n_factors));
         CF_TRY(dalloc(&e->offP, (size_t)c.n_items));
+        CF_TRY(dalloc(&e->offN, (size_t)c.n_items));
         for (int k = 0; k < 2; ++k) {
             CF_TRY(dalloc(&e->cntP_[k], (size_t)c.n_items));
             CF_HIP(hipMemsetAsync(e->cntP_[k], 0, (size_t)c.n_items * 4, e->stream));
@@ -425,7 +429,9 @@ int ensure_order(cf_engine* e, int B) {
     CF_HIP(hipStreamSynchronize(e->stream));
     CF_HIP(hipStreamSynchronize(e->side));
     dfree(e->srec);
+    dfree(e->slotN);
     CF_TRY(dalloc(&e->srec, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg)));
+    CF_TRY(dalloc(&e->slotN, (size_t)std::max(B, e->Bcap) * e->cfg.n_neg * e->cfg.n_factors));
     // in-range ids from the start (a given-up fused scatter leaves old records)
     CF_HIP(hipMemsetAsync(e->srec, 0, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg) * 4, e->stream));
     e->order_cap = std::max(B, e->Bcap);
@@ -507,6 +513,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.srec = e->srec;
         a.slotP = e->slotP;
         a.capP = e->capP;
+        a.offN = e->offN;
+        a.slotV = e->slotN;   // negatives: compact slots offN[j] + rank
     }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
@@ -698,7 +706,14 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         p.slotP = a.slotP;
         p.capP = a.capP;
         p.nPos = B;
+        p.offN = a.offN;
+        // visit every row of a table that is not much larger than the batch's
+        // occurrences of it (cfg2 at 2^19: 100K items / 1.05M occurrences,
+        // 1M users / 524K), else find the owners among the occurrences
+        p.dense_items = c.n_items <= 2 * (int64_t)B * items_per_pair(c) ? 1 : 0;
+        p.dense_users = c.n_users <= 2 * (int64_t)B * users_per_pair(c) ? 1 : 0;
     }
+    p.n_users = c.n_users;
     if (e->det) {
         p.hotP = e->hotP;
         p.hotPb = e->hotPb;
@@ -782,8 +797,8 @@ int det_hot(cf_engine* e, const StepArgs& a) {
 int psort(cf_engine* e, const StepArgs& a) {
     if (a.srec == nullptr) return CF_OK;
     ProfScope ps(e, CF_K_PSORT);
-    CF_HIP(launch_psort(a.occU, a.rankU, a.occV, a.rankV, a.B, a.W, a.cntP, e->offP, e->srec, e->cfg.n_items,
-                        e->psort_tmp, e->psort_tmp_bytes, e->stream));
+    CF_HIP(launch_psort(a.occU, a.rankU, a.occV, a.rankV, a.B, a.W, a.cntP, e->offP, a.cntV, e->offN, e->srec,
+                        e->cfg.n_items, e->psort_tmp, e->psort_tmp_bytes, e->stream));
     return CF_OK;
 }
 
@@ -1176,7 +1191,7 @@ int cf_destroy(cf_engine* e) {
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
     dfree(e->hotP); dfree(e->hotPb);
-    dfree(e->slotP); dfree(e->offP); dfree(e->srec); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
+    dfree(e->slotP); dfree(e->offP); dfree(e->offN); dfree(e->srec); dfree(e->slotN); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);

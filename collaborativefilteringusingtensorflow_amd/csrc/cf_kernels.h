@@ -120,6 +120,11 @@ struct StepArgs {
     const int32_t* __restrict__ srec;
     float* __restrict__ slotP;          // [n_items * capP, d]
     int capP;
+    // ... and the negatives in compact slots: with pos_sort, slotV is the
+    // [B * W, d] array where negative occurrence k (rank < kRankCap) of item
+    // j stores its gradient row at offN[j] + k (offN = exclusive scan of the
+    // negatives' counts cntV), so an item's negative rows are contiguous
+    const int32_t* __restrict__ offN;   // [n_items]
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
     // occU until the exchange recodes it -1 - (its row in xrows / xgrads)
@@ -140,6 +145,10 @@ constexpr int32_t kRemoteFlag = 1 << 24;
 // per 16-lane group): partial k of an item covers the positions of block
 // offP[i] / kPsortPPB + k
 constexpr int kPsortPPB = kGroupsPerBlock;
+// occurrence ranks ride in 16 bits in the pos_sort records: a negative of
+// rank >= kRankCap (a row seen 65,535+ times as a negative) adds by float
+// atomics instead of a compact slot
+constexpr int kRankCap = 0xFFFF;
 // ints per record, int4-aligned: W = 1 -> 4 (16 B), W = 5 -> 12 (48 B)
 __host__ __device__ constexpr int psort_stride(int W) { return (2 + W + (2 + W) / 2 + 3) & ~3; }
 
@@ -189,12 +198,19 @@ struct ApplyArgs {
     // between its head and tail slots
     const float* __restrict__ hotP;      // [tiles, d]
     const float* __restrict__ hotPb;     // [tiles] records: the tile's beta sum
-    // positive-sorted gradient (StepArgs): positives are occV[0, nPos)
+    // positive-sorted gradient (StepArgs): positives are occV[0, nPos);
+    // negatives' compact slot rows at slotV[offN[r] + k]
     int32_t* __restrict__ cntP;
     const int32_t* __restrict__ offP;
     const float* __restrict__ slotP;
     int capP;
     int64_t nPos;
+    const int32_t* __restrict__ offN;
+    // pos_sort apply: visit every item row (dense_items) / every user row
+    // (dense_users) instead of finding the owners among the occurrences --
+    // when the table is not much larger than the batch's occurrences of it
+    int dense_items, dense_users;
+    int64_t n_users;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -332,12 +348,13 @@ hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
                             hipStream_t s);
-// positive-sorted gradient: offP = exclusive scan of cntP (hipCUB), then
-// order[offP[i_p] + rankV[p]] = p for the B pairs; tmp sized by psort_scratch
+// positive-sorted gradient: offP / offN = exclusive scans of cntP / cntV
+// (two launches of tile sums + tile scans), then the pair records at
+// srec[offP[i_p] + rankV[p]] for the B pairs; tmp sized by psort_scratch
 size_t psort_scratch(int64_t n_items);
 hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
-                        int B, int W, const int32_t* cntP, int32_t* offP, int32_t* srec, int64_t n_items,
-                        void* tmp, size_t tmp_bytes, hipStream_t s);
+                        int B, int W, const int32_t* cntP, int32_t* offP, const int32_t* cntV, int32_t* offN,
+                        int32_t* srec, int64_t n_items, void* tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
                                 uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,

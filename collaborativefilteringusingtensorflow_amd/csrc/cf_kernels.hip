@@ -34,6 +34,8 @@
 // Reference semantics: src/models/pl/models/bprmf.py:52-88,
 // gbprmf.py:58-106, cml.py:55-129, src/models/others/models/amf.py:66-162;
 // samplers src/samplers/sampler_ranking.py:22-37, sampler_gbpr.py:23-43.
+#include <algorithm>
+
 #include "cf_kernels.h"
 #include "cf_device.h"
 
@@ -1107,6 +1109,7 @@ struct PairRows {
     int p, u, i, cu, ci, ru, ri;
     int oi;   // pos_sort: offP[i], the item's first positive-sorted position
     int j[WT], cj[WT], rj[WT];
+    int oj[WT];   // pos_sort: offN[j], the negative's first compact slot
     int g[NGA], cg[NGA], rg[NGA];
     int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
     float uu[EPL], vi[EPL], au[EPL], ai[EPL];
@@ -1161,7 +1164,10 @@ struct PairRows {
             ci = a.cntV[i] + a.cntP[i];
             oi = a.offP[i];
 #pragma unroll
-            for (int w = 0; w < WT; ++w) cj[w] = a.cntV[j[w]] + a.cntP[j[w]];
+            for (int w = 0; w < WT; ++w) {
+                cj[w] = a.cntV[j[w]] + a.cntP[j[w]];
+                oj[w] = a.offN[j[w]];
+            }
         } else {
             ci = a.count_items ? a.cntV[i] : 0;
 #pragma unroll
@@ -1182,11 +1188,18 @@ struct PairRows {
             for (int w = 0; w < WT; ++w) bj[w] = a.b[j[w]];
         }
     }
+    template <bool SORT = false>
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
         su = slot_of(cu, u, ru, a.capU, 0, a.offU);
         si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
+        if constexpr (SORT) {   // compact negative slots offN[j] + rank (slotV = [B * W, d])
 #pragma unroll
-        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
+            for (int w = 0; w < WT; ++w)
+                sj[w] = (cj[w] >= 2 && rj[w] < kRankCap) ? (int64_t)oj[w] + rj[w] : -1;
+        } else {
+#pragma unroll
+            for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
+        }
 #pragma unroll
         for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0, a.offU);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
@@ -1436,7 +1449,7 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
         if (ok[k]) pr[k].template load_rows<SORT>(a, gl);
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        if (ok[k]) pr[k].load_acc(a, gl);
+        if (ok[k]) pr[k].template load_acc<SORT>(a, gl);
 #pragma unroll
     for (int k = 0; k < P; ++k)
         if (ok[k]) pr[k].template update<SORT>(a, gl, loss_g, sq, SORT ? &s_gi[grp][0] : nullptr);
@@ -1660,8 +1673,12 @@ __device__ __forceinline__ void rows_sum(const float* __restrict__ S, int64_t s0
     }
 }
 
+#ifndef CF_APPLY_NF_PS
+#define CF_APPLY_NF_PS 8   // rows in flight per group in the pos_sort item apply
+#endif
 template <int EPL>
-__device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int gl) {
+__device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int gl, int cn, int cp, int o,
+                                              int on) {
     // multi-rank item reduce: the summed row goes to GV for the exchange
     const bool reduce_only = a.items_grad_only;
     float x[EPL], acc[EPL], g[EPL];
@@ -1669,14 +1686,35 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
         gload<EPL>(a.V, r, a.d, gl, x);
         gload_acc<EPL>(a.AV, r, a.d, gl, true, acc);
     }
-    const int cn = a.cntV[r], cp = a.cntP[r];
-    const int o = a.offP[r];
     const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
+    const int nn = cn < kRankCap ? cn : kRankCap;
+    const int npp = np < a.capP ? np : a.capP;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
-    rows_sum<EPL>(a.slotV, r * (int64_t)a.capV, cn < a.capV ? cn : a.capV, a.d, gl, g);
-    rows_sum<EPL>(a.slotP, r * (int64_t)a.capP, np < a.capP ? np : a.capP, a.d, gl, g);
-    if (cn > a.capV || np > a.capP) {
+    // the negatives' compact slot rows [on, on + nn) in rank order (contiguous),
+    // then the positives' partial rows in block order: all independent loads,
+    // NF of them in flight
+    const int nt = nn + npp;
+    constexpr int NF = CF_APPLY_NF_PS;
+    for (int t0 = 0; t0 < nt; t0 += NF) {
+        float h[NF][EPL];
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            const int t = t0 + q;
+            if (t < nt) {
+                const float* row = t < nn ? a.slotV + ((int64_t)on + t) * a.d
+                                          : a.slotP + (r * a.capP + (t - nn)) * (int64_t)a.d;
+                row_ld<EPL>(row, a.d, gl, 0.f, h[q]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NF; ++q)
+            if (t0 + q < nt) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
+            }
+    }
+    if (cn > kRankCap || np > a.capP) {   // what overflowed either range: float atomics into GV
         float h[EPL];
         gload<EPL>(a.GV, r, a.d, gl, h);
 #pragma unroll
@@ -1690,6 +1728,129 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
     if (gl == 0) {
         a.cntV[r] = 0;
         a.cntP[r] = 0;
+    }
+}
+
+// block 0 of an apply launch folds the gradient launch's loss partials in a
+// fixed order (eight partials in flight per lane, not a chain of loads)
+template <int BS>
+__device__ __forceinline__ void fold_loss(const ApplyArgs& a) {
+    constexpr int NWV = BS / kWave;
+    __shared__ double s_red[NWV];
+    const int lane = lane_id();
+    const int wv = threadIdx.x >> 6;
+    double t = 0.0;
+    for (int k0 = threadIdx.x; k0 < a.n_partial; k0 += 8 * BS) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int k = k0 + q * BS;
+            v[q] = k < a.n_partial ? a.loss_partial[k] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t += v[q];
+    }
+    t = wave_sum_d(t);
+    if (lane == 0) s_red[wv] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double tt = 0.0;
+        for (int w = 0; w < NWV; ++w) tt += s_red[w];
+        a.loss_acc[0] += tt;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pos_sort apply (apply_ps_kernel).  A duplicated item's gradient is its
+// negatives' compact slot rows (rank order) + its positive partials (block
+// order) + the float-atomic sum of what overflowed either range -- TF1's
+// dedup-sum (bprmf.py:83-88) -- then Adagrad and both counts reset.
+//  * dense items: one 16-lane group per item row (at the bench batch 99 % of
+//    the items are duplicated): its counts and offsets, then every row it
+//    sums, in one round of independent loads -- no owner detection chain;
+//  * wave blocks: 64 candidates per wave -- every user row (dense users:
+//    one coalesced count load per wave), or the batch's user / item
+//    occurrences (an owner is a rank-0 occurrence with count >= 2; for items
+//    the rank-0 positive when the item has positives in the batch, from the
+//    immutable offP, else the rank-0 negative) -- ballot-compacted and taken
+//    by the wave's four groups four at a time (no LDS, no barrier).
+// ---------------------------------------------------------------------------
+template <int EPL>
+__device__ __forceinline__ void apply_ps_item_block(const ApplyArgs& a, int block) {
+    const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
+    const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
+    if (r >= a.n_items) return;
+    const int cn = a.cntV[r], cp = a.cntP[r], o = a.offP[r], on = a.offN[r];
+    if (cn + cp < 2) return;   // untouched, or seen once (applied by the gradient launch)
+    apply_item_ps<EPL>(a, r, gl, cn, cp, o, on);
+}
+
+template <int EPL>
+__device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) {
+    const int lane = lane_id(), gw = lane >> 4, gl = lane & (kGL - 1);
+    const int64_t nUw = !a.count_users ? 0 : a.dense_users ? a.n_users : a.nU;
+    const int64_t nVw = (a.count_items && !a.dense_items) ? a.nV : 0;
+    const int64_t q = wave * kWave + lane;
+    int row = -1, isU = 0, c = 0;
+    if (q < nUw) {
+        if (a.dense_users) {
+            c = a.cntU[q];
+            if (c >= 2) row = (int)q;
+        } else {
+            const int rk = a.rankU[q], r = a.occU[q];
+            if (rk == 0 && r >= 0) {
+                c = a.cntU[r];
+                if (c >= 2) row = r;
+            }
+        }
+        isU = 1;
+    } else if (q < nUw + nVw) {
+        const int64_t k = q - nUw;
+        const int rk = a.rankV[k], r = a.occV[k];
+        if (rk == 0) {
+            // the rank-0 positive owns an item with positives in the batch
+            // (offP[r+1] - offP[r] > 0, immutable during the launch), else the
+            // rank-0 negative
+            const int64_t o0 = a.offP[r];
+            const int64_t o1 = (int64_t)r + 1 < a.n_items ? (int64_t)a.offP[r + 1] : a.nPos;
+            if ((k < a.nPos) == (o1 > o0)) {
+                c = a.cntV[r] + a.cntP[r];
+                if (c >= 2) row = r;
+            }
+        }
+    }
+    unsigned long long m = __ballot(row >= 0);
+    while (m != 0ull) {   // wave-uniform: four owners per round, one per group
+        unsigned long long mm = m;
+        for (int k = 0; k < gw; ++k) mm &= mm - 1ull;
+        const int src = mm != 0ull ? __ffsll((long long)mm) - 1 : 0;
+        const bool have = mm != 0ull;
+        for (int k = 0; k < 4; ++k) m &= m - 1ull;
+        const int rr = __shfl(row, src, kWave);
+        const int ru = __shfl(isU, src, kWave);
+        const int cc = __shfl(c, src, kWave);
+        if (!have) continue;   // group-uniform
+        if (ru) {
+            apply_row<EPL>(a, rr, true, cc, gl);
+        } else {
+            const int cn = a.cntV[rr], cp = a.cntP[rr], o = a.offP[rr], on = a.offN[rr];
+            apply_item_ps<EPL>(a, rr, gl, cn, cp, o, on);
+        }
+    }
+}
+
+// grid: [0, nbI) dense item blocks, [nbI, nbI + nbW) wave blocks, then (with
+// DRAW) the draw + count blocks of the next step (other buffer set)
+template <int EPL, bool DRAW>
+__global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
+    const int b = blockIdx.x;
+    if (b == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
+    if (b < nbI) {
+        apply_ps_item_block<EPL>(p, b);
+    } else if (b < nbI + nbW) {
+        apply_ps_wave<EPL>(p, (int64_t)(b - nbI) * kWavesPerBlock + (threadIdx.x >> 6));
+    } else if constexpr (DRAW) {
+        prep_any<BPR>(nx, b - nbI - nbW);
     }
 }
 
@@ -1780,35 +1941,13 @@ constexpr int kApplyDetectWaves = CF_APPLY_DETECT_WAVES;
 constexpr int kApplyChunk = CF_APPLY_CHUNK;
 
 // BS = workgroup size (256, or 64 for one-wave apply blocks)
-template <int EPL, int BS = kBlock, bool HOT = false, bool PS = false>
+template <int EPL, int BS = kBlock, bool HOT = false>
 __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nblocks) {
     constexpr int NWV = BS / kWave, NGR = BS / kGL;
-    __shared__ double s_red[NWV];
     const int lane = lane_id();
     const int wv = threadIdx.x >> 6;
     const int gl = lane & (kGL - 1);
-    if (block == 0 && a.loss_acc != nullptr) {
-        // fixed order; eight partials in flight per lane, not a chain of loads
-        double t = 0.0;
-        for (int k0 = threadIdx.x; k0 < a.n_partial; k0 += 8 * BS) {
-            double v[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int k = k0 + q * BS;
-                v[q] = k < a.n_partial ? a.loss_partial[k] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) t += v[q];
-        }
-        t = wave_sum_d(t);
-        if (lane == 0) s_red[wv] = t;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            double tt = 0.0;
-            for (int w = 0; w < NWV; ++w) tt += s_red[w];
-            a.loss_acc[0] += tt;
-        }
-    }
+    if (block == 0 && a.loss_acc != nullptr) fold_loss<BS>(a);
     // a block takes kApplyDetectWaves x 64 work items at a time: those waves
     // find their owners (~18 % of the occurrences at cfg2), then the block's
     // 16 groups apply them round-robin
@@ -1839,23 +1978,8 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 const int64_t k = q - nU;
                 if (a.rankV[k] == 0) {
                     const int32_t r = a.occV[k];
-                    if constexpr (PS) {
-                        // owner: the rank-0 positive of an item with positives
-                        // in the batch, else its rank-0 negative.  Which class
-                        // owns comes from offP (offP[r+1] - offP[r] = the
-                        // item's positives), never from a count: an owner
-                        // resets cntV / cntP while other waves still detect,
-                        // so a rule on cntV == 0 could crown a second owner
-                        const int64_t o0 = a.offP[r];
-                        const int64_t o1 = (int64_t)r + 1 < a.n_items ? (int64_t)a.offP[r + 1] : a.nPos;
-                        if ((k < a.nPos) == (o1 > o0)) {
-                            c = a.cntV[r] + a.cntP[r];
-                            if (c >= 2) row = r;
-                        }
-                    } else {
-                        c = a.cntV[r];
-                        if (c >= 2) row = r;
-                    }
+                    c = a.cntV[r];
+                    if (c >= 2) row = r;
                 }
             } else if (q < total) {
                 const int64_t k = q - nU - nV;
@@ -1887,18 +2011,15 @@ __device__ __forceinline__ void apply_body(const ApplyArgs& a, int block, int nb
                 rem -= c;
             }
             if (src < 0) break;  // group-uniform
-            if (PS && s_isU[src] == 0)
-                apply_item_ps<EPL>(a, s_row[src], gl);
-            else
-                apply_row<EPL, HOT>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
+            apply_row<EPL, HOT>(a, s_row[src], s_isU[src] != 0, s_cnt[src], gl);
         }
         __syncthreads();  // s_* reused by the next chunk
     }
 }
 
-template <int EPL, bool HOT, bool PS = false>
+template <int EPL, bool HOT>
 __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
-    apply_body<EPL, kBlock, HOT, PS>(a, blockIdx.x, gridDim.x);
+    apply_body<EPL, kBlock, HOT>(a, blockIdx.x, gridDim.x);
 }
 
 // one-wave apply blocks: the detecting wave's own four groups apply its owners
@@ -1910,7 +2031,7 @@ __global__ __launch_bounds__(kWave) void apply_wave_kernel(ApplyArgs a) {
 // horizontal fusion on the device-sampler path: apply of step s (blocks
 // [0, napply)) beside the draw + count of step s+1 (the rest) -- independent
 // work (other buffer set), one launch instead of two
-template <int EPL, int MODEL, bool HOT, bool PS = false>
+template <int EPL, int MODEL, bool HOT>
 #ifndef CF_APPLY_PREP_ORDER
 #define CF_APPLY_PREP_ORDER 0  // 0: apply blocks first, 1: draw blocks first, 2: interleaved
 #endif
@@ -1923,15 +2044,15 @@ __global__ __launch_bounds__(kBlock) void apply_prep_kernel(ApplyArgs p, StepArg
     if (minor_block(blockIdx.x, napply, nprep, idx))
         prep_any<MODEL>(a, idx);
     else
-        apply_body<EPL, kBlock, HOT, PS>(p, idx, napply);
+        apply_body<EPL, kBlock, HOT>(p, idx, napply);
 #elif CF_APPLY_PREP_ORDER == 1
     if ((int)blockIdx.x < nprep)
         prep_any<MODEL>(a, blockIdx.x);
     else
-        apply_body<EPL, kBlock, HOT, PS>(p, blockIdx.x - nprep, napply);
+        apply_body<EPL, kBlock, HOT>(p, blockIdx.x - nprep, napply);
 #else
     if ((int)blockIdx.x < napply)
-        apply_body<EPL, kBlock, HOT, PS>(p, blockIdx.x, napply);
+        apply_body<EPL, kBlock, HOT>(p, blockIdx.x, napply);
     else
         prep_any<MODEL>(a, blockIdx.x - napply);
 #endif
@@ -2362,15 +2483,44 @@ static int apply_grid(const ApplyArgs& a) {
 #define CF_APPLY_WAVE_BLOCKS 0
 #endif
 
-template <bool HOT, bool PS = false>
+template <bool HOT>
 static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
     const dim3 grid(apply_grid(a)), block(kBlock);
     switch (epl_for(a.d)) {
-        case 1: hipLaunchKernelGGL((apply_kernel<1, HOT, PS>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((apply_kernel<2, HOT, PS>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((apply_kernel<4, HOT, PS>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((apply_kernel<8, HOT, PS>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((apply_kernel<16, HOT, PS>), grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((apply_kernel<1, HOT>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((apply_kernel<2, HOT>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((apply_kernel<4, HOT>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((apply_kernel<8, HOT>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((apply_kernel<16, HOT>), grid, block, 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+// the pos_sort apply (+ the next step's draw when nx is given)
+static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
+    const int64_t nUw = !p.count_users ? 0 : p.dense_users ? p.n_users : p.nU;
+    const int64_t nVw = (p.count_items && !p.dense_items) ? p.nV : 0;
+    const int64_t nbI64 = (p.count_items && p.dense_items) ? (p.n_items + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
+    const int64_t nbW64 = (nUw + nVw + kBlock - 1) / kBlock;
+    const int np = prep_blocks(nx);
+    if (nbI64 + nbW64 + np > INT32_MAX) return hipErrorInvalidValue;
+    const int nbI = (int)nbI64, nbW = (int)std::max<int64_t>(nbW64, nbI64 == 0 ? 1 : 0);   // block 0 folds the loss
+    const dim3 grid(nbI + nbW + np), block(kBlock);
+    const StepArgs n = nx ? *nx : StepArgs{};
+    if (np > 0) {
+        switch (epl_for(p.d)) {
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, true>), grid, block, 0, s, p, n, nbI, nbW); break;
+        }
+    } else {
+        switch (epl_for(p.d)) {
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, false>), grid, block, 0, s, p, n, nbI, nbW); break;
+        }
     }
     return hipGetLastError();
 }
@@ -2390,21 +2540,24 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (a.cntP != nullptr) return a.hotP != nullptr ? hipErrorInvalidValue : launch_apply_h<false, true>(a, s);
+    if (a.cntP != nullptr) {   // pos_sort (d <= 128, no served rows, no deterministic tiles)
+        if (a.hotP != nullptr || a.nS > 0 || epl_for(a.d) > 8) return hipErrorInvalidValue;
+        return launch_apply_ps(a, nullptr, s);
+    }
     return a.hotP != nullptr ? launch_apply_h<true>(a, s) : launch_apply_h<false>(a, s);
 }
 
-template <int MODEL, bool HOT, bool PS = false>
+template <int MODEL, bool HOT>
 static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     const int na = apply_grid(p);
     const int np = prep_blocks(&a);
     const dim3 grid(na + np), block(kBlock);
     switch (epl_for(p.d)) {
-        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
-        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
-        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
-        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
-        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL, HOT, PS>), grid, block, 0, s, p, a, na); break;
+        case 1: hipLaunchKernelGGL((apply_prep_kernel<1, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 2: hipLaunchKernelGGL((apply_prep_kernel<2, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 4: hipLaunchKernelGGL((apply_prep_kernel<4, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        case 8: hipLaunchKernelGGL((apply_prep_kernel<8, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
+        default: hipLaunchKernelGGL((apply_prep_kernel<16, MODEL, HOT>), grid, block, 0, s, p, a, na); break;
     }
     return hipGetLastError();
 }
@@ -2412,8 +2565,8 @@ static hipError_t launch_apply_prep_m(const ApplyArgs& p, const StepArgs& a, hip
 hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t s) {
     if (a.B <= 0) return launch_apply(p, s);
     if (p.cntP != nullptr)   // pos_sort: BPR / AMF / CML (their draw is prep_body<BPR>)
-        return (p.hotP != nullptr || a.model == GBPR) ? hipErrorInvalidValue
-                                                      : launch_apply_prep_m<BPR, false, true>(p, a, s);
+        return (p.hotP != nullptr || p.nS > 0 || a.model == GBPR || epl_for(p.d) > 8)
+                   ? hipErrorInvalidValue : launch_apply_ps(p, &a, s);
     if (p.hotP != nullptr)
         return a.model == GBPR ? launch_apply_prep_m<GBPR, true>(p, a, s) : launch_apply_prep_m<BPR, true>(p, a, s);
     return a.model == GBPR ? launch_apply_prep_m<GBPR, false>(p, a, s) : launch_apply_prep_m<BPR, false>(p, a, s);
