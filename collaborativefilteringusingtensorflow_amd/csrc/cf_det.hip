@@ -73,45 +73,62 @@ int grid_of(int64_t n) {
 }
 
 // positive-sorted gradient: pair p goes to position offP[i_p] + its rank
-// among the batch's positives of i_p (counting sort by positive item), as
-// one record of psort_stride(W) ints:
-//   [u, i, j_0 .. j_{W-1}, (ru | rj0 << 16), (rj1 | rj2 << 16), .., 0 padding]
-// -- the ranks of u and of the negatives as 16-bit halves (clamped to
-// 0xFFFF), ru in the low half of the first rank word (load_idx_sorted)
-__device__ __forceinline__ int32_t rank16(int32_t r) { return r < 0xFFFF ? r : 0xFFFF; }
-
+// among the batch's positives of i_p (counting sort by positive item), as one
+// record of psort_stride(W) ints (cf_kernels.h): the ids plus every
+// occurrence's resolved destination, from the final counts and offsets
 template <int W>
-__global__ void psort_scatter_kernel(const int32_t* __restrict__ occU, const int32_t* __restrict__ rankU,
-                                     const int32_t* __restrict__ occV, const int32_t* __restrict__ rankV,
-                                     int B, const int32_t* __restrict__ offP, int32_t* __restrict__ srec) {
+__global__ __launch_bounds__(256) void psort_scatter_kernel(PsortArgs a) {
     constexpr int RS = psort_stride(W);
     const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
     const int nt = gridDim.x * blockDim.x;
+    const int B = a.B;
     for (int p = t0; p < B; p += nt) {
-        const int32_t i = occV[p];
-        int32_t v[RS], rk[W + 2];
-        v[0] = occU[p];
-        v[1] = i;
-        rk[0] = rank16(rankU[p]);
-        rk[W + 1] = 0;
+        // coalesced: the pair's ids and ranks
+        const int32_t u = a.occU[p], i = a.occV[p], ru = a.rankU[p], rp = a.rankV[p];
+        int32_t j[W], rj[W];
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const int64_t q = (int64_t)B + (int64_t)p * W + w;
-            v[2 + w] = occV[q];
-            rk[1 + w] = rank16(rankV[q]);
+            j[w] = a.occV[q];
+            rj[w] = a.rankV[q];
         }
+        // one round of independent random loads: the user's count, and per
+        // item two adjacent (offP, offN) entries -- offsets and counts at once
+        const int32_t cu = a.cntU[u];
+        const int2 i0 = a.offPN[i], i1 = a.offPN[i + 1];
+        int2 j0[W], j1[W];
 #pragma unroll
-        for (int k = 0; k < (W + 2) / 2; ++k) v[2 + W + k] = rk[2 * k] | (rk[2 * k + 1] << 16);
+        for (int w = 0; w < W; ++w) {
+            j0[w] = a.offPN[j[w]];
+            j1[w] = a.offPN[j[w] + 1];
+        }
+        const int32_t oP = i0.x, ci = (i1.x - i0.x) + (i1.y - i0.y);
+        int32_t cj[W], oN[W];
 #pragma unroll
-        for (int k = 2 + W + (W + 2) / 2; k < RS; ++k) v[k] = 0;
-        int4* r = reinterpret_cast<int4*>(srec + (int64_t)(offP[i] + rankV[p]) * RS);
+        for (int w = 0; w < W; ++w) {
+            cj[w] = (j1[w].x - j0[w].x) + (j1[w].y - j0[w].y);
+            oN[w] = j0[w].y;
+        }
+        int32_t v[RS];
+        v[0] = u;
+        v[1] = i;
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[2 + w] = j[w];
+        v[2 + W] = cu == 1 ? kSlotApply : ru < a.capU ? u * a.capU + ru : kSlotAtomic;
+        v[3 + W] = (int32_t)((uint32_t)oP | (ci == 1 ? 0x80000000u : 0u));
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[4 + W + w] = cj[w] == 1 ? kSlotApply : oN[w] + rj[w];
+#pragma unroll
+        for (int k = 4 + 2 * W; k < RS; ++k) v[k] = 0;
+        int4* r = reinterpret_cast<int4*>(a.srec + (int64_t)(oP + rp) * RS);
 #pragma unroll
         for (int k = 0; k < RS / 4; ++k) r[k] = make_int4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
 }
 
-// offP = exclusive scan of cntP (positives per item) and offN = exclusive
-// scan of cntV (negatives per item) in two launches of our own: per-tile sums
+// offPN[r] = (offP[r], offN[r]), the exclusive scans of cntP (positives per
+// item) and cntV (negatives per item), r <= n items (the last entry holds the
+// totals), in two launches of our own: per-tile sums
 // of both arrays, then every tile adds the sums of the tiles before it (read
 // by the whole block, O(tiles) per block -- ~50 tiles at 100K items) to its
 // local scan.  No cross-block publication inside a launch (the look-back
@@ -155,8 +172,7 @@ __global__ __launch_bounds__(kScanThreads) void psort_tile_sum_kernel(const int3
 __global__ __launch_bounds__(kScanThreads) void psort_tile_scan_kernel(const int32_t* __restrict__ cntP,
                                                                        const int32_t* __restrict__ cntV,
                                                                        int64_t n, const int2* __restrict__ tiles,
-                                                                       int32_t* __restrict__ offP,
-                                                                       int32_t* __restrict__ offN) {
+                                                                       int2* __restrict__ offPN) {
     __shared__ int s_p[kScanThreads / 64], s_n[kScanThreads / 64];
     __shared__ int s_bp, s_bn;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -210,36 +226,30 @@ __global__ __launch_bounds__(kScanThreads) void psort_tile_scan_kernel(const int
     }
 #pragma unroll
     for (int q = 0; q < kScanPer; ++q) {
-        if (k0 + q < n) {
-            offP[k0 + q] = ep;
-            offN[k0 + q] = en;
-        }
+        if (k0 + q <= n) offPN[k0 + q] = make_int2(ep, en);   // [n] = the totals
         ep += vp[q];
         en += vn[q];
     }
 }
 
-int psort_tiles(int64_t n_items) { return (int)((n_items + kScanTile - 1) / kScanTile); }
+// n_items + 1 entries: the last one holds the totals
+int psort_tiles(int64_t n_items) { return (int)((n_items + 1 + kScanTile - 1) / kScanTile); }
 
 }  // namespace
 
 size_t psort_scratch(int64_t n_items) { return (size_t)psort_tiles(n_items) * sizeof(int2); }
 
-hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
-                        int B, int W, const int32_t* cntP, int32_t* offP, const int32_t* cntV, int32_t* offN,
-                        int32_t* srec, int64_t n_items, void* tmp, size_t tmp_bytes, hipStream_t s) {
-    if (B <= 0) return hipSuccess;
-    const int nt = psort_tiles(n_items);
+hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    const int nt = psort_tiles(a.n_items);
     if (tmp_bytes < (size_t)nt * sizeof(int2)) return hipErrorInvalidValue;
     int2* tiles = reinterpret_cast<int2*>(tmp);
-    hipLaunchKernelGGL(psort_tile_sum_kernel, dim3(nt), dim3(kScanThreads), 0, s, cntP, cntV, n_items, tiles);
-    hipLaunchKernelGGL(psort_tile_scan_kernel, dim3(nt), dim3(kScanThreads), 0, s, cntP, cntV, n_items, tiles,
-                       offP, offN);
-    switch (W) {
-        case 1: hipLaunchKernelGGL(psort_scatter_kernel<1>, dim3(grid_of(B)), dim3(256), 0, s, occU, rankU, occV,
-                                   rankV, B, offP, srec); break;
-        case 5: hipLaunchKernelGGL(psort_scatter_kernel<5>, dim3(grid_of(B)), dim3(256), 0, s, occU, rankU, occV,
-                                   rankV, B, offP, srec); break;
+    hipLaunchKernelGGL(psort_tile_sum_kernel, dim3(nt), dim3(kScanThreads), 0, s, a.cntP, a.cntV, a.n_items, tiles);
+    hipLaunchKernelGGL(psort_tile_scan_kernel, dim3(nt), dim3(kScanThreads), 0, s, a.cntP, a.cntV, a.n_items, tiles,
+                       a.offPN);
+    switch (a.W) {
+        case 1: hipLaunchKernelGGL(psort_scatter_kernel<1>, dim3(grid_of(a.B)), dim3(256), 0, s, a); break;
+        case 5: hipLaunchKernelGGL(psort_scatter_kernel<5>, dim3(grid_of(a.B)), dim3(256), 0, s, a); break;
         default: return hipErrorInvalidValue;   // pos_sort runs at W in {1, 5}
     }
     return hipGetLastError();

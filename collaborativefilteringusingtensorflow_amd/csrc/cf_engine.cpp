@@ -107,8 +107,7 @@ struct cf_engine {
     int pos_sort = 2;                 // 0 off, 1 on, 2 auto: on for B >= kPsortAutoB
     int capP = 8;
     int32_t* cntP_[2] = {nullptr, nullptr};
-    int32_t* offP = nullptr;          // [n_items]
-    int32_t* offN = nullptr;          // [n_items] exclusive scan of the negatives' counts
+    int2* offPN = nullptr;            // [n_items + 1] exclusive scans of (positives, negatives) per item
     int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
     int order_cap = 0;
     float* slotP = nullptr;           // [n_items * capP, d]
@@ -287,6 +286,7 @@ bool psort_possible(const cf_engine* e) {
     if (!e->pos_sort || e->item_recs) return false;
     if (c.dense_item_apply && e->item_reduce != 1) return false;   // the multi-rank item reduce: slot rows only
     if (c.model != CF_BPR && c.model != CF_AMF && c.model != CF_CML) return false;
+    if ((int64_t)c.n_users * e->capU > INT32_MAX) return false;   // user slot rows ride in int32 records
     return c.n_factors <= 128 && (c.n_neg == 1 || c.n_neg == 5);
 }
 
@@ -309,15 +309,13 @@ int ensure_slots(cf_engine* e) {
     dfree(e->recV);
     dfree(e->GVrep);
     dfree(e->slotP);
-    dfree(e->offP);
-    dfree(e->offN);
+    dfree(e->offPN);
     for (int k = 0; k < 2; ++k) dfree(e->cntP_[k]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     e->psort_tmp = nullptr;
     if (psort_possible(e)) {
         CF_TRY(dalloc(&e->slotP, (size_t)c.n_items * e->capP * c.n_factors));
-        CF_TRY(dalloc(&e->offP, (size_t)c.n_items));
-        CF_TRY(dalloc(&e->offN, (size_t)c.n_items));
+        CF_TRY(dalloc(&e->offPN, (size_t)c.n_items + 1));
         for (int k = 0; k < 2; ++k) {
             CF_TRY(dalloc(&e->cntP_[k], (size_t)c.n_items));
             CF_HIP(hipMemsetAsync(e->cntP_[k], 0, (size_t)c.n_items * 4, e->stream));
@@ -509,11 +507,9 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     }
     if (psort_active(e, B) && e->cntP_[k] && e->srec && e->order_cap >= B) {
         a.cntP = e->cntP_[k];
-        a.offP = e->offP;
         a.srec = e->srec;
         a.slotP = e->slotP;
         a.capP = e->capP;
-        a.offN = e->offN;
         a.slotV = e->slotN;   // negatives: compact slots offN[j] + rank
     }
     a.shard_u0 = e->shard_u0;
@@ -702,11 +698,10 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.stashB = a.stashB;
     if (a.cntP != nullptr && a.count_items) {
         p.cntP = a.cntP;
-        p.offP = a.offP;
+        p.offPN = e->offPN;
         p.slotP = a.slotP;
         p.capP = a.capP;
         p.nPos = B;
-        p.offN = a.offN;
         // visit every row of a table that is not much larger than the batch's
         // occurrences of it (cfg2 at 2^19: 100K items / 1.05M occurrences,
         // 1M users / 524K), else find the owners among the occurrences
@@ -797,8 +792,15 @@ int det_hot(cf_engine* e, const StepArgs& a) {
 int psort(cf_engine* e, const StepArgs& a) {
     if (a.srec == nullptr) return CF_OK;
     ProfScope ps(e, CF_K_PSORT);
-    CF_HIP(launch_psort(a.occU, a.rankU, a.occV, a.rankV, a.B, a.W, a.cntP, e->offP, a.cntV, e->offN, e->srec,
-                        e->cfg.n_items, e->psort_tmp, e->psort_tmp_bytes, e->stream));
+    PsortArgs q{};
+    q.occU = a.occU; q.rankU = a.rankU;
+    q.occV = a.occV; q.rankV = a.rankV;
+    q.cntU = a.cntU; q.cntV = a.cntV; q.cntP = a.cntP;
+    q.offPN = e->offPN;
+    q.srec = e->srec;
+    q.B = a.B; q.W = a.W; q.capU = a.capU;
+    q.n_items = e->cfg.n_items;
+    CF_HIP(launch_psort(q, e->psort_tmp, e->psort_tmp_bytes, e->stream));
     return CF_OK;
 }
 
@@ -1191,7 +1193,7 @@ int cf_destroy(cf_engine* e) {
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
     dfree(e->slotVbc); dfree(e->recV); dfree(e->recVc); dfree(e->stashU); dfree(e->stashB);
     dfree(e->hotP); dfree(e->hotPb);
-    dfree(e->slotP); dfree(e->offP); dfree(e->offN); dfree(e->srec); dfree(e->slotN); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
+    dfree(e->slotP); dfree(e->offPN); dfree(e->srec); dfree(e->slotN); dfree(e->cntP_[0]); dfree(e->cntP_[1]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);

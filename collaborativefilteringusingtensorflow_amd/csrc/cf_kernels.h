@@ -112,7 +112,6 @@ struct StepArgs {
     // block - offP[i] / kPsortPPB of item i goes to slotP[i * capP + k] (k <
     // capP) or float atomics into GV.  null cntP = off
     int32_t* __restrict__ cntP;         // [n_items] positives per item (0 between steps)
-    const int32_t* __restrict__ offP;   // [n_items] exclusive scan of cntP
     // [B, psort_stride(W)] the pair at each positive-sorted position as one
     // contiguous record (u, i, j_0 .. j_{W-1}, then the ranks of u, j_0, ..
     // as 16-bit halves, clamped to 0xFFFF -- a rank only matters below the
@@ -121,10 +120,12 @@ struct StepArgs {
     float* __restrict__ slotP;          // [n_items * capP, d]
     int capP;
     // ... and the negatives in compact slots: with pos_sort, slotV is the
-    // [B * W, d] array where negative occurrence k (rank < kRankCap) of item
-    // j stores its gradient row at offN[j] + k (offN = exclusive scan of the
-    // negatives' counts cntV), so an item's negative rows are contiguous
-    const int32_t* __restrict__ offN;   // [n_items]
+    // [B * W, d] array where negative occurrence k of item j stores its
+    // gradient row at offN[j] + k (offN = exclusive scan of the negatives'
+    // counts cntV), so an item's negative rows are contiguous.  psort writes
+    // both scans interleaved, offPN[r] = (offP[r], offN[r]), r <= n_items
+    // (offPN[n_items] = the totals): an item's counts are the differences of
+    // two adjacent entries, one 16-B read
     // user sharding (GBPR group exchange): this rank owns global users
     // [shard_u0, shard_u1); a group member owned elsewhere is coded -1 - id in
     // occU until the exchange recodes it -1 - (its row in xrows / xgrads)
@@ -145,12 +146,19 @@ constexpr int32_t kRemoteFlag = 1 << 24;
 // per 16-lane group): partial k of an item covers the positions of block
 // offP[i] / kPsortPPB + k
 constexpr int kPsortPPB = kGroupsPerBlock;
-// occurrence ranks ride in 16 bits in the pos_sort records: a negative of
-// rank >= kRankCap (a row seen 65,535+ times as a negative) adds by float
-// atomics instead of a compact slot
-constexpr int kRankCap = 0xFFFF;
-// ints per record, int4-aligned: W = 1 -> 4 (16 B), W = 5 -> 12 (48 B)
-__host__ __device__ constexpr int psort_stride(int W) { return (2 + W + (2 + W) / 2 + 3) & ~3; }
+
+// A pos_sort record carries every occurrence's resolved destination --
+// psort_scatter reads the batch's final counts and offsets, so the gradient
+// launch issues its accumulator loads together with the rows (no dependent
+// count phase).  Ints per record, int4-aligned (W = 1 -> 8, W = 5 -> 16):
+//   [u, i, j_0 .. j_{W-1}, su, pi, sj_0 .. sj_{W-1}, 0 padding]
+// su / sj: >= 0 the slot row (users u * capU + rank, negatives the compact
+// slot offN[j] + rank), kSlotApply = the row's only occurrence in the batch
+// (Adagrad in place), kSlotAtomic = float atomics into the dense gradient;
+// pi = offP[i], bit 31 set when the positive is its item's only occurrence
+__host__ __device__ constexpr int psort_stride(int W) { return (4 + 2 * W + 3) & ~3; }
+constexpr int32_t kSlotApply = -1;
+constexpr int32_t kSlotAtomic = -2;
 
 struct XchgArgs {
     int n;                        // group occurrences (B * G)
@@ -201,11 +209,10 @@ struct ApplyArgs {
     // positive-sorted gradient (StepArgs): positives are occV[0, nPos);
     // negatives' compact slot rows at slotV[offN[r] + k]
     int32_t* __restrict__ cntP;
-    const int32_t* __restrict__ offP;
+    const int2* __restrict__ offPN;      // [n_items + 1] (offP, offN), see StepArgs
     const float* __restrict__ slotP;
     int capP;
     int64_t nPos;
-    const int32_t* __restrict__ offN;
     // pos_sort apply: visit every item row (dense_items) / every user row
     // (dense_users) instead of finding the owners among the occurrences --
     // when the table is not much larger than the batch's occurrences of it
@@ -348,13 +355,21 @@ hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
                             hipStream_t s);
-// positive-sorted gradient: offP / offN = exclusive scans of cntP / cntV
-// (two launches of tile sums + tile scans), then the pair records at
+// positive-sorted gradient: offPN = exclusive scans of (cntP, cntV) (two
+// launches of tile sums + tile scans), then the pair records at
 // srec[offP[i_p] + rankV[p]] for the B pairs; tmp sized by psort_scratch
 size_t psort_scratch(int64_t n_items);
-hipError_t launch_psort(const int32_t* occU, const int32_t* rankU, const int32_t* occV, const int32_t* rankV,
-                        int B, int W, const int32_t* cntP, int32_t* offP, const int32_t* cntV, int32_t* offN,
-                        int32_t* srec, int64_t n_items, void* tmp, size_t tmp_bytes, hipStream_t s);
+struct PsortArgs {
+    const int32_t* occU; const int32_t* rankU;
+    const int32_t* occV; const int32_t* rankV;
+    const int32_t* cntU;                 // the batch's final counts
+    const int32_t* cntV; const int32_t* cntP;
+    int2* offPN;                         // written: [n_items + 1] exclusive scans of (cntP, cntV)
+    int32_t* srec;                       // [B, psort_stride(W)]
+    int B, W, capU;
+    int64_t n_items;
+};
+hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
                                 uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,

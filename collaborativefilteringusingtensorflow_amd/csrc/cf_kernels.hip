@@ -631,8 +631,186 @@ __device__ __forceinline__ void prep_lane_body(const StepArgs& a, int block) {
     if (a.count_items) a.rankV[p] = atomicAdd(&a.cntV[i], 1);
 }
 
+// ---------------------------------------------------------------------------
+// the device draw with NP pairs per 8-lane group (CF_PREP_PAIRS): the draw is
+// latency-bound (pair record -> row scan -> returning count atomics), so a
+// group carries NP pairs' chains at once -- both pairs' records, then both
+// row scans' chunks, then both pairs' atomics in flight together.  Same
+// candidates, acceptance rule and counts as prep_body (the same batches).
+// Device sampler with the CSR row scan and W <= the group width only;
+// everything else takes prep_body.  Measured SLOWER at cfg2 (same box, r03:
+// draw alone 130 vs 120 us, apply + draw 199 vs 190 us, step 0.408 vs 0.3995
+// ms; profiles/r03/ab_draw_pairs.txt): the draw is not short of chains in
+// flight per wave -- its returning count atomics and the row-scan requests
+// bound it -- so one pair per group stays the default; -DCF_PREP_PAIRS=2
+// builds the variant.
+// ---------------------------------------------------------------------------
+#ifndef CF_PREP_PAIRS
+#define CF_PREP_PAIRS 1
+#endif
+constexpr int kPrepPairs = CF_PREP_PAIRS;
+
+__host__ __device__ __forceinline__ bool multi_prep(const StepArgs& a) {
+    return kPrepPairs > 1 && a.sample && a.pos_set == nullptr && a.W <= kPrepGL && !lane_prep(a);
+}
+
+template <int MODEL>
+__device__ __forceinline__ void prep_body_np(const StepArgs& a, int block) {
+    constexpr int PGL = kPrepGL, NP = kPrepPairs;
+    const int gl = threadIdx.x & (PGL - 1);
+    const int grp = threadIdx.x / PGL;
+    const int W = a.W, B = a.B;
+    const int G = (MODEL == GBPR) ? a.G : 0;
+    const int nw = W, C = PGL / nw, nl = C * nw;
+    int p[NP], u[NP], i[NP], nchunk[NP];
+    bool ok[NP];
+    uint64_t key[NP];
+    int64_t rb[NP], re[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        p[k] = (block * NP + k) * kPrepPairsPerBlock + grp;
+        ok[k] = p[k] < B;   // group-uniform
+    }
+    if (!ok[0]) return;    // (p[k] grows with k) whole group leaves; no block barrier below
+    // pair records (one 16-B load each, all in flight)
+    int4 pr[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        const uint64_t slot = a.slot_base + (uint64_t)p[k];
+        key[k] = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
+        if (ok[k]) pr[k] = a.pairs[permute(slot, a.perm)];   // sampler_ranking.py:24
+    }
+    int maxchunk = 0;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        u[k] = ok[k] ? pr[k].x : 0;
+        i[k] = ok[k] ? pr[k].y : 0;
+        rb[k] = ok[k] ? (int64_t)(uint32_t)pr[k].z : 0;
+        re[k] = ok[k] ? rb[k] + pr[k].w : 0;
+        nchunk[k] = (int)((re[k] - rb[k] + PGL - 1) / PGL);
+        maxchunk = nchunk[k] > maxchunk ? nchunk[k] : maxchunk;
+    }
+    // negItems = randint(0, n_items), redrawn while j in Pos(u)
+    // (sampler_ranking.py:30-36): lane l holds attempt l / nw of negative
+    // l % nw; every pair's first C attempts are tested in one row scan
+    int32_t jl[NP];
+    uint32_t hit[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        jl[k] = (gl < nl) ? draw_item(key[k], ((uint64_t)(gl % nw) << 32) + (uint64_t)(gl / nw), a.n_items) : -1;
+        hit[k] = 0u;
+    }
+    {
+        int32_t cand[NP][PGL];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+#pragma unroll
+            for (int c = 0; c < PGL; ++c) cand[k][c] = __shfl(jl[k], c, PGL);
+        for (int c0 = 0; c0 < maxchunk; c0 += kPrepChunks) {
+            int32_t el[NP][kPrepChunks];
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+#pragma unroll
+                for (int q = 0; q < kPrepChunks; ++q) {
+                    const int64_t t = rb[k] + (int64_t)(c0 + q) * PGL + gl;
+                    el[k][q] = (t < re[k]) ? a.indices[t] : -1;
+                }
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+#pragma unroll
+                for (int q = 0; q < kPrepChunks; ++q)
+#pragma unroll
+                    for (int c = 0; c < PGL; ++c)
+                        hit[k] |= (c < nl && el[k][q] == cand[k][c]) ? (1u << c) : 0u;
+        }
+    }
+    int32_t j[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        hit[k] = gor8(hit[k]);
+        // lane w < nw: the first accepted attempt of negative w
+        bool done = false;
+        j[k] = -1;
+        for (int c = 0; c < C; ++c) {
+            const int src = c * nw + (gl % nw);
+            const int32_t cv = __shfl(jl[k], src, PGL);
+            if (!done && gl < nw && !((hit[k] >> src) & 1u)) {
+                j[k] = cv;
+                done = true;
+            }
+        }
+        // rare: every tested attempt of some negative was a positive ->
+        // continue its sequence at attempt C, one candidate per lane
+        uint32_t pending = gor8((ok[k] && gl < nw && !done) ? (1u << gl) : 0u);
+        uint64_t ctr = ((uint64_t)gl << 32) + (uint64_t)C;
+        if ((pending >> gl) & 1u) j[k] = draw_item(key[k], ctr++, a.n_items);
+        while (pending != 0u) {  // group-uniform
+            int32_t cand[PGL];
+#pragma unroll
+            for (int c = 0; c < PGL; ++c) cand[c] = __shfl(j[k], c, PGL);
+            uint32_t h2 = 0;
+            for (int c0 = 0; c0 < nchunk[k]; c0 += kPrepChunks) {
+                int32_t el[kPrepChunks];
+#pragma unroll
+                for (int q = 0; q < kPrepChunks; ++q) {
+                    const int64_t t = rb[k] + (int64_t)(c0 + q) * PGL + gl;
+                    el[q] = (t < re[k]) ? a.indices[t] : -1;
+                }
+#pragma unroll
+                for (int q = 0; q < kPrepChunks; ++q)
+#pragma unroll
+                    for (int c = 0; c < PGL; ++c)
+                        h2 |= (c < nw && el[q] == cand[c]) ? (1u << c) : 0u;
+            }
+            h2 = gor8(h2) & pending;
+            if ((h2 >> gl) & 1u) j[k] = draw_item(key[k], ctr++, a.n_items);
+            pending = h2;
+        }
+    }
+    // occurrences and their ranks (returning count atomics), every pair's at once
+    int32_t rj[NP], ru[NP], ri[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        if (ok[k] && gl < nw) {
+            a.occV[B + p[k] * W + gl] = j[k];
+            if (a.count_items) rj[k] = atomicAdd(&a.cntV[j[k]], 1);
+        }
+        if (ok[k] && gl == 0) {
+            a.occU[p[k]] = u[k];
+            a.occV[p[k]] = i[k];
+            if (a.count_users) ru[k] = atomicAdd(&a.cntU[u[k]], 1);
+            // pos_sort: the positive's rank among the batch's positives of i
+            if (a.count_items) ri[k] = atomicAdd(a.cntP != nullptr ? &a.cntP[i[k]] : &a.cntV[i[k]], 1);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+        if (ok[k] && gl < nw && a.count_items) a.rankV[B + p[k] * W + gl] = rj[k];
+        if (ok[k] && gl == 0) {
+            if (a.count_users) a.rankU[p[k]] = ru[k];
+            if (a.count_items) a.rankV[p[k]] = ri[k];
+        }
+    }
+    if (MODEL == GBPR) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            if (!ok[k]) continue;
+            for (int q = gl; q < G; q += PGL) {
+                // group = np.random.choice(item_posUserList[i], gsize) (sampler_gbpr.py:41)
+                const int64_t cb = a.indptr_t[i[k]], ce = a.indptr_t[i[k] + 1];
+                const uint64_t h = mix64(key[k] + ((uint64_t)(kMaxNeg + q) << 32));
+                int32_t g = a.indices_t[cb + (int64_t)uniform_below(h, (uint64_t)(ce - cb))];
+                g = (g >= a.shard_u0 && g < a.shard_u1) ? g - a.shard_u0 : -1 - g;
+                a.occU[B + p[k] * G + q] = g;
+                if (a.count_users && g >= 0) a.rankU[B + p[k] * G + q] = atomicAdd(&a.cntU[g], 1);
+            }
+        }
+    }
+}
+
 // the draw + count of one block of a step's batch: one lane per pair when no
-// row scan is needed (lane_prep), else the 8-lane cooperative row scan
+// row scan is needed (lane_prep), several pairs per 8-lane group on the
+// device sampler's row scan (multi_prep), else prep_body
 template <int MODEL>
 __device__ __forceinline__ void prep_any(const StepArgs& a, int block) {
 #if CF_LANE_DRAW
@@ -643,11 +821,15 @@ __device__ __forceinline__ void prep_any(const StepArgs& a, int block) {
         return;
     }
 #endif
+    if (multi_prep(a)) {
+        prep_body_np<MODEL>(a, block);
+        return;
+    }
     prep_body<MODEL>(a, block);
 }
 
 __host__ __device__ __forceinline__ int prep_pairs_per_block(const StepArgs& a) {
-    return lane_prep(a) ? kBlock : kPrepPairsPerBlock;
+    return lane_prep(a) ? kBlock : multi_prep(a) ? kPrepPairs * kPrepPairsPerBlock : kPrepPairsPerBlock;
 }
 
 template <int MODEL>
@@ -1109,7 +1291,6 @@ struct PairRows {
     int p, u, i, cu, ci, ru, ri;
     int oi;   // pos_sort: offP[i], the item's first positive-sorted position
     int j[WT], cj[WT], rj[WT];
-    int oj[WT];   // pos_sort: offN[j], the negative's first compact slot
     int g[NGA], cg[NGA], rg[NGA];
     int64_t su, si, sj[WT], sg[NGA];  // slot rows (or -1)
     float uu[EPL], vi[EPL], au[EPL], ai[EPL];
@@ -1118,8 +1299,9 @@ struct PairRows {
     float bi, bj[WT];
     float abi, abj[WT];   // GBPR: bias accumulators of rows seen once
 
-    // pos_sort: the ids of the pair at positive-sorted position pos, from its
-    // contiguous record (coalesced across the wave's groups)
+    // pos_sort: the pair at positive-sorted position pos, from its contiguous
+    // record (coalesced across the wave's groups): ids and every occurrence's
+    // resolved destination (psort_scatter), so no count loads follow
     __device__ __forceinline__ void load_idx_sorted(const StepArgs& a, int pos) {
         constexpr int RS = psort_stride(WT);
         const int4* r = reinterpret_cast<const int4*>(a.srec + (int64_t)pos * RS);
@@ -1133,11 +1315,20 @@ struct PairRows {
         i = v[1];
         p = pos;   // (the pair index itself is not needed on this path)
         ri = 0;
-        ru = v[2 + WT] & 0xFFFF;
+        ru = 0;
+        const int32_t su_code = v[2 + WT], pi = v[3 + WT];
+        cu = su_code == kSlotApply ? 1 : 2;
+        su = su_code >= 0 ? su_code : -1;
+        ci = pi < 0 ? 1 : 2;
+        oi = pi & 0x7FFFFFFF;
+        si = -1;
 #pragma unroll
         for (int w = 0; w < WT; ++w) {
             j[w] = v[2 + w];
-            rj[w] = (v[2 + WT + (w + 1) / 2] >> (16 * ((w + 1) & 1))) & 0xFFFF;
+            rj[w] = 0;
+            const int32_t sc = v[4 + WT + w];
+            cj[w] = sc == kSlotApply ? 1 : 2;
+            sj[w] = sc >= 0 ? sc : -1;
         }
     }
     __device__ __forceinline__ void load_idx(const StepArgs& a, int pair) {
@@ -1159,20 +1350,24 @@ struct PairRows {
     }
     template <bool SORT = false>
     __device__ __forceinline__ void load_rows(const StepArgs& a, int gl) {
-        cu = a.count_users ? a.cntU[u] : 0;
-        if constexpr (SORT) {   // an item's count = its positives (cntP) + its negatives (cntV)
-            ci = a.cntV[i] + a.cntP[i];
-            oi = a.offP[i];
+        if constexpr (SORT) {
+            // destinations came with the record: the accumulator rows of the
+            // rows seen once are issued with the table rows (one load phase)
+            gload<EPL>(a.U, u, a.d, gl, uu);
+            gload<EPL>(a.V, i, a.d, gl, vi);
 #pragma unroll
-            for (int w = 0; w < WT; ++w) {
-                cj[w] = a.cntV[j[w]] + a.cntP[j[w]];
-                oj[w] = a.offN[j[w]];
-            }
-        } else {
-            ci = a.count_items ? a.cntV[i] : 0;
+            for (int w = 0; w < WT; ++w) gload<EPL>(a.V, j[w], a.d, gl, vj[w]);
+            const bool item_acc = !a.items_grad_only;
+            gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
+            gload_acc<EPL>(a.AV, i, a.d, gl, item_acc && ci == 1, ai);
 #pragma unroll
-            for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+            for (int w = 0; w < WT; ++w) gload_acc<EPL>(a.AV, j[w], a.d, gl, item_acc && cj[w] == 1, aj[w]);
+            return;
         }
+        cu = a.count_users ? a.cntU[u] : 0;
+        ci = a.count_items ? a.cntV[i] : 0;
+#pragma unroll
+        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
 #pragma unroll
         for (int k = 0; k < NG; ++k) cg[k] = (a.count_users && g[k] >= 0) ? a.cntU[g[k]] : 0;
         gload<EPL>(a.U, u, a.d, gl, uu);
@@ -1190,16 +1385,11 @@ struct PairRows {
     }
     template <bool SORT = false>
     __device__ __forceinline__ void load_acc(const StepArgs& a, int gl) {
+        if constexpr (SORT) return;   // loaded with the rows (load_rows)
         su = slot_of(cu, u, ru, a.capU, 0, a.offU);
         si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
-        if constexpr (SORT) {   // compact negative slots offN[j] + rank (slotV = [B * W, d])
 #pragma unroll
-            for (int w = 0; w < WT; ++w)
-                sj[w] = (cj[w] >= 2 && rj[w] < kRankCap) ? (int64_t)oj[w] + rj[w] : -1;
-        } else {
-#pragma unroll
-            for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
-        }
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
 #pragma unroll
         for (int k = 0; k < NG; ++k) sg[k] = slot_of(cg[k], g[k], rg[k], a.capU, 0, a.offU);
         gload_acc<EPL>(a.AU, u, a.d, gl, cu == 1, au);
@@ -1687,7 +1877,7 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
         gload_acc<EPL>(a.AV, r, a.d, gl, true, acc);
     }
     const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
-    const int nn = cn < kRankCap ? cn : kRankCap;
+    const int nn = cn;   // every negative occurrence has its compact slot
     const int npp = np < a.capP ? np : a.capP;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
@@ -1714,7 +1904,7 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
                 for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
             }
     }
-    if (cn > kRankCap || np > a.capP) {   // what overflowed either range: float atomics into GV
+    if (np > a.capP) {   // partials past the positives' slot range: float atomics into GV
         float h[EPL];
         gload<EPL>(a.GV, r, a.d, gl, h);
 #pragma unroll
@@ -1780,9 +1970,10 @@ __device__ __forceinline__ void apply_ps_item_block(const ApplyArgs& a, int bloc
     const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
     const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
     if (r >= a.n_items) return;
-    const int cn = a.cntV[r], cp = a.cntP[r], o = a.offP[r], on = a.offN[r];
+    const int2 o0 = a.offPN[r], o1 = a.offPN[r + 1];
+    const int cp = o1.x - o0.x, cn = o1.y - o0.y;
     if (cn + cp < 2) return;   // untouched, or seen once (applied by the gradient launch)
-    apply_item_ps<EPL>(a, r, gl, cn, cp, o, on);
+    apply_item_ps<EPL>(a, r, gl, cn, cp, o0.x, o0.y);
 }
 
 template <int EPL>
@@ -1811,10 +2002,9 @@ __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) 
             // the rank-0 positive owns an item with positives in the batch
             // (offP[r+1] - offP[r] > 0, immutable during the launch), else the
             // rank-0 negative
-            const int64_t o0 = a.offP[r];
-            const int64_t o1 = (int64_t)r + 1 < a.n_items ? (int64_t)a.offP[r + 1] : a.nPos;
-            if ((k < a.nPos) == (o1 > o0)) {
-                c = a.cntV[r] + a.cntP[r];
+            const int2 o0 = a.offPN[r], o1 = a.offPN[r + 1];
+            if ((k < a.nPos) == (o1.x > o0.x)) {
+                c = (o1.x - o0.x) + (o1.y - o0.y);
                 if (c >= 2) row = r;
             }
         }
@@ -1833,8 +2023,8 @@ __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) 
         if (ru) {
             apply_row<EPL>(a, rr, true, cc, gl);
         } else {
-            const int cn = a.cntV[rr], cp = a.cntP[rr], o = a.offP[rr], on = a.offN[rr];
-            apply_item_ps<EPL>(a, rr, gl, cn, cp, o, on);
+            const int2 o0 = a.offPN[rr], o1 = a.offPN[rr + 1];
+            apply_item_ps<EPL>(a, rr, gl, o1.y - o0.y, o1.x - o0.x, o0.x, o0.y);
         }
     }
 }

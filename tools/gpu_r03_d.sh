@@ -1,0 +1,20 @@
+#!/bin/bash
+# same-box A/B: r03base (before compact negative slots / dense apply) vs the current build
+set -o pipefail
+export PYTHONUNBUFFERED=1
+OUT=gpurun_out/r03d
+mkdir -p $OUT
+B=collaborativefilteringusingtensorflow_amd/build
+A="--no-cpu-baseline --no-ndcg --secondary-batch 0 --steps 200 --warmup 20"
+cat > /tmp/psf.py <<'PY'
+import sys, json
+d = json.loads(sys.stdin.read()); k = d['kernels']
+print(sys.argv[1], round(d['ms_per_step'], 4), {n: round(v['avg_us'], 1) for n, v in k.items() if n != 'note'})
+PY
+for r in 1 2; do
+for v in r03base default; do
+  lib=$PWD/$B/libcf_engine.so; [ $v != default ] && lib=$PWD/$B/variants/$v/libcf_engine.so
+  CF_ENGINE_LIB=$lib timeout -k 10 200 python bench.py $A >> $OUT/cfg2_$v.jsonl 2>> $OUT/bench.err || { echo "BENCH FAILED"; tail -20 $OUT/bench.err; exit 1; }
+  tail -1 $OUT/cfg2_$v.jsonl | python /tmp/psf.py "cfg2 $v"
+done
+done
