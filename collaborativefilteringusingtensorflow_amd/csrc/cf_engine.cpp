@@ -1265,7 +1265,8 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pos_set);
     CF_TRY(dalloc(&e->indptr, (size_t)c.n_users + 1));
-    CF_TRY(dalloc(&e->indices, (size_t)nnz));
+    CF_TRY(dalloc(&e->indices, (size_t)nnz + 4));   // + 4: the draw's 16-B row loads never leave it
+    CF_HIP(hipMemsetAsync(e->indices + nnz, 0xFF, 16, e->stream));
     CF_TRY(dalloc(&e->pairs, (size_t)nnz));
     CF_HIP(hipMemcpyAsync(e->indptr, indptr, ((size_t)c.n_users + 1) * 8, hipMemcpyHostToDevice, e->stream));
     CF_HIP(hipMemcpyAsync(e->indices, indices, (size_t)nnz * 4, hipMemcpyHostToDevice, e->stream));

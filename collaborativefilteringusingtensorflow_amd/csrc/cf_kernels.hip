@@ -323,6 +323,18 @@ __device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t
 constexpr int kPrepGL = CF_PREP_GL;
 constexpr int kPrepPairsPerBlock = kBlock / kPrepGL;
 constexpr int kPrepChunks = CF_PREP_CHUNKS;
+// row scan in 16-B loads (4 ids per lane per chunk): measured SLOWER at cfg2
+// (same box, r03: draw alone 183 vs 119 us, 0.489 vs 0.399 ms/step;
+// profiles/r03/ab_draw_vec_sortw.txt) -- the masked 4 x 8 compare per chunk
+// and the misaligned 128-B spans cost more than the fewer load instructions
+// save; 4-B loads stay the default
+#ifndef CF_PREP_VEC
+#define CF_PREP_VEC 0
+#endif
+#ifndef CF_PREP_VCHUNKS
+#define CF_PREP_VCHUNKS 4 // 128-B row chunks in flight per group (512 ids)
+#endif
+constexpr int kPrepVChunks = CF_PREP_VCHUNKS;
 
 // OR over the kPrepGL lanes of a draw group
 __device__ __forceinline__ uint32_t gor8(uint32_t v) {
@@ -348,6 +360,58 @@ __device__ __forceinline__ bool is_positive(const StepArgs& a, int u, int32_t j)
         if (t == kPosEmpty) return false;
         s = (s + 1) & a.pos_mask;
     }
+}
+
+// Which of the group's candidates cand[0, ncand) lie in the user's sorted
+// CSR row [rb, re) (bit c of the group-OR'ed result).  CF_PREP_VEC: lane gl
+// reads 16 B (4 ids) of every 128-B chunk from the 16-B-aligned start at or
+// before rb, kPrepVChunks chunks in flight -- a 51-id row is two load
+// instructions instead of seven 4-B ones (the indices allocation is padded
+// by 4 ids, so an int4 never leaves it); ids outside [rb, re) never match.
+__device__ __forceinline__ uint32_t row_hits(const int32_t* __restrict__ ind, int64_t rb, int64_t re, int gl,
+                                             const int32_t (&cand)[kPrepGL], int ncand) {
+    uint32_t hit = 0;
+#if CF_PREP_VEC
+    constexpr int CW = 4 * kPrepGL;   // ids per chunk
+    const int64_t a0 = rb & ~(int64_t)3;
+    const int nch = (int)((re - a0 + CW - 1) / CW);
+    for (int c0 = 0; c0 < nch; c0 += kPrepVChunks) {
+        int4 el[kPrepVChunks];
+#pragma unroll
+        for (int q = 0; q < kPrepVChunks; ++q) {
+            const int64_t t = a0 + (int64_t)(c0 + q) * CW + 4 * gl;
+            el[q] = (t < re) ? *reinterpret_cast<const int4*>(ind + t) : make_int4(-1, -1, -1, -1);
+        }
+#pragma unroll
+        for (int q = 0; q < kPrepVChunks; ++q) {
+            const int64_t t = a0 + (int64_t)(c0 + q) * CW + 4 * gl;
+            const int32_t e4[4] = {el[q].x, el[q].y, el[q].z, el[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool in = t + e >= rb && t + e < re;
+#pragma unroll
+                for (int c = 0; c < kPrepGL; ++c)
+                    hit |= (in && c < ncand && e4[e] == cand[c]) ? (1u << c) : 0u;
+            }
+        }
+    }
+#else
+    const int nchunk = (int)((re - rb + kPrepGL - 1) / kPrepGL);
+    for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
+        int32_t el[kPrepChunks];
+#pragma unroll
+        for (int q = 0; q < kPrepChunks; ++q) {
+            const int64_t t = rb + (int64_t)(c0 + q) * kPrepGL + gl;
+            el[q] = (t < re) ? ind[t] : -1;
+        }
+#pragma unroll
+        for (int q = 0; q < kPrepChunks; ++q)
+#pragma unroll
+            for (int c = 0; c < kPrepGL; ++c)
+                hit |= (c < ncand && el[q] == cand[c]) ? (1u << c) : 0u;
+    }
+#endif
+    return hit;
 }
 
 template <int MODEL>
@@ -377,7 +441,6 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         u = a.occU[p];
         i = a.occV[p];
     }
-    const int nchunk = (int)((re - rb + PGL - 1) / PGL);
     for (int w0 = 0; w0 < W; w0 += PGL) {
         const int nw = (W - w0 < PGL) ? (W - w0) : PGL;
         const int w = w0 + gl;
@@ -409,20 +472,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
                 int32_t cand[PGL];
 #pragma unroll
                 for (int k = 0; k < PGL; ++k) cand[k] = __shfl(jl, k, PGL);
-                for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
-                    int32_t el[kPrepChunks];
-#pragma unroll
-                    for (int q = 0; q < kPrepChunks; ++q) {
-                        const int64_t t = rb + (int64_t)(c0 + q) * PGL + gl;
-                        el[q] = (t < re) ? a.indices[t] : -1;
-                    }
-#pragma unroll
-                    for (int q = 0; q < kPrepChunks; ++q)
-#pragma unroll
-                        for (int k = 0; k < PGL; ++k)
-                            hit |= (k < nl && el[q] == cand[k]) ? (1u << k) : 0u;
-                }
-                hit = gor8(hit);
+                hit = gor8(row_hits(a.indices, rb, re, gl, cand, nl));
             }
             // lane w < nw: the first accepted attempt of negative w
             bool done = false;
@@ -443,21 +493,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
                 int32_t cand[PGL];
 #pragma unroll
                 for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
-                uint32_t h2 = 0;
-                for (int c0 = 0; c0 < nchunk; c0 += kPrepChunks) {
-                    int32_t el[kPrepChunks];
-#pragma unroll
-                    for (int q = 0; q < kPrepChunks; ++q) {
-                        const int64_t t = rb + (int64_t)(c0 + q) * PGL + gl;
-                        el[q] = (t < re) ? a.indices[t] : -1;
-                    }
-#pragma unroll
-                    for (int q = 0; q < kPrepChunks; ++q)
-#pragma unroll
-                        for (int k = 0; k < PGL; ++k)
-                            h2 |= (k < nw && el[q] == cand[k]) ? (1u << k) : 0u;
-                }
-                h2 = gor8(h2) & pending;
+                uint32_t h2 = gor8(row_hits(a.indices, rb, re, gl, cand, nw)) & pending;
                 if ((h2 >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
                 pending = h2;
             }
@@ -1676,6 +1712,19 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
         grad_fast_body<MODEL, EPL, WT, P, kGroupsPerBlock, SORT>(a, idx);
 }
 
+// the positive-sorted gradient launch (pos_sort) as its own kernel, so its
+// register budget can be set apart from the other phased instantiations:
+// CF_SORT_MIN_WAVES = minimum waves per SIMD (8 = at most 64 VGPRs).  8 was
+// measured SLOWER at cfg2 (gradient launch 236 vs 179 us: the 74-VGPR body
+// spills), so the budget is left to the compiler (6 waves/SIMD)
+#ifndef CF_SORT_MIN_WAVES
+#define CF_SORT_MIN_WAVES 1
+#endif
+template <int MODEL, int EPL, int WT>
+__global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a) {
+    grad_fast_body<MODEL, EPL, WT, 1, kGroupsPerBlock, true>(a, blockIdx.x);
+}
+
 // the same gradient blocks at one wave per workgroup (no draw blocks): a
 // finer dispatch granule, so the last round of workgroups leaves less of the
 // chip idle (a step's gradient launch is only ~2.7 rounds of 256-lane blocks)
@@ -2596,11 +2645,12 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
     if constexpr (MODEL != GBPR && P == 1) {
         if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
             if (np > 0) return hipErrorInvalidValue;
+            const dim3 sgrid(ng);
             switch (epl_for(a.d)) {
-                case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
-                case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
-                case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
-                default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, false, true>), grid, block, 0, s, a, n, ng, 0); break;
+                case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT>), sgrid, block, 0, s, a); break;
+                case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT>), sgrid, block, 0, s, a); break;
+                case 4: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT>), sgrid, block, 0, s, a); break;
+                default: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT>), sgrid, block, 0, s, a); break;
             }
             return hipGetLastError();
         }
