@@ -319,10 +319,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-ndcg", action="store_true", help="skip the cfg1 NDCG@10 check")
+    ap.add_argument("--fused-variant", type=int, default=0,
+                    help="cf_set_option fused_variant: 0 software-pipelined fused scoring + top-k, 1 sequential")
     ap.add_argument("--score-pass", action="store_true",
                     help="also time one full scoring + top-10 pass over this rank's users")
     ap.add_argument("--grad-path", type=int, default=0,
-                    help="cf_set_option grad_path: 0 auto, 1 generic kernel, 2 phased kernel when eligible")
+                    help="cf_set_option grad_path: 0 auto, 1 generic kernel, 2 phased kernel when eligible, 3 LDS-staged negatives when eligible")
     ap.add_argument("--prep-stream", type=int, default=0,
                     help="cf_set_option prep_stream: 0 in-order (default), 1 side stream")
     ap.add_argument("--pipeline", type=int, default=1,
@@ -449,6 +451,8 @@ def main():
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
                  dense_item_apply=sharded, seed=1000 + rank, **kw)
     eng.set_option("grad_path", args.grad_path)
+    if args.fused_variant != 0:   # (the engine's default is 0)
+        eng.set_option("fused_variant", args.fused_variant)
     eng.set_option("prep_stream", args.prep_stream)
     eng.set_option("pipeline", args.pipeline)
     if args.hot_replicas:
@@ -682,7 +686,9 @@ def main():
         out["score_pass"] = {"users": nu_all, "items": ni, "d": d, "k": 10, "seconds": ts,
                              "TFLOPs": flop / ts / 1e12,
                              "frac_fp32_mfma_peak": flop / ts / 1e12 / (157.3 * world),
-                             "kernel": "fused_topk_kernel (v_mfma_f32_32x32x2_f32 + streaming top-k)",
+                             "kernel": ("fused_topk_pipe_kernel" if args.fused_variant == 0 and cfg["model"] != "cml"
+                                        else "fused_topk_kernel") +
+                                       " (v_mfma_f32_32x32x2_f32 + streaming top-k)",
                              "kernel_ms_hip_events": tk_ms if tk_n else None,
                              "kernel_TFLOPs": (2.0 * (u1 - u0) * ni * d / (1e-3 * tk_ms) / 1e12)
                              if tk_n and tk_ms > 0 else None}

@@ -215,6 +215,7 @@ struct cf_engine {
     size_t keys_cap = 0;
 
     int topk_path = 0;  // cf_set_option("topk_path")
+    int fused_variant = 0;  // cf_set_option("fused_variant")
     int grad_path = 0;  // cf_set_option("grad_path")
     int item_reduce = 1;  // cf_set_option("item_reduce"): dense mode counts item rows
     int bias_slots = 0;   // cf_set_option("bias_slots"): duplicated item-bias gradients in slots (1) or atomics (0)
@@ -1021,6 +1022,7 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
     f.indices = e->indices;
     f.idx_out = d_idx;
     f.val_out = d_val;
+    f.variant = e->fused_variant;
     hipError_t he = hipMemcpyAsync(d_users, users, (size_t)n * 4, hipMemcpyHostToDevice, e->stream);
     if (he == hipSuccess) {
         ProfScope ps(e, CF_K_TOPK);
@@ -2049,6 +2051,11 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (!e || !name) return fail(CF_EINVAL, "null argument");
     CF_TRY(set_dev(e));   // some options (re)allocate device buffers
     const std::string n(name);
+    if (n == "fused_variant") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "fused_variant must be 0 or 1");
+        e->fused_variant = (int)value;
+        return CF_OK;
+    }
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
         e->topk_path = (int)value;
@@ -2148,7 +2155,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "grad_path") {
-        if (value < 0 || value > 2) return fail(CF_EINVAL, "grad_path must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(CF_EINVAL, "grad_path must be 0, 1, 2 or 3");
         CF_TRY(discard_pending(e));   // a drawn-ahead batch was counted for the old path (pos_sort)
         e->grad_path = (int)value;
         return CF_OK;
@@ -2185,6 +2192,7 @@ int cf_step_path(cf_engine* e, int32_t B, int32_t* flags_out) {
     int f = 0;
     if (grad_fast_w(a) != 0) f |= CF_PATH_PHASED;
     if (psort_active(e, B)) f |= CF_PATH_POS_SORT;
+    else if (grad_lds(a)) f |= CF_PATH_LDS;   // (pos_sort takes the sorted kernel)
     if (e->item_recs && (!c.dense_item_apply || e->item_reduce)) f |= CF_PATH_ITEM_RECORDS;
     if (e->det) f |= CF_PATH_DETERMINISTIC;
     if (c.dense_item_apply) f |= CF_PATH_DENSE_ITEMS;

@@ -514,9 +514,282 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same pass software-pipelined across item tiles (variant 0, default):
+// while a wave's MFMAs build tile t's scores in one accumulator set, the
+// candidate test of tile t-1 runs on the other set, one row (q) per group of
+// four MFMAs -- the VALU work issues in the shadow of the matrix core instead
+// of after it.  Tile t's train-mask bits, bias and (CML) |v|^2 are taken
+// into registers while tile t is current, so the LDS image is unchanged
+// (two blocks per CU).  Insertions (rare once the thresholds have risen) run
+// after the MFMA loop; every list still receives at most one tile's 64 keys
+// between compaction checks.  Same keys, same lists, same output as
+// fused_topk_kernel.
+// ---------------------------------------------------------------------------
+template <int MODEL>
+__global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArgs a) {
+    __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFusedMaxD];
+    __shared__ unsigned long long buf[kFusedUsers * kFusedCap];
+    __shared__ unsigned long long thr[kFusedUsers];
+    __shared__ unsigned long long mask[kFusedUsers];
+    __shared__ int cnt[kFusedUsers];
+    __shared__ float unorm[kFusedUsers];
+    __shared__ float bt[kFusedItems];
+    __shared__ int thr_ver;
+
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wv = tid >> 6;
+    const int wr = wv >> 1, wc = wv & 1;
+    const int h = lane >> 5, c = lane & 31;
+    const int d = a.d, Dp = a.Dp, Dh = a.Dh;
+    const int u0 = blockIdx.x * kFusedUsers;
+    if (tid == 0) thr_ver = 0;
+    const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
+
+    constexpr int kAH = kFusedMaxD / 2;
+    float ua[kAH];
+    {
+        const int r = wr * 32 + c;
+        const float* urow = a.U + (int64_t)a.users[u0 + (r < nu ? r : 0)] * d;
+#pragma unroll
+        for (int t = 0; t < kAH; ++t) {
+            const int kk = h * Dh + t;
+            ua[t] = (r < nu && t < Dh && kk < d) ? urow[kk] : 0.f;
+        }
+        if (MODEL == CML) {
+            float sq = 0.f;
+#pragma unroll
+            for (int t = 0; t < kAH; ++t) sq = fmaf(ua[t], ua[t], sq);
+            sq += __shfl_xor(sq, 32, 64);
+            if (wc == 0 && h == 0) unorm[r] = sq;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+    }
+    int64_t cur = 0, end = 0;
+    int64_t nxt = INT64_MAX;
+    if (tid < kFusedUsers) {
+        thr[tid] = 0ull;
+        cnt[tid] = 0;
+        if (a.exclude_train && tid < nu) {
+            const int u = a.users[u0 + tid];
+            cur = a.indptr[u];
+            end = a.indptr[u + 1];
+            if (cur < end) nxt = a.indices[cur];
+        }
+    }
+    const bool vec = (d & 3) == 0;
+    const int q4 = Dp >> 2;
+    constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + kBlock - 1) / kBlock;
+    float4 pre[kPre];
+    // (tile-loop-invariant addresses are formed where they are used, behind
+    // an opaque copy of tid: hoisted, they would hold ~30 VGPRs all sweep)
+    auto load_tile = [&](int64_t jt) {
+        int tid_ = tid;
+        asm volatile("" : "+v"(tid_));
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) {
+            const int t = tid_ + q * kBlock;
+            const int r = t / q4, kk = (t - r * q4) * 4;
+            const int64_t j = jt + r;
+            pre[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t < kFusedItems * q4 && j < a.n_items && kk < d)
+                pre[q] = *reinterpret_cast<const float4*>(a.V + j * d + kk);
+        }
+    };
+    auto store_tile = [&]() {
+        int tid_ = tid;
+        asm volatile("" : "+v"(tid_));
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) {
+            const int t = tid_ + q * kBlock;
+            const int r = t / q4, kk = (t - r * q4) * 4;
+            if (t < kFusedItems * q4) *reinterpret_cast<float4*>(Vs + vs_off(r, kk)) = pre[q];
+        }
+    };
+    if (vec) {
+        load_tile(0);
+        store_tile();
+    }
+    const int jl = wc * 32 + c;              // this lane's item column in a tile
+    // row q of this lane's 16 accumulator rows
+    auto row_of = [&](int q) { return wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h; };
+    // the previous tile's scores, train-mask bits, bias, |v|^2 and column
+    floatx16 accp;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) accp[q] = 0.f;
+    uint32_t mbp = 0;
+    float bp = 0.f, vnp = 0.f;
+    int64_t Jp = -1;                         // -1: no previous tile
+    auto score = [&](int q, float accv) {
+        float s = accv;
+        if (MODEL == GBPR) s += bp;
+        if (MODEL == CML) {   // |u|^2 re-read each time (hoisted: 16 VGPRs)
+            int R = row_of(q);
+            asm volatile("" : "+v"(R));
+            s = 2.f * s - vnp - unorm[R];
+        }
+        return float_key(s);
+    };
+    // a score whose key word is below its row's threshold word cannot enter
+    // the list: the test reads that word from LDS (the row's 64-bit threshold,
+    // high half), no registers held across tiles
+    const uint32_t* thr_hi = reinterpret_cast<const uint32_t*>(thr) + 1;
+    // branch-free (every operand read unconditionally, R < 64 always), so the
+    // scheduler can spread the tests between the MFMAs
+    const bool jp_ok_init = false;
+    bool jp_ok = jp_ok_init;   // Jp is a column of a real previous tile
+    auto pass_of = [&](int q) -> uint32_t {
+        const int R = row_of(q);
+        const uint32_t fk = score(q, accp[q]);
+        const uint32_t ok = (uint32_t)(R < nu) & (uint32_t)(fk >= thr_hi[2 * R]) & (uint32_t)jp_ok &
+                            ~(mbp >> q) & 1u;
+        return ok << q;
+    };
+    auto insert = [&](uint32_t pass) {
+        while (pass != 0u) {
+            const int q = __ffs(pass) - 1;
+            pass &= pass - 1u;
+            const int R = row_of(q);
+            const unsigned long long key = ((unsigned long long)score(q, accp[q]) << 32) |
+                                           (0xFFFFFFFFull - (unsigned long long)Jp);
+            if (key > thr[R]) {
+                const int pos = atomicAdd(&cnt[R], 1);
+                buf[R * kFusedCap + pos] = key;
+            }
+        }
+    };
+    auto compact_check = [&]() {
+        constexpr int kRowsPerWave = kFusedUsers / kWavesPerBlock;
+        const int Rl = wv + kWavesPerBlock * lane;
+        unsigned long long need = __ballot(lane < kRowsPerWave && Rl < nu &&
+                                           cnt[lane < kRowsPerWave ? Rl : 0] > kFusedCap - kFusedItems);
+        if (need != 0ull) {
+            while (need != 0ull) {
+                const int l = __ffsll((long long)need) - 1;
+                need &= need - 1ull;
+                const int R = wv + kWavesPerBlock * l;
+                wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+            }
+        }
+    };
+
+    for (int64_t j0 = 0; j0 < a.n_items; j0 += kFusedItems) {
+        if (!vec) {
+            for (int t = tid; t < kFusedItems * Dp; t += kBlock) {
+                const int r = t / Dp, kk = t - r * Dp;
+                const int64_t j = j0 + r;
+                Vs[vs_off(r, kk)] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
+            }
+        }
+        if (MODEL == GBPR && tid < kFusedItems)
+            bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
+        if (tid < kFusedUsers) {
+            unsigned long long m = 0ull;
+            while (nxt < j0 + kFusedItems) {
+                m |= 1ull << (int)(nxt - j0);
+                ++cur;
+                nxt = cur < end ? (int64_t)a.indices[cur] : INT64_MAX;
+            }
+            mask[tid] = m;
+        }
+        __syncthreads();
+        const bool more = vec && j0 + kFusedItems < a.n_items;
+        if (more) load_tile(j0 + kFusedItems);
+        // this tile's mask bits and bias, kept for its candidate test next step
+        uint32_t mbn = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) mbn |= (uint32_t)((mask[row_of(q)] >> jl) & 1ull) << q;
+        const float bn = (MODEL == GBPR) ? bt[jl] : 0.f;
+        floatx16 acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+        float vsq = 0.f;
+        const int br = wc * 32 + c;
+        uint32_t pass = 0;
+        // the swizzled B-operand address is formed where it is used: hoisted,
+        // its 16 values would hold 16 VGPRs through the whole sweep
+        auto bop = [&](int t0) {
+            int r = br, hd = h * Dh;
+            asm volatile("" : "+v"(r), "+v"(hd));
+            return *reinterpret_cast<const float4*>(Vs + vs_off(r, hd + t0));
+        };
+        auto mfma4 = [&](int t0, const float4 b4) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
+            if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+        };
+        if (Dh == kAH) {
+            // one previous-tile row test per group of four MFMAs (16 and 16);
+            // the next group's B operand is read before this group's MFMAs
+            float4 bc = bop(0);
+#pragma unroll
+            for (int t0 = 0; t0 < kAH; t0 += 4) {
+                const float4 bn4 = bop(t0 + 4 < kAH ? t0 + 4 : t0);
+                mfma4(t0, bc);
+                pass |= pass_of(t0 >> 2);
+                bc = bn4;
+            }
+        } else {
+#pragma unroll
+            for (int t0 = 0; t0 < kAH; t0 += 4)
+                if (t0 < Dh) mfma4(t0, bop(t0));   // block-uniform
+#pragma unroll
+            for (int q = 0; q < 16; ++q) pass |= pass_of(q);
+        }
+        insert(pass);
+        float vnorm = 0.f;
+        if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);
+        __syncthreads();
+        if (more) store_tile();
+        compact_check();
+        __syncthreads();
+        accp = acc;
+        mbp = mbn;
+        bp = bn;
+        vnp = vnorm;
+        Jp = j0 + jl;
+        jp_ok = Jp < a.n_items;
+    }
+    // the last tile's candidates
+    {
+        uint32_t pass = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pass |= pass_of(q);
+        insert(pass);
+    }
+    __syncthreads();
+    for (int R = wv; R < nu; R += kWavesPerBlock) {
+        const int n = wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        const int64_t orow = (int64_t)(u0 + R) * a.k;
+        if (lane < a.k) {
+            int id = -1;
+            float v = __int_as_float(0x7fc00000);
+            if (lane < n) {
+                const unsigned long long e = buf[R * kFusedCap + lane];
+                id = (int)(0xFFFFFFFFull - (e & 0xFFFFFFFFull));
+                v = key_float((uint32_t)(e >> 32));
+            }
+            a.idx_out[orow + lane] = id;
+            if (a.val_out) a.val_out[orow + lane] = v;
+        }
+    }
+}
+
 hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
     if (a.n_users <= 0) return hipSuccess;
     const dim3 grid((a.n_users + kFusedUsers - 1) / kFusedUsers), block(kBlock);
+    // CML's distance transform does not fit the pipelined kernel's registers
+    // at two blocks per CU (its A operands spill): it keeps the sequential one
+    if (a.variant == 0 && a.model != CML) {
+        if (a.model == GBPR)
+            hipLaunchKernelGGL(fused_topk_pipe_kernel<GBPR>, grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL(fused_topk_pipe_kernel<BPR>, grid, block, 0, s, a);
+        return hipGetLastError();
+    }
     switch (a.model) {
         case GBPR: hipLaunchKernelGGL(fused_topk_kernel<GBPR>, grid, block, 0, s, a); break;
         case CML: hipLaunchKernelGGL(fused_topk_kernel<CML>, grid, block, 0, s, a); break;

@@ -295,6 +295,7 @@ struct FusedTopkArgs {
     const int32_t* __restrict__ indices;
     int32_t* __restrict__ idx_out;       // [n_users, k]
     float* __restrict__ val_out;         // [n_users, k] (nullable)
+    int variant;                         // 0: software-pipelined kernel, 1: the sequential one
 };
 
 struct TopkArgs {
@@ -312,6 +313,8 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + cou
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
 // the phased gradient kernel's compile-time W (1 or 5) a step takes, 0 = generic
 int grad_fast_w(const StepArgs& a);
+// the step takes grad_lds_kernel (LDS-staged negatives)
+bool grad_lds(const StepArgs& a);
 // blocks (= loss partials) of the grad launch for this step shape
 int grad_blocks(const StepArgs& a, bool with_draw = false);
 int grad_blocks_max(int B);  // upper bound over every grad variant

@@ -1734,6 +1734,357 @@ __global__ __launch_bounds__(kWave) void grad_fast_wave_kernel(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// grad with LDS-staged negatives (d = 128, W = 5; BPR / AMF / CML; no
+// pos_sort, no fused draw): cfg3 / cfg5's instantiation.
+//
+// The phased kernel keeps a pair's seven rows plus the accumulators of its
+// singleton rows in registers: 218 VGPRs at d = 128 (2 waves / SIMD; CML 256
+// + AGPRs, 1 wave).  Here the five negative rows of a wave's four pairs go
+// from memory straight into LDS with global_load_lds_dwordx4 -- no VGPR
+// destination, one wave-instruction moves two 512-B rows -- 40 KB per block,
+// so four blocks (16 waves) fit a CU's 160 KB, and registers hold only u, i
+// and the accumulator rows.  A negative's row is read from LDS where its term
+// is formed (BPR / AMF once; CML for the distance, then for the gradient).
+// Each wave reads only the rows it staged itself: no barrier.
+// Element mapping: slot s of lane gl is element ((s ^ par) << 4) | gl, par =
+// the group's parity, so the two groups of a ds_read_b32 half-wave (lanes
+// 0-31, 32-63) hit different banks (staged rows are 128 dwords apart).
+// Same arithmetic as grad_fast_kernel up to fp32 summation order.
+// ---------------------------------------------------------------------------
+constexpr int kLdsRow = 128;   // floats per staged row
+
+__device__ __forceinline__ int elem_par(int s, int gl, int par) { return ((s ^ par) << 4) | gl; }
+
+// full rows only (d == 16 * EPL): no element masks, straight-line code
+template <int EPL>
+__device__ __forceinline__ void prow_ld(const float* __restrict__ row, int gl, int par, float (&x)[EPL]) {
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) x[s] = row[elem_par(s, gl, par)];
+}
+
+template <int EPL>
+__device__ __forceinline__ void prow_st(float* __restrict__ row, int gl, int par, const float (&x)[EPL]) {
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) row[elem_par(s, gl, par)] = x[s];
+}
+
+template <int EPL>
+__device__ __forceinline__ void prow_atomic(float* __restrict__ row, int gl, int par, const float (&g)[EPL]) {
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) unsafeAtomicAdd(row + elem_par(s, gl, par), g[s]);
+}
+
+// gapply_pre / gfinish_pre / ifinish_pre in the parity mapping
+template <int EPL>
+__device__ __forceinline__ void papply(float* __restrict__ X, float* __restrict__ A, int64_t r, int d, int gl,
+                                       int par, const float (&x0)[EPL], const float (&acc0)[EPL],
+                                       const float (&g)[EPL], float lr, bool clip, float c) {
+    float acc[EPL], x[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        acc[s] = fmaf(g[s], g[s], acc0[s]);
+        x[s] = x0[s] - adagrad_delta(lr, g[s], acc[s]);
+    }
+    if (clip) {
+        const float n = sqrtf(gdot<EPL>(x, x));
+        const float den = fmaxf(n, c);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) x[s] = (x[s] * c) / den;
+    }
+    prow_st<EPL>(X + r * (int64_t)d, gl, par, x);
+    prow_st<EPL>(A + r * (int64_t)d, gl, par, acc);
+}
+
+template <int EPL>
+__device__ __forceinline__ void pfinish(float* __restrict__ X, float* __restrict__ A, float* __restrict__ G,
+                                        float* __restrict__ S, int32_t* __restrict__ cnt, int64_t r, int count,
+                                        int64_t slot, int d, int gl, int par, const float (&x0)[EPL],
+                                        const float (&acc0)[EPL], const float (&g)[EPL], const StepArgs& a) {
+    if (count == 1) {
+        if (a.items_grad_only && X == a.V)
+            prow_st<EPL>(G + r * (int64_t)d, gl, par, g);   // sole writer of the zeroed dense row
+        else
+            papply<EPL>(X, A, r, d, gl, par, x0, acc0, g, a.lr, a.clip != 0, a.clip_norm);
+        if (gl == 0) cnt[r] = 0;
+    } else if (slot >= 0) {
+        prow_st<EPL>(S + slot * (int64_t)d, gl, par, g);
+    } else {
+        prow_atomic<EPL>(acc_of(G, slot, a) + r * (int64_t)d, gl, par, g);
+        if (a.items_grad_only && a.capV == 0 && X == a.V && gl == 0) cnt[r] = 0;  // see gfinish
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void pifinish(const StepArgs& a, int64_t r, int count, int64_t slot, int p,
+                                         float alpha, float beta, int gl, int par, const float (&x0)[EPL],
+                                         const float (&acc0)[EPL], const float (&g)[EPL]) {
+    if (a.recV != nullptr && count >= 2 && slot >= 0) {
+        if (gl == 0) a.recV[slot] = make_int4(p, __float_as_int(alpha), __float_as_int(beta), 0);
+        return;
+    }
+    pfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, r, count, slot, a.d, gl, par, x0, acc0, g, a);
+}
+
+template <int EPL>
+__device__ __forceinline__ void pacc_ld(const float* __restrict__ A, int64_t r, int d, int gl, int par, bool want,
+                                        float (&acc)[EPL]) {
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) acc[s] = 1.f;
+    if (want) prow_ld<EPL>(A + r * (int64_t)d, gl, par, acc);
+}
+
+// minimum waves per SIMD the LDS-staged kernel is built for (1 = the
+// compiler's register budget; LDS alone allows 4)
+#ifndef CF_LDS_WAVES
+#define CF_LDS_WAVES 1
+#endif
+#define CF_LDS_ATTR __attribute__((amdgpu_waves_per_eu(CF_LDS_WAVES, 8)))
+// one negative's LDS reads are not hoisted above the previous negative's
+// terms (the scheduler would otherwise keep all five rows live)
+#ifndef CF_LDS_FENCE
+#define CF_LDS_FENCE 1
+#endif
+#if CF_LDS_FENCE
+#define CF_LDS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define CF_LDS_SCHED_FENCE() ((void)0)
+#endif
+template <int MODEL, int WT>
+__global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a) {
+    constexpr int EPL = 8;
+    constexpr int RPW = (kWave / kGL) * WT;   // staged rows per wave
+    static_assert(RPW % 2 == 0, "two rows per LDS-DMA wave-instruction");
+    static_assert(MODEL == BPR || MODEL == AMF || MODEL == CML, "no group users / tuples here");
+    // exactly 40 KB, so four blocks fit a CU (the loss partials reuse it)
+    __shared__ float s_v[kGroupsPerBlock * WT * kLdsRow];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int gl = threadIdx.x & (kGL - 1);
+    const int grp = threadIdx.x >> 4;
+    const int par = grp & 1;
+    const int d = a.d;
+    const int p = blockIdx.x * kGroupsPerBlock + grp;
+    const bool ok = p < a.B;
+
+    // ids (every lane of the group loads the same words)
+    int u = 0, i = 0, ru = 0, ri = 0;
+    int j[WT], rj[WT];
+#pragma unroll
+    for (int w = 0; w < WT; ++w) {
+        j[w] = -1;
+        rj[w] = 0;
+    }
+    if (ok) {
+        u = a.occU[p];
+        i = a.occV[p];
+        ru = a.count_users ? a.rankU[p] : 0;
+        ri = a.count_items ? a.rankV[p] : 0;
+#pragma unroll
+        for (int w = 0; w < WT; ++w) {
+            j[w] = a.occV[a.B + p * WT + w];
+            rj[w] = a.count_items ? a.rankV[a.B + p * WT + w] : 0;
+        }
+    }
+    // stage the negatives: wave-instruction k moves the wave's rows 2k (lanes
+    // 0-31) and 2k + 1 (lanes 32-63), 16 B per lane; row r is negative r % WT
+    // of the wave's pair r / WT, whose id lane (r / WT) * 16 + r % WT holds
+    {
+        int jsel = -1;
+#pragma unroll
+        for (int w = 0; w < WT; ++w)
+            if (gl == w) jsel = j[w];
+        float* wbase = s_v + (threadIdx.x >> 6) * RPW * kLdsRow;
+        const int c4 = (lane & 31) * 4;
+#pragma unroll
+        for (int k = 0; k < RPW / 2; ++k) {
+            const int r = 2 * k + (lane >> 5);
+            const int q = r / WT;
+            const int jj = __shfl(jsel, q * kGL + (r - q * WT), kWave);
+            if (jj >= 0)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(a.V + (int64_t)jj * d + c4),
+                    (__attribute__((address_space(3))) void*)(wbase + 2 * k * kLdsRow), 16, 0, 0);
+        }
+    }
+    // counts and the u / i rows, then slots and the accumulator rows of the
+    // rows this batch touches once
+    int cu = 0, ci = 0, cj[WT];
+    float uu[EPL], vi[EPL];
+#pragma unroll
+    for (int w = 0; w < WT; ++w) cj[w] = 0;
+    if (ok) {
+        cu = a.count_users ? a.cntU[u] : 0;
+        ci = a.count_items ? a.cntV[i] : 0;
+#pragma unroll
+        for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
+        prow_ld<EPL>(a.U + (int64_t)u * d, gl, par, uu);
+        prow_ld<EPL>(a.V + (int64_t)i * d, gl, par, vi);
+    }
+    int64_t su = -1, si = -1, sj[WT];
+    float au[EPL], ai[EPL];
+    const bool item_acc = !a.items_grad_only;
+    if (ok) {
+        su = slot_of(cu, u, ru, a.capU, 0, a.offU);
+        si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
+#pragma unroll
+        for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
+        pacc_ld<EPL>(a.AU, u, d, gl, par, cu == 1, au);
+        pacc_ld<EPL>(a.AV, i, d, gl, par, item_acc && ci == 1, ai);
+    }
+    // the staged rows have landed (an LDS-DMA retires on vmcnt).  The
+    // builtin, not inline asm: the compiler's wait tracking sees it and stops
+    // guarding every later LDS read with a vmcnt wait for the DMA
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) expcnt(7) lgkmcnt(15)
+
+    float loss_g = 0.f, sq = 0.f;
+    if (ok) {
+        const float* sv = s_v + grp * WT * kLdsRow;
+        if (a.recV != nullptr) {   // item records' X: only pairs that leave one
+            bool need = ci >= 2 && si >= 0;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) need |= cj[w] >= 2 && sj[w] >= 0;
+            if (need) prow_st<EPL>(a.stashU + (int64_t)p * d, gl, par, uu);
+        }
+        if (MODEL == BPR || MODEL == AMF) {
+            // terms first (no stores), then u and i, then the negatives'
+            // gradient rows from the staged rows again: no store of one
+            // negative sits between the next one's loads and their use
+            const float ui = gdot<EPL>(uu, vi);
+            float gu[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
+            float sc = 0.f;
+            float cw[WT];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                float vj[EPL];
+                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+                const float x = ui - gdot<EPL>(uu, vj);
+                float c = -rcp_1p(expf(x));
+                if (MODEL == AMF) {
+                    loss_g += softplus(-x);
+                    if (a.adversarial) {
+                        const float xc = fmaxf(fminf(x, 1e8f), -80.f);
+                        loss_g += a.reg_adv * softplus(-xc);
+                        if (x >= -80.f && x <= 1e8f) c *= (1.f + a.reg_adv);
+                    }
+                } else {
+                    loss_g += neg_log_sigmoid(x);
+                }
+                sc += c;
+                cw[w] = c;
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] = fmaf(c, vi[s] - vj[s], gu[s]);
+                    sq = fmaf(vj[s], vj[s], sq);
+                }
+            }
+            float gi[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] += a.reg * uu[s];
+                gi[s] = sc * uu[s] + a.reg * vi[s];
+                sq = fmaf(uu[s], uu[s], sq);
+                sq = fmaf(vi[s], vi[s], sq);
+            }
+            pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, par, uu, au, gu, a);
+            pifinish<EPL>(a, i, ci, si, p, sc, a.reg, gl, par, vi, ai, gi);
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                CF_LDS_SCHED_FENCE();
+                float vj[EPL], aj[EPL], gj[EPL];
+                pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aj);
+                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) gj[s] = -cw[w] * uu[s] + a.reg * vj[s];
+                pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], a.reg, gl, par, vj, aj, gj);
+            }
+        } else {  // CML
+            float du[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) du[s] = uu[s] - vi[s];
+            const float dp = gdot<EPL>(du, du);
+            float dn[WT];
+            float m = INFINITY;
+            int imp = 0;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                CF_LDS_SCHED_FENCE();
+                float t[EPL];
+                prow_ld<EPL>(sv + w * kLdsRow, gl, par, t);
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) t[s] = uu[s] - t[s];
+                dn[w] = gdot<EPL>(t, t);
+                m = fminf(m, dn[w]);
+                imp += (dp - dn[w] + a.margin > 0.f) ? 1 : 0;
+            }
+            float cnt = 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) cnt += (dn[w] == m) ? 1.f : 0.f;
+            const float z = dp - m + a.margin;
+            const float lw = a.use_rank_weight ? logf((float)imp / (float)WT * a.n_items_f + 1.f) : 1.f;
+            loss_g += fmaxf(z, 0.f) * lw;
+            const float aa = (z > 0.f) ? lw : 0.f;
+            const bool l2 = a.reg_cov > 0.f;
+            float gu[EPL], gi[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] = 2.f * aa * du[s];
+                gi[s] = -2.f * aa * du[s];
+            }
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                const float share = (dn[w] == m) ? 1.f / cnt : 0.f;
+                const float coef = 2.f * aa * share;
+                CF_LDS_SCHED_FENCE();
+                float vj[EPL], gj[EPL], aj[EPL];
+                pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aj);
+                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    const float dv = uu[s] - vj[s];
+                    gu[s] = fmaf(-coef, dv, gu[s]);
+                    gj[s] = coef * dv;
+                    if (l2) {
+                        gj[s] += a.reg_cov * vj[s];
+                        sq = fmaf(vj[s], vj[s], sq);
+                    }
+                }
+                // a touched row with a zero gradient is still clipped (cml.py:128-129)
+                pifinish<EPL>(a, j[w], cj[w], sj[w], p, coef, (l2 ? a.reg_cov : 0.f) - coef, gl, par, vj,
+                              aj, gj);
+            }
+            if (l2) {
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    gu[s] += a.reg_cov * uu[s];
+                    gi[s] += a.reg_cov * vi[s];
+                    sq = fmaf(uu[s], uu[s], sq);
+                    sq = fmaf(vi[s], vi[s], sq);
+                }
+            }
+            pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, par, uu, au, gu, a);
+            pifinish<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), gl, par, vi, ai, gi);
+        }
+    }
+
+    // each group's loss partial goes into its own wave's staged rows, which
+    // that wave no longer reads
+    const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
+    const float sq_g = gsum(sq);
+    double* s_loss = reinterpret_cast<double*>(s_v);
+    constexpr int kWaveD = RPW * kLdsRow / 2;   // doubles per wave region
+    if (gl == 0)
+        s_loss[(grp >> 2) * kWaveD + (grp & 3)] = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < kGroupsPerBlock; ++k) t += s_loss[(k >> 2) * kWaveD + (k & 3)];
+        a.loss_partial[blockIdx.x] = t;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // apply the summed gradient of every duplicated row: the TF1 IndexedSlices
 // dedup-sum + SparseApplyAdagrad (bprmf.py:74-75 and siblings).
 // One lane per work item -- the batch's user occurrences, item occurrences
@@ -2555,18 +2906,33 @@ static int epl_for(int d) {
 #define CF_FAST_PAIRS_GBPR_W5 2
 #endif
 
+#ifndef CF_GRAD_LDS
+#define CF_GRAD_LDS 1   // 0: auto never takes grad_lds_kernel (grad_path 3 still does)
+#endif
+
+// the LDS-staged W = 5 kernel (grad_lds_kernel): grad_path 3, or auto where
+// it applies; its grid is the phased kernel's at one pair per group
+static bool lds_path(const StepArgs& a) {
+    const bool want = a.grad_path == 3 || (a.grad_path == 0 && CF_GRAD_LDS);
+    return want && a.W == 5 && a.d == kLdsRow && a.srec == nullptr &&
+           (a.model == BPR || a.model == AMF || a.model == CML);
+}
+
 // which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
-// fast, 0 = generic
+// fast (or the LDS-staged kernel), 0 = generic
 static int fast_w(const StepArgs& a) {
+    if (lds_path(a)) return 5;
     // CML at W = 5 keeps five distance rows and the clip live per pair: the
-    // generic kernel measured faster there (cfg3: 160 vs 184 us), so auto
-    // (grad_path 0) leaves it on the generic kernel; 2 forces the fast path
+    // generic kernel measured faster than the phased one there (cfg3: 160 vs
+    // 184 us), so auto (grad_path 0) leaves it on the generic kernel unless
+    // the LDS-staged kernel applies; 2 forces the phased kernel
     const bool ok = a.grad_path != 1 && epl_for(a.d) <= 8 && (a.model != GBPR || a.G == 1) &&
                     !(a.grad_path == 0 && a.model == CML && a.W == 5);
     return ok && (a.W == 1 || a.W == 5) ? a.W : 0;
 }
 
 int grad_fast_w(const StepArgs& a) { return fast_w(a); }
+bool grad_lds(const StepArgs& a) { return lds_path(a); }
 
 #ifndef CF_GRAD_WAVE_BLOCKS
 // 1: fast path without draw blocks in one-wave workgroups (measured no faster
@@ -2686,6 +3052,14 @@ static hipError_t launch_grad_plr(const StepArgs& a, hipStream_t s) {
 template <int MODEL>
 static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     const int e = epl_for(a.d);
+    if constexpr (MODEL == BPR || MODEL == AMF || MODEL == CML) {
+        // a fused draw (pipeline 2) takes the phased kernel: same grid
+        if (lds_path(a) && prep_blocks(nx) == 0) {
+            const dim3 grid((a.B + kGroupsPerBlock - 1) / kGroupsPerBlock), block(kBlock);
+            hipLaunchKernelGGL((grad_lds_kernel<MODEL, 5>), grid, block, 0, s, a);
+            return hipGetLastError();
+        }
+    }
     const int fw = fast_w(a);
     if (fw == 1) return launch_grad_fast<MODEL, 1, CF_FAST_PAIRS_W1>(a, nx, s);
     if (fw == 5 && MODEL == GBPR && e <= 4) return launch_grad_fast<MODEL, 5, CF_FAST_PAIRS_GBPR_W5>(a, nx, s);

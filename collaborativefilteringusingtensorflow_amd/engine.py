@@ -390,7 +390,8 @@ class Engine(object):
                 "cf_score_topk")
         return (idx, val) if return_values else idx
 
-    PATH_FLAGS = {"phased": 1, "pos_sort": 2, "item_records": 4, "deterministic": 8, "dense_items": 16}
+    PATH_FLAGS = {"phased": 1, "pos_sort": 2, "item_records": 4, "deterministic": 8, "dense_items": 16,
+                  "lds": 32}
 
     def step_path(self, batch_size):
         """The kernel path a step of ``batch_size`` pairs takes now

@@ -339,7 +339,8 @@ enum cf_path_flag {
     CF_PATH_POS_SORT = 2,       /* positive-sorted gradient (psort + partial rows)         */
     CF_PATH_ITEM_RECORDS = 4,   /* item records + user-row stash instead of slot rows      */
     CF_PATH_DETERMINISTIC = 8,  /* sort-based ranks, compact slots, no float atomics       */
-    CF_PATH_DENSE_ITEMS = 16    /* multi-rank item path (dense item gradient)              */
+    CF_PATH_DENSE_ITEMS = 16,   /* multi-rank item path (dense item gradient)              */
+    CF_PATH_LDS = 32            /* gradient kernel with LDS-staged negatives (grad_lds_kernel) */
 };
 int cf_step_path(cf_engine* eng, int32_t B, int32_t* flags_out);
 
@@ -375,10 +376,16 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 28 and d <= 128, else
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
- *   "grad_path"  0 = auto (phased gradient kernel for W in {1,5}, d <= 128,
+ *   "fused_variant" the fused scoring + top-k kernel: 0 = software-pipelined
+ *                (tile t's candidate test beside tile t+1's MFMAs, default),
+ *                1 = sequential (MFMAs, then candidates).  Same output.
+ *   "grad_path"  0 = auto (BPR / AMF / CML at W = 5, 64 < d <= 128, d % 4 == 0
+ *                without pos_sort: the kernel with LDS-staged negative rows;
+ *                else the phased gradient kernel for W in {1,5}, d <= 128,
  *                GBPR group size 1, except CML at W = 5; generic kernel
  *                otherwise), 1 = generic kernel always, 2 = phased kernel
- *                whenever eligible.  All give the same arithmetic.
+ *                whenever eligible, 3 = the LDS-staged kernel whenever
+ *                eligible.  All give the same arithmetic.
  *   "prep_stream" 0 = everything in order on the engine stream (default);
  *                1 = sample/count on a side stream, overlapping the previous
  *                step's gradient.  Same results.

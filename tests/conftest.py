@@ -26,6 +26,14 @@ RTOL, ATOL = 1e-5, 1e-6
 # accumulators sum their squares) and stays inside this relaxed one
 # (tests/test_oracle.py::test_fp32_oracle_drift_bounds_cml_tolerance)
 CML_TRAJ = dict(rtol=5e-5, atol=3e-6)
+# Ensemble stress shapes (tests/test_gpu_ensemble.py::test_ensemble_ragged_hot_rows:
+# 50 x 80 tables, a hot user in a third of the pairs, the [B, B] cross loss of
+# ensemble.py:84-91 summed into each row): the oracle run in float32 leaves
+# the rtol 1e-4 band around the float64 oracle by up to 7.4x within six
+# steps (an accumulator 2.9157 in float64 is 2.9132 in float32: sums of ~B^2
+# cancelling terms per row), and stays under 0.5 of this one
+# (tests/test_oracle.py::test_fp32_oracle_drift_bounds_ensemble_tolerance)
+ENS_HOT = dict(rtol=2e-3, atol=1e-4)
 
 
 def assert_close(got, ref, what, rtol=RTOL, atol=ATOL):

@@ -3,8 +3,8 @@
 
 * trajectories on ml-100k fold 1 through the device-sampler pipeline
   (cf_train_steps: draw of step s+1 fused into the apply of step s) at the
-  bench shapes: CML d=128, W=5 on the generic (auto) and the phased gradient
-  kernel (cml.py:55-129); GBPR d=64, W=5, G=1 on the phased kernel
+  bench shapes: CML d=128, W=5 on the LDS-staged (auto), the generic and the
+  phased gradient kernel (cml.py:55-129); GBPR d=64, W=5, G=1 on the phased kernel
   (gbprmf.py:58-106); AMF d=128, W=5 across the phase switch
   (amf.py:139-162, 216-244).  The oracle replays the same batches (an engine
   with the same seed draws the identical stream with cf_sample).
@@ -69,11 +69,14 @@ TABLES = {"cml": ("user", "item", "acc_user", "acc_item"),
 
 
 @pytest.mark.parametrize("model,d,grad_path,switch", [
-    ("cml", 128, 0, None),    # cfg3 as benched: auto = the generic kernel for CML at W = 5
+    ("cml", 128, 0, None),    # cfg3 as benched: auto = the LDS-staged kernel (grad_lds_kernel)
+    ("cml", 128, 1, None),    # cfg3 on the generic kernel
     ("cml", 128, 2, None),    # cfg3 on the phased kernel
     ("gbpr", 64, 0, None),    # cfg4: auto = phased grad_fast_kernel<GBPR, EPL 4, W 5>
-    ("amf", 128, 0, 14),      # cfg5 across the phase switch (fresh accumulators)
-], ids=["cml-d128-generic", "cml-d128-phased", "gbpr-d64-w5-g1", "amf-d128-switch"])
+    ("amf", 128, 0, 14),      # cfg5 across the phase switch (fresh accumulators), LDS-staged
+    ("amf", 128, 2, 14),      # cfg5 on the phased kernel
+], ids=["cml-d128-lds", "cml-d128-generic", "cml-d128-phased", "gbpr-d64-w5-g1", "amf-d128-switch",
+        "amf-d128-switch-phased"])
 @pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
 def test_bench_shape_pipeline_trajectory(fold1, model, d, grad_path, switch, item_slots):
     W, B, K = 5, 100, 28
@@ -107,16 +110,19 @@ def _cfg2_graph():
     return synth_graph(1_000_000, 100_000, 50.0, 0.8, 20261015, n_threads=16)
 
 
+@pytest.mark.parametrize("grad_path", [0, 2], ids=["auto-lds", "phased"])
 @pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
 @pytest.mark.parametrize("model", ["cml", "amf"], ids=["cfg3-cml", "cfg5-amf-phase2"])
-def test_full_size_step(model, item_slots):
+def test_full_size_step(model, item_slots, grad_path):
     """One step at full cfg3 / cfg5 size (1M users x 100K items, d=128, W=5,
-    B=65,536), after three pipelined steps, against the float64 oracle."""
+    B=65,536), after three pipelined steps, against the float64 oracle; auto
+    is the LDS-staged kernel the bench runs."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni, d, W, B = 1_000_000, 100_000, 128, 5, 65536
     ip, ix = _cfg2_graph()
     e = Engine(model, nu, ni, d, n_neg=W, seed=78, **HP[model])
     e.set_option("item_slots", item_slots)
+    e.set_option("grad_path", grad_path)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=1)
     if model == "amf":
@@ -185,14 +191,17 @@ def _check_lists(gpu_idx, scores, ref_lists, atol):
                 assert abs(scores[r][a] - scores[r][b]) <= atol, (r, a, b, scores[r][a], scores[r][b])
 
 
-def test_fused_topk_d128_cfg5_slice():
+@pytest.mark.parametrize("fused_variant", [0, 1], ids=["pipelined", "sequential"])
+def test_fused_topk_d128_cfg5_slice(fused_variant):
     """The fused fp32-MFMA scoring + streaming top-10 (the cfg5 scoring
     kernel, amf.py:144-148 + bprmf.py:90-103) at d=128 on 4,096 users of the
-    cfg5 graph, train items excluded."""
+    cfg5 graph, train items excluded; both fused kernels (the bench's
+    score pass runs the pipelined one)."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni, d = 1_000_000, 100_000, 128
     ip, ix = _cfg2_graph()
     e = Engine("amf", nu, ni, d, n_neg=5, seed=80, **HP["amf"])
+    e.set_option("fused_variant", fused_variant)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=True, seed=1)
     e.train_steps(65536, 2)

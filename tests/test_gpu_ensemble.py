@@ -11,7 +11,7 @@ with ragged B, hot rows and repeated items."""
 import numpy as np
 import pytest
 
-from conftest import assert_close, get_stream
+from conftest import ENS_HOT, assert_close, get_stream
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -35,10 +35,11 @@ def make(K, nu, ni, d, reg, seed=5):
     return e, U.astype(np.float64), V.astype(np.float64), H.astype(np.float64)
 
 
-def check_tables(e, U, V, H, AU, AV, AH):
+def check_tables(e, U, V, H, AU, AV, AH, tol=None):
+    tol = tol or dict(rtol=RTOL, atol=ATOL)
     for name, o in (("user", U), ("item", V), ("h", H), ("acc_user", AU), ("acc_item", AV),
                     ("acc_h", AH)):
-        assert_close(e.get_table(name), o, name, rtol=RTOL, atol=ATOL)
+        assert_close(e.get_table(name), o, name, **tol)
 
 
 @pytest.mark.parametrize("K,d,reg", [(3, 100, 0.01), (2, 20, 0.1), (1, 16, 0.05)])
@@ -68,7 +69,8 @@ def test_ensemble_ragged_hot_rows(K, B, d):
         lg = e.step(uij)
         lo = O.ens_step(U, V, H, AU, AV, AH, uij, 0.02)
         assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
-    check_tables(e, U, V, H, AU, AV, AH)
+    # fp32-grounded band: the float32 oracle itself leaves rtol 1e-4 here
+    check_tables(e, U, V, H, AU, AV, AH, tol=ENS_HOT)
     e.close()
 
 

@@ -1,6 +1,8 @@
 """GPU parity of the recommend step (bprmf.py:77-103 and siblings): scores,
 train-item exclusion and top-k order (descending, ties to the lower id, TF
-TopKV2) against the oracle's literal restatement."""
+TopKV2) against the oracle's literal restatement.  Every test runs on both
+fused kernels (cf_set_option fused_variant: the software-pipelined one and
+the sequential one)."""
 import numpy as np
 import pytest
 
@@ -8,11 +10,21 @@ from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
 
+_FV = [0]
+
+
+@pytest.fixture(autouse=True, params=[0, 1], ids=["fused-pipe", "fused-seq"])
+def fused_variant(request):
+    _FV[0] = request.param
+    yield request.param
+    _FV[0] = 0
+
 
 def setup(model, fold1, d, seed, bias=False, truncated=True):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
     e = Engine(model, nu, ni, d, n_neg=1, gsize=1, seed=1)
+    e.set_option("fused_variant", _FV[0])
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     rng = np.random.RandomState(seed)
     U = O.init_table(rng, (nu, d), truncated=truncated)
@@ -76,6 +88,7 @@ def test_ties_go_to_lower_id(fold1, path):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
     e = Engine("bpr", nu, ni, 4, seed=1)
+    e.set_option("fused_variant", _FV[0])
     e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
     U = np.ones((nu, 4), np.float32)
     V = np.zeros((ni, 4), np.float32)
@@ -103,6 +116,7 @@ def test_exclusion_and_padding(fold1, path):
     ip = np.array([0, 8, 9], np.int64)
     ix = np.array(list(range(8)) + [3], np.int32)
     e = Engine("bpr", 2, 10, 4, seed=1)
+    e.set_option("fused_variant", _FV[0])
     e.set_interactions(ip, ix)
     rng = np.random.RandomState(0)
     e.set_table("user", rng.randn(2, 4).astype(np.float32))
