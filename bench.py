@@ -320,7 +320,7 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-ndcg", action="store_true", help="skip the cfg1 NDCG@10 check")
     ap.add_argument("--fused-variant", type=int, default=0,
-                    help="cf_set_option fused_variant: 0 software-pipelined fused scoring + top-k, 1 sequential")
+                    help="cf_set_option fused_variant: 0 sequential fused scoring + top-k, 1 software-pipelined")
     ap.add_argument("--score-pass", action="store_true",
                     help="also time one full scoring + top-10 pass over this rank's users")
     ap.add_argument("--grad-path", type=int, default=0,
@@ -686,7 +686,7 @@ def main():
         out["score_pass"] = {"users": nu_all, "items": ni, "d": d, "k": 10, "seconds": ts,
                              "TFLOPs": flop / ts / 1e12,
                              "frac_fp32_mfma_peak": flop / ts / 1e12 / (157.3 * world),
-                             "kernel": ("fused_topk_pipe_kernel" if args.fused_variant == 0 and cfg["model"] != "cml"
+                             "kernel": ("fused_topk_pipe_kernel" if args.fused_variant == 1 and cfg["model"] != "cml"
                                         else "fused_topk_kernel") +
                                        " (v_mfma_f32_32x32x2_f32 + streaming top-k)",
                              "kernel_ms_hip_events": tk_ms if tk_n else None,

@@ -294,6 +294,9 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
     return r * kFusedMaxD + ((((kk >> 2) ^ (r & 31)) << 2) | (kk & 3));
 }
 
+#ifndef CF_FUSED_BPREFETCH
+#define CF_FUSED_BPREFETCH 1   // read each MFMA group's B operand one group ahead
+#endif
 template <int MODEL>
 __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) {
     // ~80 KB of LDS: two blocks per CU.  The user operands live in registers.
@@ -420,8 +423,24 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         float vsq = 0.f;
         const int br = wc * 32 + c;              // B operand row (item) of this lane
 #ifndef CF_FUSED_EXP_NOMFMA   // attribution builds (wrong results by design)
+#if CF_FUSED_BPREFETCH
+        auto bop = [&](int t0) {   // address formed at use (hoisted: 16 VGPRs)
+            int r = br, hd = h * Dh;
+            asm volatile("" : "+v"(r), "+v"(hd));
+            return *reinterpret_cast<const float4*>(Vs + vs_off(r, hd + t0));
+        };
+#else
+        auto bop = [&](int t0) { return *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0)); };
+#endif
+        auto mfma4b = [&](int t0, const float4 b4) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, acc, 0, 0, 0);
+            if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+        };
         auto mfma4 = [&](int t0) {
-            const float4 b4 = *reinterpret_cast<const float4*>(Vs + vs_off(br, h * Dh + t0));
+            const float4 b4 = bop(t0);
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, acc, 0, 0, 0);
@@ -432,8 +451,20 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
             // branch-free: a conditional per k-chunk made the compiler wait
             // for every outstanding global load (the prefetched next tile)
             // at each chunk (s_waitcnt vmcnt(0) before the LDS reads)
+#if CF_FUSED_BPREFETCH
+            // the next group's B operand is read before this group's MFMAs,
+            // so no MFMA group waits on its own LDS read
+            float4 bc = bop(0);
+#pragma unroll
+            for (int t0 = 0; t0 < kAH; t0 += 4) {
+                const float4 bn4 = bop(t0 + 4 < kAH ? t0 + 4 : t0);
+                mfma4b(t0, bc);
+                bc = bn4;
+            }
+#else
 #pragma unroll
             for (int t0 = 0; t0 < kAH; t0 += 4) mfma4(t0);
+#endif
         } else {
 #pragma unroll
             for (int t0 = 0; t0 < kAH; t0 += 4)
@@ -515,7 +546,9 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
 }
 
 // ---------------------------------------------------------------------------
-// The same pass software-pipelined across item tiles (variant 0, default):
+// The same pass software-pipelined across item tiles (fused_variant 1;
+// measured SLOWER than the sequential kernel, 63 vs 85.6 TFLOP/s at cfg5 on
+// one box, profiles/r03/score_pass/ -- kept for A/B, not the default):
 // while a wave's MFMAs build tile t's scores in one accumulator set, the
 // candidate test of tile t-1 runs on the other set, one row (q) per group of
 // four MFMAs -- the VALU work issues in the shadow of the matrix core instead
@@ -783,7 +816,7 @@ hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
     const dim3 grid((a.n_users + kFusedUsers - 1) / kFusedUsers), block(kBlock);
     // CML's distance transform does not fit the pipelined kernel's registers
     // at two blocks per CU (its A operands spill): it keeps the sequential one
-    if (a.variant == 0 && a.model != CML) {
+    if (a.variant == 1 && a.model != CML) {
         if (a.model == GBPR)
             hipLaunchKernelGGL(fused_topk_pipe_kernel<GBPR>, grid, block, 0, s, a);
         else

@@ -295,7 +295,7 @@ struct FusedTopkArgs {
     const int32_t* __restrict__ indices;
     int32_t* __restrict__ idx_out;       // [n_users, k]
     float* __restrict__ val_out;         // [n_users, k] (nullable)
-    int variant;                         // 0: software-pipelined kernel, 1: the sequential one
+    int variant;                         // 0: the sequential kernel, 1: software-pipelined (A/B)
 };
 
 struct TopkArgs {

@@ -376,9 +376,10 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 28 and d <= 128, else
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
- *   "fused_variant" the fused scoring + top-k kernel: 0 = software-pipelined
- *                (tile t's candidate test beside tile t+1's MFMAs, default),
- *                1 = sequential (MFMAs, then candidates).  Same output.
+ *   "fused_variant" the fused scoring + top-k kernel: 0 = sequential (MFMAs,
+ *                then the candidate test; default), 1 = software-pipelined
+ *                (tile t's candidate test beside tile t+1's MFMAs; measured
+ *                slower, kept for A/B; CML always takes 0).  Same output.
  *   "grad_path"  0 = auto (BPR / AMF / CML at W = 5, 64 < d <= 128, d % 4 == 0
  *                without pos_sort: the kernel with LDS-staged negative rows;
  *                else the phased gradient kernel for W in {1,5}, d <= 128,

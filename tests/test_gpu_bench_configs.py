@@ -191,12 +191,12 @@ def _check_lists(gpu_idx, scores, ref_lists, atol):
                 assert abs(scores[r][a] - scores[r][b]) <= atol, (r, a, b, scores[r][a], scores[r][b])
 
 
-@pytest.mark.parametrize("fused_variant", [0, 1], ids=["pipelined", "sequential"])
+@pytest.mark.parametrize("fused_variant", [0, 1], ids=["sequential", "pipelined"])
 def test_fused_topk_d128_cfg5_slice(fused_variant):
     """The fused fp32-MFMA scoring + streaming top-10 (the cfg5 scoring
     kernel, amf.py:144-148 + bprmf.py:90-103) at d=128 on 4,096 users of the
     cfg5 graph, train items excluded; both fused kernels (the bench's
-    score pass runs the pipelined one)."""
+    score pass runs the sequential one)."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni, d = 1_000_000, 100_000, 128
     ip, ix = _cfg2_graph()

@@ -172,8 +172,8 @@ def test_cfg2_full_size_step_parity(cfg2_graph):
 
 def test_cfg2_bench_batch_pos_sort_matches_oracle(cfg2_graph):
     """The benched cfg2 instantiation itself: B = 2^19 pairs per step with
-    pos_sort auto (on), i.e. psort + grad_fast_kernel<BPR, d 64, W 1, SORT>
-    + the PS apply fused with the next draw (apply_prep_kernel), where the
+    pos_sort auto (on), i.e. psort + grad_sort_kernel<BPR, d 64, W 1> + the
+    pos_sort apply fused with the next draw (apply_ps_kernel), where the
     Zipf-head positives' partials overflow capP into float atomics.  Three
     pipelined steps move off the initial state; then two more pipelined
     steps (cf_train_steps: the first one's apply launch draws the second's

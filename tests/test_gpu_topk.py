@@ -1,8 +1,8 @@
 """GPU parity of the recommend step (bprmf.py:77-103 and siblings): scores,
 train-item exclusion and top-k order (descending, ties to the lower id, TF
 TopKV2) against the oracle's literal restatement.  Every test runs on both
-fused kernels (cf_set_option fused_variant: the software-pipelined one and
-the sequential one)."""
+fused kernels (cf_set_option fused_variant: the sequential one and the
+software-pipelined one)."""
 import numpy as np
 import pytest
 
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 _FV = [0]
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["fused-pipe", "fused-seq"])
+@pytest.fixture(autouse=True, params=[0, 1], ids=["fused-seq", "fused-pipe"])
 def fused_variant(request):
     _FV[0] = request.param
     yield request.param
