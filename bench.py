@@ -517,7 +517,10 @@ def main():
     # of step s+1 ("grad_prep"); otherwise (pipeline 1, the default) the
     # gradient launch is "step" and the draw rides in the apply launch
     dom = "grad_prep" if (args.pipeline == 2 and not sharded) else "step"
-    eng.set_option("profile_mask", 1 << KERNELS[dom])
+    # the split GBPR exchange step runs its gradient in two launches (pairs
+    # with local group members, then the rest): both are timed, summed per step
+    split_grad = sharded and cfg["model"] == "gbpr"
+    eng.set_option("profile_mask", (1 << KERNELS[dom]) | ((1 << KERNELS["step_remote"]) if split_grad else 0))
     # every PROFILE_EVERY-th launch is timed: an event pair on every launch
     # costs the loop ~6 us/step (cfg2), sampled launches ~1/PROFILE_EVERY of it
     eng.set_option("profile_every", PROFILE_EVERY)
@@ -534,6 +537,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms, step_n = eng.profile_read(dom)
+    if split_grad:
+        rem_ms, _ = eng.profile_read("step_remote")
+        step_ms += rem_ms
 
     # per-kernel breakdown: a separate, untimed pass with every launch timed
     kernels = {}
@@ -545,8 +551,8 @@ def main():
         run(nb)
         sync()
         eng.profile(False)
-        for kname in ("sample", "slot", "step", "grad_prep", "apply", "apply_prep", "apply_slot", "item_reduce",
-                      "apply_dense", "clip", "psort"):
+        for kname in ("sample", "slot", "step", "step_remote", "grad_prep", "apply", "apply_prep", "apply_slot",
+                      "item_reduce", "apply_dense", "clip", "psort"):
             ms, n = eng.profile_read(kname)
             if n:
                 kernels[kname] = {"launches": n, "avg_us": 1e3 * ms / n, "total_ms": ms}

@@ -18,7 +18,7 @@ MODEL_IDS = {"bpr": CF_BPR, "bprmf": CF_BPR, "gbpr": CF_GBPR, "gbprmf": CF_GBPR,
 TABLES = {"user": 0, "item": 1, "bias": 2, "acc_user": 3, "acc_item": 4, "acc_bias": 5}
 KERNELS = {"sample": 0, "step": 1, "apply": 2, "apply_dense": 3, "clip": 4, "score": 5,
            "topk": 6, "slot": 7, "apply_prep": 8, "grad_prep": 9, "apply_slot": 10,
-           "item_reduce": 11, "psort": 12}
+           "item_reduce": 11, "psort": 12, "step_remote": 13}
 STATUS = {0: "CF_OK", -1: "CF_EINVAL", -2: "CF_EHIP", -3: "CF_ESTATE", -4: "CF_ENOMEM", -5: "CF_EAGAIN"}
 CF_EAGAIN = -5
 
@@ -107,6 +107,8 @@ SIGNATURES = {
     "cf_step_path": (ctypes.c_int, [_P, _I32, _PI32]),
     "cf_xchg_serve": (ctypes.c_int, [_P, _I64]),
     "cf_xchg_grad": (ctypes.c_int, [_P]),
+    "cf_xchg_grad_part": (ctypes.c_int, [_P, _I32]),
+    "cf_xchg_finish_items": (ctypes.c_int, [_P]),
     "cf_xchg_finish": (ctypes.c_int, [_P, _I64]),
     "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
     "cf_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, _I64]),

@@ -164,6 +164,8 @@ struct cf_engine {
     float *x_rows = nullptr, *x_grads = nullptr, *x_serve_rows = nullptr, *x_serve_grads = nullptr;
     int64_t x_send_cap = 0, x_recv_cap = 0;
     int x_stage = 0;                 // 0 idle, 1 begun, 2 served, 3 grads done
+    int x_part = 0;                  // split step: gradient parts done (1: local-member pairs)
+    bool x_items_done = false;       // split step: the items' apply ran (cf_xchg_finish_items)
     // the next exchange batch drawn ahead (cf_xchg_draw), taken by cf_xchg_adopt;
     // send_ids holds two halves of send_cap ids, one per buffer set
     bool x_pend = false;
@@ -1873,6 +1875,8 @@ int cf_xchg_begin(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* 
     e->x_set = k;
     e->x_B = B;
     e->x_stage = 1;
+    e->x_part = 0;
+    e->x_items_done = false;
     return CF_OK;
 }
 
@@ -1918,6 +1922,8 @@ int cf_xchg_adopt(cf_engine* e, int32_t B) {
     e->x_B = e->x_pend_B;
     e->x_pend = false;
     e->x_stage = 1;
+    e->x_part = 0;
+    e->x_items_done = false;
     return CF_OK;
 }
 
@@ -1933,6 +1939,7 @@ int cf_xchg_serve(cf_engine* e, int64_t n_recv) {
 
 int cf_xchg_grad(cf_engine* e) {
     CF_TRY(check_xchg(e, 2));
+    if (e->x_part != 0) return fail(CF_ESTATE, "a split gradient (cf_xchg_grad_part) is in progress");
     const StepArgs& a = e->x_args;
     {
         ProfScope ps(e, CF_K_STEP);
@@ -1941,6 +1948,49 @@ int cf_xchg_grad(cf_engine* e) {
     e->last_occV = a.occV;
     e->last_nV = (int64_t)e->x_B * items_per_pair(e->cfg);
     e->x_stage = 3;
+    return CF_OK;
+}
+
+// split step: pairs whose group members are all local (part 1, beside the
+// member-row all-to-all), then the others (part 2, after it); each part
+// writes its own half of the loss partials
+int cf_xchg_grad_part(cf_engine* e, int32_t part) {
+    if (part == 0) return cf_xchg_grad(e);
+    CF_TRY(check_xchg(e, 2));
+    if (part != 1 && part != 2) return fail(CF_EINVAL, "part must be 0, 1 or 2");
+    if (part != e->x_part + 1) return fail(CF_ESTATE, "gradient parts run in order: 1 (local members), then 2");
+    StepArgs a = e->x_args;
+    a.member_pass = part;
+    if (part == 2) a.loss_partial = e->loss_partial + grad_blocks(e->x_args);
+    {
+        ProfScope ps(e, part == 1 ? CF_K_STEP : CF_K_STEP_REMOTE);
+        CF_HIP(launch_grad(a, e->stream));
+    }
+    e->x_part = part;
+    if (part == 2) {
+        e->last_occV = a.occV;
+        e->last_nV = (int64_t)e->x_B * items_per_pair(e->cfg);
+        e->x_stage = 3;
+    }
+    return CF_OK;
+}
+
+// loss partials of this exchange step's gradient launch(es)
+static int xchg_partials(cf_engine* e) { return grad_blocks(e->x_args) * (e->x_part == 2 ? 2 : 1); }
+
+// split step: the item rows' summed gradient into the bound buffer (the item
+// exchange can start), before the served gradients arrive for the users
+int cf_xchg_finish_items(cf_engine* e) {
+    CF_TRY(check_xchg(e, 3));
+    if (e->x_items_done) return fail(CF_ESTATE, "the items of this exchange step are already finished");
+    ApplyArgs p = apply_args(e, e->x_args, e->x_B, e->x_set, nullptr);   // the users' apply folds the loss
+    p.count_users = 0;
+    p.n_partial = xchg_partials(e);
+    if (p.count_items) {
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    e->x_items_done = true;
     return CF_OK;
 }
 
@@ -1953,11 +2003,15 @@ int cf_xchg_finish(cf_engine* e, int64_t n_recv) {
     p.served_ids = e->x_recv_ids;   // served rows with no local occurrence apply here
     p.served_own = e->x_own;
     p.nS = n_recv;
+    p.n_partial = xchg_partials(e);
+    if (e->x_items_done) p.count_items = 0;
     {
         ProfScope ps(e, CF_K_APPLY);
         CF_HIP(launch_apply(p, e->stream));
     }
     e->x_stage = 0;
+    e->x_part = 0;
+    e->x_items_done = false;
     return CF_OK;
 }
 

@@ -295,7 +295,7 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 }
 
 #ifndef CF_FUSED_BPREFETCH
-#define CF_FUSED_BPREFETCH 1   // read each MFMA group's B operand one group ahead
+#define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
 template <int MODEL>
 __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) {
@@ -755,9 +755,9 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
             if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
         };
         if (Dh == kAH) {
-            // one previous-tile row test per group of four MFMAs (16 and 16);
-            // the next group's B operand is read before this group's MFMAs
-            float4 bc = bop(0);
+            // one previous-tile row test per group of four MFMAs (16 and 16)
+#if CF_FUSED_BPREFETCH
+            float4 bc = bop(0);   // the next group's B operand read ahead
 #pragma unroll
             for (int t0 = 0; t0 < kAH; t0 += 4) {
                 const float4 bn4 = bop(t0 + 4 < kAH ? t0 + 4 : t0);
@@ -765,6 +765,13 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
                 pass |= pass_of(t0 >> 2);
                 bc = bn4;
             }
+#else
+#pragma unroll
+            for (int t0 = 0; t0 < kAH; t0 += 4) {
+                mfma4(t0, bop(t0));
+                pass |= pass_of(t0 >> 2);
+            }
+#endif
         } else {
 #pragma unroll
             for (int t0 = 0; t0 < kAH; t0 += 4)

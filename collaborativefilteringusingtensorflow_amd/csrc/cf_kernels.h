@@ -132,6 +132,10 @@ struct StepArgs {
     int64_t shard_u0, shard_u1;
     const float* __restrict__ xrows;  // [sent, d] rows of other ranks' group users
     float* __restrict__ xgrads;       // [sent, d] their gradient rows
+    // split exchange step (cf_xchg_grad_part): 1 = only the pairs whose group
+    // members are all this rank's users (runs while the member rows are in
+    // flight), 2 = only the others; 0 = every pair
+    int member_pass;
     // tuple ranking (PLR): occV holds the tuple's items, W = width - 2
     int plr_kind;                     // 0 PRIGP, 1 CPLR
     float alpha, beta, gamma;

@@ -932,6 +932,11 @@ __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
     for (int k = 0; k < kPairsPerGroup; ++k) {
         const int p = (block * kPairsPerGroup + k) * kGroupsPerBlock + grp;
         if (p >= B) break;  // group-uniform
+        if (MODEL == GBPR && a.member_pass != 0) {   // split exchange step (group-uniform)
+            bool local = true;
+            for (int k2 = 0; k2 < G; ++k2) local &= a.occU[B + p * G + k2] >= 0;
+            if (local != (a.member_pass == 1)) continue;
+        }
         const int u = a.occU[p];
         const int i = a.occV[p];
         const int ru = a.count_users ? a.rankU[p] : 0;
@@ -1670,6 +1675,17 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
             else
                 pr[k].load_idx(a, pp[k]);
         }
+    if constexpr (MODEL == GBPR) {   // split exchange step: this pass's pairs only (group-uniform)
+        if (a.member_pass != 0) {
+#pragma unroll
+            for (int k = 0; k < P; ++k) {
+                bool local = true;
+#pragma unroll
+                for (int m = 0; m < PairRows<MODEL, EPL, WT>::NG; ++m) local &= pr[k].g[m] >= 0;
+                if (local != (a.member_pass == 1)) ok[k] = false;
+            }
+        }
+    }
 #pragma unroll
     for (int k = 0; k < P; ++k)
         if (ok[k]) pr[k].template load_rows<SORT>(a, gl);

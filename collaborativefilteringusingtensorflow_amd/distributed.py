@@ -307,14 +307,18 @@ def item_users(indptr, indices, n_items):
     return np.cumsum(tp), users[order].astype(np.int32)
 
 
-def _a2a(dist, out, inp, out_splits, in_splits, group):
-    """all_to_all_single along dim 0; gloo gets host copies of device tensors."""
+def _a2a(dist, out, inp, out_splits, in_splits, group, async_op=False):
+    """all_to_all_single along dim 0; gloo gets host copies of device tensors
+    (synchronously).  With ``async_op`` on RCCL the work handle is returned
+    (the collective runs beside later launches on the stream until waited);
+    otherwise None once complete."""
     if out.is_cuda and dist.get_backend(group) == "gloo":
         o = out.cpu()
         dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
         out.copy_(o)
-    else:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        return None
+    w = dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=async_op)
+    return w if async_op else None
 
 
 class GroupExchangeStep(object):
@@ -333,9 +337,10 @@ class GroupExchangeStep(object):
     on that copy's event, long complete, for the split sizes of its
     all-to-alls."""
 
-    def __init__(self, backend, items, world, process_group=None, pipelined=True):
+    def __init__(self, backend, items, world, process_group=None, pipelined=True, split=True):
         import torch
         import torch.distributed as dist
+        self.split = split
         self.backend = backend
         self.items = _items(items, process_group)
         self.item_grad = self.items.grad
@@ -400,14 +405,38 @@ class GroupExchangeStep(object):
         cap = getattr(be, "send_cap", 0)
         _a2a(dist, be.recv_ids[:nr], be.send_ids[h * cap:h * cap + ns], rc, sc, self.group)
         be.xchg_serve(nr)
-        _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group)
-        be.xchg_grad()
-        _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group)
-        be.xchg_finish(nr)
         x = self.items
-        x.reduce(dist, False)
+        if not (self.split and hasattr(be, "xchg_grad_part")):
+            _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group)
+            be.xchg_grad()
+            _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group)
+            be.xchg_finish(nr)
+            x.reduce(dist, False)
+            x.apply(be)
+            x.gather(dist, False)
+            return
+        # split step: the pairs whose members are all local run while the
+        # member rows are in flight, the items' sums start the item exchange
+        # while the member gradients are in flight; the user update waits for
+        # them (exact sum-before-update, gbprmf.py:101-106)
+        overlap = x.overlap(dist)
+        w = _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group, async_op=overlap)
+        be.xchg_grad_part(1)
+        if w is not None:
+            w.wait()
+        be.xchg_grad_part(2)
+        w = _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group, async_op=overlap)
+        be.xchg_finish_items()
+        work = x.reduce(dist, overlap)
+        if w is not None:
+            w.wait()
+        be.xchg_finish(nr)
+        if overlap and work is not None:
+            work.wait()
         x.apply(be)
-        x.gather(dist, False)
+        work = x.gather(dist, overlap)
+        if overlap and work is not None:
+            work.wait()
 
     def sync_state(self):
         self.items.sync_state(self._dist)
@@ -461,6 +490,12 @@ class EngineExchange(object):
 
     def xchg_grad(self):
         self.e.xchg_grad()
+
+    def xchg_grad_part(self, part):
+        self.e.xchg_grad_part(part)
+
+    def xchg_finish_items(self):
+        self.e.xchg_finish_items()
 
     def xchg_finish(self, n):
         self.e.xchg_finish(n)

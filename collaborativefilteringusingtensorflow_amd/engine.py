@@ -358,6 +358,12 @@ class Engine(object):
     def xchg_grad(self):
         N.check(self._L.cf_xchg_grad(self._h), "cf_xchg_grad")
 
+    def xchg_grad_part(self, part):
+        N.check(self._L.cf_xchg_grad_part(self._h, int(part)), "cf_xchg_grad_part")
+
+    def xchg_finish_items(self):
+        N.check(self._L.cf_xchg_finish_items(self._h), "cf_xchg_finish_items")
+
     def xchg_finish(self, n_recv):
         N.check(self._L.cf_xchg_finish(self._h, int(n_recv)), "cf_xchg_finish")
 

@@ -93,7 +93,9 @@ enum cf_kernel_id {
                             into the bound buffer, before the all-reduce    */
     CF_K_PSORT = 12,     /* pos_sort: scan of the positive counts + scatter of
                             the pairs into positive-item order               */
-    CF_K_COUNT = 13
+    CF_K_STEP_REMOTE = 13,/* split exchange step: the gradient of the pairs with
+                            a remote group member (cf_xchg_grad_part 2)      */
+    CF_K_COUNT = 14
 };
 
 /*
@@ -317,7 +319,18 @@ int cf_bind_table(cf_engine* eng, int32_t table, void* device_ptr, int64_t n_ele
  * 2 * send_cap ids: cf_xchg_begin packs into half 0, cf_xchg_draw into the
  * half it returns.
  * A drawn-ahead batch is dropped (sampler rewound) by any other stepping or
- * sampling call. */
+ * sampling call.
+ * Split form (overlaps the exchanges with compute; same results):
+ *   cf_xchg_serve, then the rows all-to-all issued ASYNCHRONOUSLY, and
+ *   cf_xchg_grad_part(1)  the pairs whose group members are all local (no
+ *                         received row needed) while the rows are in flight
+ *   wait for the rows; cf_xchg_grad_part(2)  the other pairs
+ *   the grads all-to-all issued asynchronously, and
+ *   cf_xchg_finish_items  the item rows' summed gradient into the bound item
+ *                         buffer: the item exchange may start now
+ *   wait for the grads; cf_xchg_finish  as above, users only.
+ * cf_xchg_grad_part(0) = cf_xchg_grad.  Replaces nothing in the reference
+ * (no multi-GPU there); keeps gbprmf.py:101-106's sum-before-update. */
 int cf_set_shard(cf_engine* eng, int32_t world, int32_t rank, const int64_t* user_bounds /*[world+1]*/);
 /* global item -> user CSR (sampler_gbpr.py:15), user ids global */
 int cf_set_group_source(cf_engine* eng, const int64_t* indptr_t, const int32_t* indices_t, int64_t nnz);
@@ -329,6 +342,8 @@ int cf_xchg_draw(cf_engine* eng, int32_t B, void* send_counts_dev, int32_t* half
 int cf_xchg_adopt(cf_engine* eng, int32_t B);
 int cf_xchg_serve(cf_engine* eng, int64_t n_recv);
 int cf_xchg_grad(cf_engine* eng);
+int cf_xchg_grad_part(cf_engine* eng, int32_t part);
+int cf_xchg_finish_items(cf_engine* eng);
 int cf_xchg_finish(cf_engine* eng, int64_t n_recv);
 
 /* Which kernels a step of B pairs takes with the current options (bench

@@ -32,7 +32,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce",
-            pipelined=True):
+            pipelined=True, split=True):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -56,6 +56,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     step, _items = make_gpu_group_exchange(e, world, rank, bounds, ip, ix, 1682, d, 100,
                                            torch.device("cuda", 0), exchange=exchange)
     step.pipelined = step.pipelined and pipelined
+    step.split = split
     drawn = []
     if sampled == "steps":           # device-sampled steps only (pipelined count exchange)
         for _ in range(7):
@@ -79,7 +80,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     step.sync_state()
     torch.cuda.synchronize()
     q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("bias"),
-           e.get_table("acc_user"), drawn, e.get_table("acc_item"), e.get_table("acc_bias")))
+           e.get_table("acc_user"), drawn, e.get_table("acc_item"), e.get_table("acc_bias"), e.take_loss()))
     e.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -88,12 +89,12 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
 SIZES = (64, 64, 48, 48, 64, 32, 32, 64)
 
 
-def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True):
+def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True, split=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange,
-                                               pipelined))
+                                               pipelined, split))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -104,9 +105,13 @@ def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipeli
     return res
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split", "serial"])
 @pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
 @pytest.mark.parametrize("stream", ["gbpr_b100_g1_w5", "gbpr_b100_g3_w2"])
-def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exchange):
+def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exchange, split):
+    """split: the split exchange step (cf_xchg_grad_part 1 / 2, cf_xchg_finish_items);
+    serial: cf_xchg_grad + cf_xchg_finish.  The ranks' losses sum to the
+    global step's (each part writes its own half of the loss partials)."""
     from oracle import cf_oracle as O
     rng = np.random.RandomState(12)
     d = 16
@@ -115,12 +120,15 @@ def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exch
     b0 = O.init_table(rng, (1682,))
     batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
                 streams[stream + "/groups"][s]) for s in range(8)]
-    res = _run(fold1, batches, U0, V0, b0, exchange=exchange)
+    res = _run(fold1, batches, U0, V0, b0, exchange=exchange, split=split)
     U, V, b = U0.astype(np.float64), V0.astype(np.float64), b0.astype(np.float64)
     AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
+    lo = 0.0
     for pairs, negs, groups in batches:
-        O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
-    for rank, u0, u1, Ul, Vr, br, AUl, _, AVr, Abr in res:
+        lo += O.gbpr_step(U, V, b, AU, AV, Ab, pairs, negs, groups, 0.4, 0.01)
+    lg = sum(r[10] for r in res)
+    assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
+    for rank, u0, u1, Ul, Vr, br, AUl, _, AVr, Abr, _ in res:
         assert_close(Ul, U[u0:u1], ("user", rank))
         assert_close(AUl, AU[u0:u1], ("acc_user", rank))
         assert_close(Vr, V, ("item", rank))
@@ -141,7 +149,7 @@ def test_two_rank_device_sampled_groups_span_shards(fold1):
     res = _run(fold1, dummy, U0, V0, b0, sampled=True)
     ip, ix = fold1["train_indptr"], fold1["train_indices"]
     cross = 0
-    for rank, u0, u1, Ul, Vr, br, AUl, drawn, _, _ in res:
+    for rank, u0, u1, Ul, Vr, br, AUl, drawn, _, _, _ in res:
         assert np.all(np.isfinite(Ul)) and np.all(np.isfinite(Vr))
         for pairs, groups in drawn:
             for (u, i), g in zip(pairs, groups):

@@ -3,9 +3,10 @@
 
 GBPR draws group members from every user of the item (sampler_gbpr.py:15,41),
 so with users sharded a member can live on the other rank.  Each rank drives
-the product ``GroupExchangeStep`` (three all-to-alls + the item all-reduce)
-with an oracle-backed stand-in that implements the same protocol as the C ABI
-(cf_xchg_begin / serve / grad / finish, include/cf_engine.h).  After K steps
+the product ``GroupExchangeStep`` (three all-to-alls + the item all-reduce,
+serial or in the split form) with an oracle-backed stand-in that implements
+the same protocol as the C ABI (cf_xchg_begin / serve / grad / grad_part /
+finish_items / finish, include/cf_engine.h).  After K steps
 every rank's user shard, the replicated item table and bias must equal the
 oracle run on the concatenated global batches.
 """
@@ -64,13 +65,31 @@ class OracleGroupShard(object):
         self.serve_rows[:n] = torch.as_tensor(self.U[ids])
 
     def xchg_grad(self):
+        self.pending = (np.zeros(0, np.int64), np.zeros((0, self.d)))
+        self._grad(np.ones(self.pairs.shape[0], bool))
+
+    # split step (cf_xchg_grad_part): 1 = pairs whose members are all local,
+    # 2 = the others; cf_xchg_finish_items has nothing to do here (the item
+    # gradient is complete after the gradient parts)
+    def xchg_grad_part(self, part):
+        local = np.all((self.slot < 0).reshape(self.groups.shape), axis=1)
+        if part == 1:
+            self.pending = (np.zeros(0, np.int64), np.zeros((0, self.d)))
+        self.parts_run = getattr(self, "parts_run", 0) + 1
+        self._grad(local if part == 1 else ~local)
+
+    def xchg_finish_items(self):
+        pass
+
+    def _grad(self, sel):
         rho, reg, d = self.rho, self.reg, self.d
-        pairs, negs, groups = self.pairs, self.negs, self.groups
+        pairs, negs, groups = self.pairs[sel], self.negs[sel], self.groups[sel]
+        slot = self.slot.reshape(self.groups.shape)[sel].reshape(-1)
         Bn, G = groups.shape
         u_idx, i_idx = pairs[:, 0], pairs[:, 1]
         flat = groups.reshape(-1)
-        Ug = np.where((self.slot >= 0)[:, None],
-                      self.rows.numpy()[np.maximum(self.slot, 0)],
+        Ug = np.where((slot >= 0)[:, None],
+                      self.rows.numpy()[np.maximum(slot, 0)],
                       self.U[np.clip(flat - self.u0, 0, self.U.shape[0] - 1)]).reshape(Bn, G, d)
         Uu, Vi, Vj = self.U[u_idx], self.V[i_idx], self.V[negs]
         bi, bj = self.b[i_idx], self.b[negs]
@@ -82,10 +101,12 @@ class OracleGroupShard(object):
         gUg = ((rho / G) * s[:, None, None] * Vi[:, None, :] + reg * Ug).reshape(-1, d)
         gVi = s[:, None] * ((rho / G) * Ug.sum(axis=1) + (1 - rho) * Uu) + reg * Vi
         gVj = -c[:, :, None] * Uu[:, None, :]
-        loc = self.slot < 0
-        self.pending = (np.concatenate([u_idx, flat[loc] - self.u0]),
-                        np.concatenate([gUu, gUg[loc]]))
-        self.grads[:] = torch.as_tensor(gUg[~loc][np.argsort(self.slot[~loc])])
+        loc = slot < 0
+        rows, grads = self.pending
+        self.pending = (np.concatenate([rows, u_idx, flat[loc] - self.u0]),
+                        np.concatenate([grads, gUu, gUg[loc]]))
+        if (~loc).any():
+            self.grads[torch.as_tensor(slot[~loc])] = torch.as_tensor(gUg[~loc])
         GV, Gb = self._gv(), self._gb()
         np.add.at(GV, np.concatenate([i_idx, negs.reshape(-1)]),
                   np.concatenate([gVi, gVj.reshape(-1, d)]))
@@ -162,7 +183,7 @@ class RSOracleGroupShard(OracleGroupShard):
         self.b[r0 + rb] -= self.lr * Gb[rb] / np.sqrt(self.Ab[r0 + rb])
 
 
-def _worker(rank, world, port, fold, batches, U0, V0, b0, q, exchange="allreduce"):
+def _worker(rank, world, port, fold, batches, U0, V0, b0, q, exchange="allreduce", split=True):
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
     from collaborativefilteringusingtensorflow_amd.distributed import (GroupExchangeStep,
@@ -179,10 +200,10 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, exchange="allreduce
                                    [(be.Vfull, d), (be.bfull, 1)], ch, rank, grad_bias=be.bias_grad,
                                    bias_slice=torch.zeros(ch, dtype=torch.float64),
                                    state=[(be.AVfull, d), (be.Abfull, 1)])
-        step = GroupExchangeStep(be, items, world)
+        step = GroupExchangeStep(be, items, world, split=split)
     else:
         be = OracleGroupShard(U0[u0:u1], V0, b0, bounds, rank, rho=0.4, reg=0.01)
-        step = GroupExchangeStep(be, be.item_grad, world)
+        step = GroupExchangeStep(be, be.item_grad, world, split=split)
     n_remote = 0
     for pairs, negs, groups in batches:
         mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
@@ -192,6 +213,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, exchange="allreduce
         n_remote += int(np.sum((g < u0) | (g >= u1)))
         step(pairs=lp, negs=negs[mine], groups=g)
     step.sync_state()
+    assert getattr(be, "parts_run", 0) == (2 * len(batches) if split else 0)
     q.put((rank, u0, u1, be.U, be.V.copy(), be.b.copy(), be.AU, n_remote, be.AV.copy(), be.Ab.copy()))
     dist.barrier()
     dist.destroy_process_group()
@@ -216,11 +238,15 @@ def test_item_users_is_the_transpose(fold1):
         assert sorted(tu[tp[i]:tp[i + 1]].tolist()) == sorted(np.asarray(ru[rp[i]:rp[i + 1]]).tolist())
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split", "serial"])
 @pytest.mark.parametrize("stream,world,exchange", [("gbpr_b100_g1_w5", 2, "allreduce"),
                                                    ("gbpr_b100_g3_w2", 2, "allreduce"),
                                                    ("gbpr_b100_g1_w5", 2, "rs_ag"),
                                                    ("gbpr_b100_g1_w5", 3, "rs_ag")])
-def test_group_exchange_equals_global_step(fold1, streams, stream, world, exchange):
+def test_group_exchange_equals_global_step(fold1, streams, stream, world, exchange, split):
+    """split: GroupExchangeStep's split step (local-member pairs beside the
+    rows all-to-all, the item exchange beside the gradients all-to-all);
+    serial: the three-all-to-all step."""
     from oracle import cf_oracle as O
     rng = np.random.RandomState(9)
     U0 = O.init_table(rng, (943, 8), dtype=np.float64)
@@ -231,7 +257,7 @@ def test_group_exchange_equals_global_step(fold1, streams, stream, world, exchan
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q, exchange))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q, exchange, split))
              for r in range(world)]
     for p in procs:
         p.start()
