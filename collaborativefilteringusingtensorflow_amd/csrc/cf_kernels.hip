@@ -1767,8 +1767,6 @@ __global__ __launch_bounds__(kWave) void grad_fast_wave_kernel(StepArgs a) {
 // 0-31, 32-63) hit different banks (staged rows are 128 dwords apart).
 // Same arithmetic as grad_fast_kernel up to fp32 summation order.
 // ---------------------------------------------------------------------------
-constexpr int kLdsRow = 128;   // floats per staged row
-
 __device__ __forceinline__ int elem_par(int s, int gl, int par) { return ((s ^ par) << 4) | gl; }
 
 // full rows only (d == 16 * EPL): no element masks, straight-line code
@@ -1832,10 +1830,11 @@ __device__ __forceinline__ void pfinish(float* __restrict__ X, float* __restrict
 
 template <int EPL>
 __device__ __forceinline__ void pifinish(const StepArgs& a, int64_t r, int count, int64_t slot, int p,
-                                         float alpha, float beta, int gl, int par, const float (&x0)[EPL],
-                                         const float (&acc0)[EPL], const float (&g)[EPL]) {
+                                         float alpha, float beta, int which, int gl, int par,
+                                         const float (&x0)[EPL], const float (&acc0)[EPL],
+                                         const float (&g)[EPL]) {
     if (a.recV != nullptr && count >= 2 && slot >= 0) {
-        if (gl == 0) a.recV[slot] = make_int4(p, __float_as_int(alpha), __float_as_int(beta), 0);
+        if (gl == 0) a.recV[slot] = make_int4(p, __float_as_int(alpha), __float_as_int(beta), which);
         return;
     }
     pfinish<EPL>(a.V, a.AV, a.GV, a.slotV, a.cntV, r, count, slot, a.d, gl, par, x0, acc0, g, a);
@@ -1865,24 +1864,32 @@ __device__ __forceinline__ void pacc_ld(const float* __restrict__ A, int64_t r, 
 #else
 #define CF_LDS_SCHED_FENCE() ((void)0)
 #endif
-template <int MODEL, int WT>
+// EPL = 8 (d = 128): BPR / AMF / CML, 40 KB of staged rows per block, a
+// negative's accumulator loaded where it is finished (rows seen once are rare
+// at 100K items).  EPL = 4 (d = 64): GBPR at G = 1 (cfg4), 20 KB per block;
+// at 1M items nearly every negative is its row's only occurrence, so the
+// negatives' accumulators are loaded with the rows (GBPR's ACC_EARLY).
+template <int MODEL, int EPL, int WT>
 __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a) {
-    constexpr int EPL = 8;
+    constexpr int ROW = kGL * EPL;            // floats per staged row (full rows only)
+    constexpr int RPI = kWave * 4 / ROW;      // rows per LDS-DMA wave-instruction (16 B per lane)
+    constexpr int LPR = kWave / RPI;          // lanes per row
     constexpr int RPW = (kWave / kGL) * WT;   // staged rows per wave
-    static_assert(RPW % 2 == 0, "two rows per LDS-DMA wave-instruction");
-    static_assert(MODEL == BPR || MODEL == AMF || MODEL == CML, "no group users / tuples here");
-    // exactly 40 KB, so four blocks fit a CU (the loss partials reuse it)
-    __shared__ float s_v[kGroupsPerBlock * WT * kLdsRow];
+    constexpr bool ACC_EARLY = MODEL == GBPR;
+    static_assert(RPW % RPI == 0, "whole rows per LDS-DMA wave-instruction");
+    static_assert(MODEL == BPR || MODEL == AMF || MODEL == CML || MODEL == GBPR, "no tuples here");
+    // 40 KB (d = 128) / 20 KB (d = 64) per block; the loss partials reuse it
+    __shared__ float s_v[kGroupsPerBlock * WT * ROW];
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
     const int par = grp & 1;
     const int d = a.d;
     const int p = blockIdx.x * kGroupsPerBlock + grp;
-    const bool ok = p < a.B;
+    bool ok = p < a.B;
 
     // ids (every lane of the group loads the same words)
-    int u = 0, i = 0, ru = 0, ri = 0;
+    int u = 0, i = 0, ru = 0, ri = 0, g = 0, rg = 0;
     int j[WT], rj[WT];
 #pragma unroll
     for (int w = 0; w < WT; ++w) {
@@ -1899,34 +1906,49 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
             j[w] = a.occV[a.B + p * WT + w];
             rj[w] = a.count_items ? a.rankV[a.B + p * WT + w] : 0;
         }
+        if (MODEL == GBPR) {   // G = 1: the group member (-1 - k: row k of xrows, another rank's user)
+            g = a.occU[a.B + p];
+            rg = a.count_users ? a.rankU[a.B + p] : 0;
+            // split exchange step: only this pass's pairs (group-uniform)
+            if (a.member_pass != 0 && (g >= 0) != (a.member_pass == 1)) ok = false;
+        }
     }
-    // stage the negatives: wave-instruction k moves the wave's rows 2k (lanes
-    // 0-31) and 2k + 1 (lanes 32-63), 16 B per lane; row r is negative r % WT
-    // of the wave's pair r / WT, whose id lane (r / WT) * 16 + r % WT holds
+    if (!ok) {
+#pragma unroll
+        for (int w = 0; w < WT; ++w) j[w] = -1;   // nothing staged for this group
+    }
+    // stage the negatives: wave-instruction k moves the wave's rows
+    // RPI*k .. RPI*k + RPI - 1 (LPR lanes each, 16 B per lane); row r is
+    // negative r % WT of the wave's pair r / WT, whose id lane (r / WT) * 16 +
+    // r % WT holds
     {
         int jsel = -1;
 #pragma unroll
         for (int w = 0; w < WT; ++w)
             if (gl == w) jsel = j[w];
-        float* wbase = s_v + (threadIdx.x >> 6) * RPW * kLdsRow;
-        const int c4 = (lane & 31) * 4;
+        float* wbase = s_v + (threadIdx.x >> 6) * RPW * ROW;
+        const int c4 = (lane % LPR) * 4;
 #pragma unroll
-        for (int k = 0; k < RPW / 2; ++k) {
-            const int r = 2 * k + (lane >> 5);
+        for (int k = 0; k < RPW / RPI; ++k) {
+            const int r = RPI * k + lane / LPR;
             const int q = r / WT;
             const int jj = __shfl(jsel, q * kGL + (r - q * WT), kWave);
             if (jj >= 0)
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(a.V + (int64_t)jj * d + c4),
-                    (__attribute__((address_space(3))) void*)(wbase + 2 * k * kLdsRow), 16, 0, 0);
+                    (__attribute__((address_space(3))) void*)(wbase + RPI * k * ROW), 16, 0, 0);
         }
     }
     // counts and the u / i rows, then slots and the accumulator rows of the
     // rows this batch touches once
-    int cu = 0, ci = 0, cj[WT];
-    float uu[EPL], vi[EPL];
+    int cu = 0, ci = 0, cg = 0, cj[WT];
+    float uu[EPL], vi[EPL], ug[MODEL == GBPR ? EPL : 1];
+    float bi = 0.f, bj[WT];   // GBPR item biases
 #pragma unroll
-    for (int w = 0; w < WT; ++w) cj[w] = 0;
+    for (int w = 0; w < WT; ++w) {
+        cj[w] = 0;
+        bj[w] = 0.f;
+    }
     if (ok) {
         cu = a.count_users ? a.cntU[u] : 0;
         ci = a.count_items ? a.cntV[i] : 0;
@@ -1934,10 +1956,20 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
         for (int w = 0; w < WT; ++w) cj[w] = a.count_items ? a.cntV[j[w]] : 0;
         prow_ld<EPL>(a.U + (int64_t)u * d, gl, par, uu);
         prow_ld<EPL>(a.V + (int64_t)i * d, gl, par, vi);
+        if constexpr (MODEL == GBPR) {
+            cg = (a.count_users && g >= 0) ? a.cntU[g] : 0;
+            prow_ld<EPL>(g >= 0 ? a.U + (int64_t)g * d : a.xrows + (int64_t)(-1 - g) * d, gl, par, ug);
+            bi = a.b[i];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) bj[w] = a.b[j[w]];
+        }
     }
-    int64_t su = -1, si = -1, sj[WT];
-    float au[EPL], ai[EPL];
+    int64_t su = -1, si = -1, sg = -1, sj[WT];
+    float au[EPL], ai[EPL], ag[MODEL == GBPR ? EPL : 1], aje[ACC_EARLY ? WT : 1][EPL];
+    float abi = 0.f, abj[WT];   // GBPR: bias accumulators of rows seen once
     const bool item_acc = !a.items_grad_only;
+#pragma unroll
+    for (int w = 0; w < WT; ++w) abj[w] = 0.f;
     if (ok) {
         su = slot_of(cu, u, ru, a.capU, 0, a.offU);
         si = slot_of(ci, i, ri, a.capV, a.repV, a.offV);
@@ -1945,6 +1977,17 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
         for (int w = 0; w < WT; ++w) sj[w] = slot_of(cj[w], j[w], rj[w], a.capV, a.repV, a.offV);
         pacc_ld<EPL>(a.AU, u, d, gl, par, cu == 1, au);
         pacc_ld<EPL>(a.AV, i, d, gl, par, item_acc && ci == 1, ai);
+        if constexpr (MODEL == GBPR) {
+            sg = slot_of(cg, g, rg, a.capU, 0, a.offU);
+            pacc_ld<EPL>(a.AU, g, d, gl, par, g >= 0 && cg == 1, ag);
+            abi = (item_acc && ci == 1) ? a.Ab[i] : 0.f;
+#pragma unroll
+            for (int w = 0; w < WT; ++w) abj[w] = (item_acc && cj[w] == 1) ? a.Ab[j[w]] : 0.f;
+        }
+        if constexpr (ACC_EARLY) {
+#pragma unroll
+            for (int w = 0; w < WT; ++w) pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aje[w]);
+        }
     }
     // the staged rows have landed (an LDS-DMA retires on vmcnt).  The
     // builtin, not inline asm: the compiler's wait tracking sees it and stops
@@ -1953,9 +1996,9 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
 
     float loss_g = 0.f, sq = 0.f;
     if (ok) {
-        const float* sv = s_v + grp * WT * kLdsRow;
+        const float* sv = s_v + grp * WT * ROW;
         if (a.recV != nullptr) {   // item records' X: only pairs that leave one
-            bool need = ci >= 2 && si >= 0;
+            bool need = MODEL != GBPR && ci >= 2 && si >= 0;
 #pragma unroll
             for (int w = 0; w < WT; ++w) need |= cj[w] >= 2 && sj[w] >= 0;
             if (need) prow_st<EPL>(a.stashU + (int64_t)p * d, gl, par, uu);
@@ -1973,7 +2016,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 float vj[EPL];
-                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+                prow_ld<EPL>(sv + w * ROW, gl, par, vj);
                 const float x = ui - gdot<EPL>(uu, vj);
                 float c = -rcp_1p(expf(x));
                 if (MODEL == AMF) {
@@ -2003,18 +2046,18 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
                 sq = fmaf(vi[s], vi[s], sq);
             }
             pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, par, uu, au, gu, a);
-            pifinish<EPL>(a, i, ci, si, p, sc, a.reg, gl, par, vi, ai, gi);
+            pifinish<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, par, vi, ai, gi);
 #pragma unroll
             for (int w = 0; w < WT; ++w) {
                 CF_LDS_SCHED_FENCE();
                 float vj[EPL], aj[EPL], gj[EPL];
                 pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aj);
-                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+                prow_ld<EPL>(sv + w * ROW, gl, par, vj);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) gj[s] = -cw[w] * uu[s] + a.reg * vj[s];
-                pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], a.reg, gl, par, vj, aj, gj);
+                pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], a.reg, 0, gl, par, vj, aj, gj);
             }
-        } else {  // CML
+        } else if (MODEL == CML) {
             float du[EPL];
 #pragma unroll
             for (int s = 0; s < EPL; ++s) du[s] = uu[s] - vi[s];
@@ -2026,7 +2069,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
             for (int w = 0; w < WT; ++w) {
                 CF_LDS_SCHED_FENCE();
                 float t[EPL];
-                prow_ld<EPL>(sv + w * kLdsRow, gl, par, t);
+                prow_ld<EPL>(sv + w * ROW, gl, par, t);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) t[s] = uu[s] - t[s];
                 dn[w] = gdot<EPL>(t, t);
@@ -2054,7 +2097,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
                 CF_LDS_SCHED_FENCE();
                 float vj[EPL], gj[EPL], aj[EPL];
                 pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aj);
-                prow_ld<EPL>(sv + w * kLdsRow, gl, par, vj);
+                prow_ld<EPL>(sv + w * ROW, gl, par, vj);
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) {
                     const float dv = uu[s] - vj[s];
@@ -2066,7 +2109,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
                     }
                 }
                 // a touched row with a zero gradient is still clipped (cml.py:128-129)
-                pifinish<EPL>(a, j[w], cj[w], sj[w], p, coef, (l2 ? a.reg_cov : 0.f) - coef, gl, par, vj,
+                pifinish<EPL>(a, j[w], cj[w], sj[w], p, coef, (l2 ? a.reg_cov : 0.f) - coef, 0, gl, par, vj,
                               aj, gj);
             }
             if (l2) {
@@ -2079,7 +2122,57 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
                 }
             }
             pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, par, uu, au, gu, a);
-            pifinish<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), gl, par, vi, ai, gi);
+            pifinish<EPL>(a, i, ci, si, p, -2.f * aa, 2.f * aa + (l2 ? a.reg_cov : 0.f), 0, gl, par, vi, ai, gi);
+        } else if constexpr (MODEL == GBPR) {   // G == 1 (gbprmf.py:58-106)
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) sq = fmaf(ug[s], ug[s], sq);
+            const float ui = a.rho * gdot<EPL>(ug, vi) + (1.f - a.rho) * gdot<EPL>(uu, vi) + bi;
+            float gu[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) gu[s] = 0.f;
+            float sc = 0.f;
+            float cw[WT];
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                float vj[EPL];
+                prow_ld<EPL>(sv + w * ROW, gl, par, vj);
+                const float x = ui - (gdot<EPL>(uu, vj) + bj[w]);
+                const float c = -rcp_1p(expf(x));
+                loss_g += neg_log_sigmoid(x) + 0.5f * a.reg * bj[w] * bj[w];
+                sc += c;
+                cw[w] = c;
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) gu[s] = fmaf(-c, vj[s], gu[s]);
+            }
+            const float rg_ = a.rho;   // rho / G with G == 1
+            float gi[EPL], gg[EPL], bl[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                gu[s] += (1.f - a.rho) * sc * vi[s] + a.reg * uu[s];
+                bl[s] = rg_ * ug[s] + (1.f - a.rho) * uu[s];
+                gi[s] = sc * bl[s] + a.reg * vi[s];
+                gg[s] = rg_ * sc * vi[s] + a.reg * ug[s];
+                sq = fmaf(uu[s], uu[s], sq);
+                sq = fmaf(vi[s], vi[s], sq);
+            }
+            pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, par, uu, au, gu, a);
+            if (g >= 0)
+                pfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, g, cg, sg, d, gl, par, ug, ag, gg, a);
+            else   // another rank's user: its gradient row goes back to the owner
+                prow_st<EPL>(a.xgrads + (int64_t)(-1 - g) * d, gl, par, gg);
+            if (gl == 0) bias_finish_pre(a, i, ci, sc, si, bi, abi);
+            if (a.recV != nullptr && ci >= 2 && si >= 0) prow_st<EPL>(a.stashB + (int64_t)p * d, gl, par, bl);
+            pifinish<EPL>(a, i, ci, si, p, sc, a.reg, 1, gl, par, vi, ai, gi);
+#pragma unroll
+            for (int w = 0; w < WT; ++w) {
+                CF_LDS_SCHED_FENCE();
+                float vj[EPL], gj[EPL];
+                prow_ld<EPL>(sv + w * ROW, gl, par, vj);
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) gj[s] = -cw[w] * uu[s];   // no L2 on V[j] (gbprmf.py:59-64)
+                if (gl == 0) bias_finish_pre(a, j[w], cj[w], -cw[w] + a.reg * bj[w], sj[w], bj[w], abj[w]);
+                pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], 0.f, 0, gl, par, vj, aje[ACC_EARLY ? w : 0], gj);
+            }
         }
     }
 
@@ -2088,7 +2181,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
     const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
     const float sq_g = gsum(sq);
     double* s_loss = reinterpret_cast<double*>(s_v);
-    constexpr int kWaveD = RPW * kLdsRow / 2;   // doubles per wave region
+    constexpr int kWaveD = RPW * ROW / 2;   // doubles per wave region
     if (gl == 0)
         s_loss[(grp >> 2) * kWaveD + (grp & 3)] = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
     __syncthreads();
@@ -2926,12 +3019,18 @@ static int epl_for(int d) {
 #define CF_GRAD_LDS 1   // 0: auto never takes grad_lds_kernel (grad_path 3 still does)
 #endif
 
+#ifndef CF_GRAD_LDS_GBPR
+#define CF_GRAD_LDS_GBPR 1   // 0: auto keeps GBPR (cfg4) on the phased kernel (grad_path 3 still takes it)
+#endif
 // the LDS-staged W = 5 kernel (grad_lds_kernel): grad_path 3, or auto where
-// it applies; its grid is the phased kernel's at one pair per group
+// it applies -- BPR / AMF / CML at d = 128, GBPR (G = 1) at d = 64; one pair
+// per 16-lane group, 16 per block
 static bool lds_path(const StepArgs& a) {
     const bool want = a.grad_path == 3 || (a.grad_path == 0 && CF_GRAD_LDS);
-    return want && a.W == 5 && a.d == kLdsRow && a.srec == nullptr &&
-           (a.model == BPR || a.model == AMF || a.model == CML);
+    if (!want || a.W != 5 || a.srec != nullptr) return false;
+    if (a.model == BPR || a.model == AMF || a.model == CML) return a.d == 128;
+    if (a.model == GBPR) return a.d == 64 && a.G == 1 && (a.grad_path == 3 || CF_GRAD_LDS_GBPR);
+    return false;
 }
 
 // which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
@@ -2957,6 +3056,7 @@ bool grad_lds(const StepArgs& a) { return lds_path(a); }
 #endif
 
 int grad_blocks(const StepArgs& a, bool with_draw) {
+    if (!with_draw && lds_path(a)) return (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
     const int fw = fast_w(a);
     const int B = a.B;
     const int gpb = (CF_GRAD_WAVE_BLOCKS && !with_draw) ? kWave / kGL : kGroupsPerBlock;
@@ -3068,11 +3168,15 @@ static hipError_t launch_grad_plr(const StepArgs& a, hipStream_t s) {
 template <int MODEL>
 static hipError_t launch_grad_m(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     const int e = epl_for(a.d);
-    if constexpr (MODEL == BPR || MODEL == AMF || MODEL == CML) {
-        // a fused draw (pipeline 2) takes the phased kernel: same grid
+    if constexpr (MODEL == BPR || MODEL == AMF || MODEL == CML || MODEL == GBPR) {
+        // a fused draw (pipeline 2) takes the phased kernel (grad_blocks with
+        // the draw counts its grid)
         if (lds_path(a) && prep_blocks(nx) == 0) {
             const dim3 grid((a.B + kGroupsPerBlock - 1) / kGroupsPerBlock), block(kBlock);
-            hipLaunchKernelGGL((grad_lds_kernel<MODEL, 5>), grid, block, 0, s, a);
+            if constexpr (MODEL == GBPR)
+                hipLaunchKernelGGL((grad_lds_kernel<GBPR, 4, 5>), grid, block, 0, s, a);
+            else
+                hipLaunchKernelGGL((grad_lds_kernel<MODEL, 8, 5>), grid, block, 0, s, a);
             return hipGetLastError();
         }
     }

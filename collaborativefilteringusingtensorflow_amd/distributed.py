@@ -406,7 +406,10 @@ class GroupExchangeStep(object):
         _a2a(dist, be.recv_ids[:nr], be.send_ids[h * cap:h * cap + ns], rc, sc, self.group)
         be.xchg_serve(nr)
         x = self.items
-        if not (self.split and hasattr(be, "xchg_grad_part")):
+        # one rank has no remote members to overlap with (the split only adds
+        # a launch and an apply there); a rank with none to fetch (ns == 0)
+        # runs its whole gradient at once beside the rows it serves
+        if not (self.split and self.world > 1 and hasattr(be, "xchg_grad_part")):
             _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group)
             be.xchg_grad()
             _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group)
@@ -421,10 +424,15 @@ class GroupExchangeStep(object):
         # them (exact sum-before-update, gbprmf.py:101-106)
         overlap = x.overlap(dist)
         w = _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group, async_op=overlap)
-        be.xchg_grad_part(1)
-        if w is not None:
-            w.wait()
-        be.xchg_grad_part(2)
+        if ns > 0:
+            be.xchg_grad_part(1)
+            if w is not None:
+                w.wait()
+            be.xchg_grad_part(2)
+        else:
+            be.xchg_grad()
+            if w is not None:
+                w.wait()
         w = _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group, async_op=overlap)
         be.xchg_finish_items()
         work = x.reduce(dist, overlap)

@@ -32,7 +32,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce",
-            pipelined=True, split=True):
+            pipelined=True, split=True, grad_path=0):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -49,6 +49,7 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
     d = U0.shape[1]
     e = Engine("gbpr", u1 - u0, 1682, d, n_neg=W, gsize=G, rho=0.4, reg=0.01,
                dense_item_apply=True, seed=20 + rank)
+    e.set_option("grad_path", grad_path)
     e.set_interactions(lip, lix)
     e.set_table("user", U0[u0:u1])
     e.set_table("item", V0)
@@ -89,12 +90,13 @@ def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="
 SIZES = (64, 64, 48, 48, 64, 32, 32, 64)
 
 
-def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True, split=True):
+def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True, split=True,
+         grad_path=0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange,
-                                               pipelined, split))
+                                               pipelined, split, grad_path))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -112,15 +114,25 @@ def test_two_rank_group_exchange_equals_global_step(fold1, streams, stream, exch
     """split: the split exchange step (cf_xchg_grad_part 1 / 2, cf_xchg_finish_items);
     serial: cf_xchg_grad + cf_xchg_finish.  The ranks' losses sum to the
     global step's (each part writes its own half of the loss partials)."""
+    _two_rank_global_step(fold1, streams, stream, exchange, split, 16, 0)
+
+
+@pytest.mark.parametrize("split", [True, False], ids=["split", "serial"])
+def test_two_rank_group_exchange_lds_kernel(fold1, streams, split):
+    """The same at d = 64 on the LDS-staged GBPR kernel (grad_path 3), whose
+    member pass filter serves the split step."""
+    _two_rank_global_step(fold1, streams, "gbpr_b100_g1_w5", "allreduce", split, 64, 3)
+
+
+def _two_rank_global_step(fold1, streams, stream, exchange, split, d, grad_path):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(12)
-    d = 16
     U0 = O.init_table(rng, (943, d))
     V0 = O.init_table(rng, (1682, d))
     b0 = O.init_table(rng, (1682,))
     batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
                 streams[stream + "/groups"][s]) for s in range(8)]
-    res = _run(fold1, batches, U0, V0, b0, exchange=exchange, split=split)
+    res = _run(fold1, batches, U0, V0, b0, exchange=exchange, split=split, grad_path=grad_path)
     U, V, b = U0.astype(np.float64), V0.astype(np.float64), b0.astype(np.float64)
     AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
     lo = 0.0

@@ -164,3 +164,37 @@ def test_lds_path_reported(fold1):
         flags, path = e.step_path(65536)
         assert path["lds"] == want, (gp, path)
         e.close()
+
+
+@pytest.mark.parametrize("bias_slots", [0, 1], ids=["bias-atomics", "bias-slots"])
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+def test_lds_kernel_gbpr_d64(fold1, streams, item_slots, bias_slots):
+    """GBPR (G = 1) on the LDS-staged kernel at d = 64 (grad_path 3; cfg4's
+    shape): the reference's captured gbpr_b100_g1_w5 stream against the
+    float64 oracle (gbprmf.py:58-106: V[j] without L2, b regularised)."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    st = get_stream(streams, "gbpr_b100_g1_w5")
+    d, rho, reg = 64, 0.4, 0.01
+    rng = np.random.RandomState(5)
+    nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
+    U = O.init_table(rng, (nu, d))
+    V = O.init_table(rng, (ni, d))
+    b = O.init_table(rng, (ni,))
+    e = Engine("gbpr", nu, ni, d, n_neg=5, gsize=1, rho=rho, reg=reg, seed=7)
+    e.set_option("grad_path", 3)
+    e.set_option("item_slots", item_slots)
+    e.set_option("bias_slots", bias_slots)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.set_table("user", U)
+    e.set_table("item", V)
+    e.set_table("bias", b)
+    assert e.step_path(100)[1]["lds"]
+    T = [U.astype(np.float64), V.astype(np.float64), b.astype(np.float64)]
+    T += [np.full_like(T[0], 0.1), np.full_like(T[1], 0.1), np.full_like(T[2], 0.1)]
+    for s in range(30):
+        lg = e.step(st["pairs"][s], st["negs"][s], st["groups"][s])
+        lo = O.gbpr_step(*T, st["pairs"][s], st["negs"][s], st["groups"][s], rho, reg)
+        assert abs(lg - lo) <= RTOL * abs(lo), (s, lg, lo)
+    for name, o in zip(("user", "item", "bias", "acc_user", "acc_item", "acc_bias"), T):
+        assert_close(e.get_table(name), o, name)
+    e.close()
