@@ -319,6 +319,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-ndcg", action="store_true", help="skip the cfg1 NDCG@10 check")
+    ap.add_argument("--dense-apply", type=int, default=int(os.environ.get("CF_DENSE_APPLY", "-1")),
+                    help="cf_set_option dense_apply: 1 item-row apply on the slot / record path (default), 0 owner scan")
     ap.add_argument("--fused-variant", type=int, default=0,
                     help="cf_set_option fused_variant: 0 sequential fused scoring + top-k, 1 software-pipelined")
     ap.add_argument("--score-pass", action="store_true",
@@ -465,6 +467,8 @@ def main():
         eng.set_option("bias_slots", args.bias_slots)
     if args.item_slots >= 0:
         eng.set_option("item_slots", args.item_slots)
+    if args.dense_apply >= 0:
+        eng.set_option("dense_apply", args.dense_apply)
     if args.pos_sort >= 0:
         eng.set_option("pos_sort", args.pos_sort)
     if args.deterministic:

@@ -218,6 +218,7 @@ struct cf_engine {
 
     int topk_path = 0;  // cf_set_option("topk_path")
     int fused_variant = 0;  // cf_set_option("fused_variant")
+    int dense_apply = 1;    // cf_set_option("dense_apply"): item-row apply outside pos_sort
     int grad_path = 0;  // cf_set_option("grad_path")
     int item_reduce = 1;  // cf_set_option("item_reduce"): dense mode counts item rows
     int bias_slots = 0;   // cf_set_option("bias_slots"): duplicated item-bias gradients in slots (1) or atomics (0)
@@ -710,6 +711,13 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         // 1M users / 524K), else find the owners among the occurrences
         p.dense_items = c.n_items <= 2 * (int64_t)B * items_per_pair(c) ? 1 : 0;
         p.dense_users = c.n_users <= 2 * (int64_t)B * users_per_pair(c) ? 1 : 0;
+    } else if (e->dense_apply && !e->det && !a.items_grad_only && a.count_items && c.model != CF_GBPR &&
+             c.model != CF_PLR) {
+        // slot rows / item records: one group per item row when the item table
+        // is not much larger than the batch's item occurrences (cfg3 / cfg5:
+        // 100K items, 393K occurrences); users keep the occurrence owners
+        p.dense_items = c.n_items <= 2 * (int64_t)B * items_per_pair(c) ? 1 : 0;
+        p.dense_users = 0;
     }
     p.n_users = c.n_users;
     if (e->det) {
@@ -2105,6 +2113,11 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (!e || !name) return fail(CF_EINVAL, "null argument");
     CF_TRY(set_dev(e));   // some options (re)allocate device buffers
     const std::string n(name);
+    if (n == "dense_apply") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "dense_apply must be 0 or 1");
+        e->dense_apply = (int)value;
+        return CF_OK;
+    }
     if (n == "fused_variant") {
         if (value < 0 || value > 1) return fail(CF_EINVAL, "fused_variant must be 0 or 1");
         e->fused_variant = (int)value;

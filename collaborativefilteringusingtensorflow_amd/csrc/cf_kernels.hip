@@ -2538,14 +2538,33 @@ __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) 
     }
 }
 
+// the same dense item blocks outside pos_sort (slot rows or item records in
+// per-row slot ranges, round 3): one 16-lane group per item row reads the
+// row's count -- 16 consecutive rows' counts per block, one coalesced read --
+// and applies a duplicated row (apply_row); no owner detection among the
+// batch's item occurrences
+template <int EPL>
+__device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int block) {
+    const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
+    const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
+    if (r >= a.n_items) return;
+    const int c = a.cntV[r];
+    if (c < 2) return;   // untouched, or seen once (applied by the gradient launch)
+    apply_row<EPL>(a, r, false, c, gl);
+}
+
 // grid: [0, nbI) dense item blocks, [nbI, nbI + nbW) wave blocks, then (with
-// DRAW) the draw + count blocks of the next step (other buffer set)
-template <int EPL, bool DRAW>
+// DRAW) the draw + count blocks of the next step (other buffer set).  PS:
+// pos_sort's item rows (offPN), else apply_rows_item_block
+template <int EPL, bool DRAW, bool PS = true>
 __global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
     const int b = blockIdx.x;
     if (b == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
     if (b < nbI) {
-        apply_ps_item_block<EPL>(p, b);
+        if constexpr (PS)
+            apply_ps_item_block<EPL>(p, b);
+        else
+            apply_rows_item_block<EPL>(p, b);
     } else if (b < nbI + nbW) {
         apply_ps_wave<EPL>(p, (int64_t)(b - nbI) * kWavesPerBlock + (threadIdx.x >> 6));
     } else if constexpr (DRAW) {
@@ -3230,7 +3249,9 @@ static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// the pos_sort apply (+ the next step's draw when nx is given)
+// the pos_sort apply (+ the next step's draw when nx is given); PS false: the
+// dense item rows of the slot-row / record path (apply_rows_item_block)
+template <bool PS = true>
 static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
     const int64_t nUw = !p.count_users ? 0 : p.dense_users ? p.n_users : p.nU;
     const int64_t nVw = (p.count_items && !p.dense_items) ? p.nV : 0;
@@ -3243,20 +3264,28 @@ static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStr
     const StepArgs n = nx ? *nx : StepArgs{};
     if (np > 0) {
         switch (epl_for(p.d)) {
-            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, true>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
         }
     } else {
         switch (epl_for(p.d)) {
-            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, false>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
         }
     }
     return hipGetLastError();
+}
+
+// the slot-row / record path's dense item apply applies (the engine sets
+// dense_items only outside pos_sort and deterministic mode, for a table not
+// much larger than the batch's item occurrences)
+static bool dense_rows_apply(const ApplyArgs& a) {
+    return a.cntP == nullptr && a.dense_items && a.count_items && a.nS == 0 && a.hotP == nullptr &&
+           a.offV == nullptr && epl_for(a.d) <= 8;
 }
 
 hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
@@ -3278,6 +3307,7 @@ hipError_t launch_apply(const ApplyArgs& a, hipStream_t s) {
         if (a.hotP != nullptr || a.nS > 0 || epl_for(a.d) > 8) return hipErrorInvalidValue;
         return launch_apply_ps(a, nullptr, s);
     }
+    if (dense_rows_apply(a)) return launch_apply_ps<false>(a, nullptr, s);
     return a.hotP != nullptr ? launch_apply_h<true>(a, s) : launch_apply_h<false>(a, s);
 }
 
@@ -3303,6 +3333,7 @@ hipError_t launch_apply_prep(const ApplyArgs& p, const StepArgs& a, hipStream_t 
                    ? hipErrorInvalidValue : launch_apply_ps(p, &a, s);
     if (p.hotP != nullptr)
         return a.model == GBPR ? launch_apply_prep_m<GBPR, true>(p, a, s) : launch_apply_prep_m<BPR, true>(p, a, s);
+    if (a.model != GBPR && dense_rows_apply(p)) return launch_apply_ps<false>(p, &a, s);   // draw is prep_body<BPR>
     return a.model == GBPR ? launch_apply_prep_m<GBPR, false>(p, a, s) : launch_apply_prep_m<BPR, false>(p, a, s);
 }
 

@@ -198,3 +198,38 @@ def test_lds_kernel_gbpr_d64(fold1, streams, item_slots, bias_slots):
     for name, o in zip(("user", "item", "bias", "acc_user", "acc_item", "acc_bias"), T):
         assert_close(e.get_table(name), o, name)
     e.close()
+
+
+@pytest.mark.parametrize("item_slots", [0, 1], ids=["rows", "records"])
+@pytest.mark.parametrize("model,d", [("bpr", 32), ("amf", 128), ("cml", 128)])
+def test_dense_rows_apply_pipeline(fold1, model, d, item_slots):
+    """The dense item-row apply of the slot-row / record path (dense_apply 1,
+    round 3: one group per item row instead of owners found among the
+    occurrences; it engages when n_items <= 2 B (1 + W): here 1,682 items and
+    B = 512, W = 5) in the device-sampler pipeline, replayed by the oracle on
+    the identical batches; dense_apply 0 (the owner scan) lands on the same
+    oracle.  CML takes 2 steps: at B = 512 its float32 oracle leaves the
+    CML_TRAJ band around the float64 one by 2x after 6 steps (12.5x after
+    12; 0.4-1.0x after 4, batch-dependent) and stays under 0.2 of it after 2
+    (measured on the same kind of batches)."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    B, K = 512, (2 if model == "cml" else 12)
+    hp = HP[model]
+    for dense in (1, 0):
+        def mk():
+            e = Engine(model, int(fold1["n_users"]), int(fold1["n_items"]), d, n_neg=5, seed=7, **hp)
+            e.set_option("item_slots", item_slots)
+            e.set_option("dense_apply", dense)
+            e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+            e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=6)
+            return e
+        dev, rep = mk(), mk()
+        T = {t: dev.get_table(t).astype(np.float64) for t in ("user", "item", "acc_user", "acc_item")}
+        batches = [rep.sample(B) for _ in range(K)]
+        rep.close()
+        loss_dev = dev.train_steps(B, K)
+        loss_ref = sum(_oracle(model, T, p_, n_, False, hp, int(fold1["n_items"])) for p_, n_, _ in batches)
+        assert abs(loss_dev - loss_ref) <= RTOL * abs(loss_ref), (dense, loss_dev, loss_ref)
+        for t in T:
+            assert_close(dev.get_table(t), T[t], (t, dense), **(CML_TRAJ if model == "cml" else {}))
+        dev.close()
