@@ -356,6 +356,8 @@ def main():
                     help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
     ap.add_argument("--pos-sort", type=int, default=-1,
                     help="cf_set_option pos_sort (gradient pairs in positive-item order; -1 default)")
+    ap.add_argument("--pair-prefetch", type=int, default=-1,
+                    help="cf_set_option pair_prefetch (the gradient launch fetches the next draw's pair records)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="cf_set_option deterministic (sort-based ranks, no float atomics)")
     ap.add_argument("--dry-run", action="store_true",
@@ -471,6 +473,8 @@ def main():
         eng.set_option("dense_apply", args.dense_apply)
     if args.pos_sort >= 0:
         eng.set_option("pos_sort", args.pos_sort)
+    if args.pair_prefetch >= 0:
+        eng.set_option("pair_prefetch", args.pair_prefetch)
     if args.deterministic:
         eng.set_option("deterministic", 1)
     if args.slot_max:

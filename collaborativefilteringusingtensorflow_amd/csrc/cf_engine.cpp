@@ -67,6 +67,9 @@ struct cf_engine {
     int64_t* indptr = nullptr;
     int32_t* indices = nullptr;
     int4* pairs = nullptr;   // (u, i, row start, row length) per interaction
+    int4* pf_recs[2] = {nullptr, nullptr};   // prefetched pair records per buffer set (StepArgs::pf_out)
+    int pf_cap = 0;
+    int pair_prefetch = 0;   // measured slower at cfg2 (gradient launch +20 us, draw -2 us): off
     unsigned long long* pos_set = nullptr;  // Pos(u) membership set of (u << 32 | i) keys
     uint64_t pos_mask = 0;
     int neg_check = 0;       // cf_set_option("neg_check"): 1 = Pos(u) set, 0 = CSR row scan
@@ -105,12 +108,12 @@ struct cf_engine {
     // in cntP, pairs visited in positive-item order, one partial row per
     // (gradient block, positive item) in slotP (StepArgs::cntP)
     int pos_sort = 2;                 // 0 off, 1 on, 2 auto: on for B >= kPsortAutoB
-    int capP = 8;
+    int capP = 8;                     // obsolete (slot_max_pos): partials are uncapped since round 3
     int32_t* cntP_[2] = {nullptr, nullptr};
     int2* offPN = nullptr;            // [n_items + 1] exclusive scans of (positives, negatives) per item
     int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
     int order_cap = 0;
-    float* slotP = nullptr;           // [n_items * capP, d]
+    float* slotP = nullptr;           // [order_cap / kPsortPPB + 1 + n_items, d] (StepArgs::slotP)
     float* slotN = nullptr;           // [order_cap * n_neg, d] compact negative slot rows (offN[j] + rank)
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
@@ -296,7 +299,10 @@ bool psort_possible(const cf_engine* e) {
 
 bool psort_active(const cf_engine* e, int B) {
     const cf_config& c = e->cfg;
-    if (!psort_possible(e) || (e->pos_sort == 2 && B < kPsortAutoB) || e->det || e->hot_rep > 1 ||
+    // deterministic mode keeps pos_sort (sort-based ranks) except
+    // on the multi-rank item reduce
+    if (!psort_possible(e) || (e->pos_sort == 2 && B < kPsortAutoB) || (e->det && c.dense_item_apply) ||
+        e->hot_rep > 1 ||
         e->neg_check == 2 || e->pipeline == 2)
         return false;
     if (e->grad_path == 1 || (e->grad_path == 0 && c.model == CF_CML && c.n_neg == 5)) return false;
@@ -312,13 +318,11 @@ int ensure_slots(cf_engine* e) {
     dfree(e->slotVb);
     dfree(e->recV);
     dfree(e->GVrep);
-    dfree(e->slotP);
     dfree(e->offPN);
     for (int k = 0; k < 2; ++k) dfree(e->cntP_[k]);
     if (e->psort_tmp) (void)hipFree(e->psort_tmp);
     e->psort_tmp = nullptr;
     if (psort_possible(e)) {
-        CF_TRY(dalloc(&e->slotP, (size_t)c.n_items * e->capP * c.n_factors));
         CF_TRY(dalloc(&e->offPN, (size_t)c.n_items + 1));
         for (int k = 0; k < 2; ++k) {
             CF_TRY(dalloc(&e->cntP_[k], (size_t)c.n_items));
@@ -364,7 +368,7 @@ int ensure_det(cf_engine* e, int B) {
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     e->det_tmp = nullptr;
     e->det_cap = 0;
-    const int64_t rows = c.n_users + c.n_items;
+    const int64_t rows = c.n_users + 2 * c.n_items;   // pos_sort ranks positives and negatives apart
     CF_TRY(dalloc(&e->det_keys, (size_t)(2 * n)));
     CF_TRY(dalloc(&e->det_vals, (size_t)(2 * n)));
     CF_TRY(dalloc(&e->det_off, (size_t)rows));
@@ -432,7 +436,11 @@ int ensure_order(cf_engine* e, int B) {
     CF_HIP(hipStreamSynchronize(e->side));
     dfree(e->srec);
     dfree(e->slotN);
+    dfree(e->slotP);
     CF_TRY(dalloc(&e->srec, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg)));
+    // one partial row per (gradient block, positive item): row block + item
+    CF_TRY(dalloc(&e->slotP, ((size_t)std::max(B, e->Bcap) / kPsortPPB + 1 + (size_t)e->cfg.n_items) *
+                                 e->cfg.n_factors));
     CF_TRY(dalloc(&e->slotN, (size_t)std::max(B, e->Bcap) * e->cfg.n_neg * e->cfg.n_factors));
     // in-range ids from the start (a given-up fused scatter leaves old records)
     CF_HIP(hipMemsetAsync(e->srec, 0, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg) * 4, e->stream));
@@ -513,8 +521,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.cntP = e->cntP_[k];
         a.srec = e->srec;
         a.slotP = e->slotP;
-        a.capP = e->capP;
         a.slotV = e->slotN;   // negatives: compact slots offN[j] + rank
+        a.offV = nullptr;     // (deterministic mode: users keep their compact slots offU[u] + rank)
     }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
@@ -704,7 +712,6 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         p.cntP = a.cntP;
         p.offPN = e->offPN;
         p.slotP = a.slotP;
-        p.capP = a.capP;
         p.nPos = B;
         // visit every row of a table that is not much larger than the batch's
         // occurrences of it (cfg2 at 2^19: 100K items / 1.05M occurrences,
@@ -720,7 +727,7 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         p.dense_users = 0;
     }
     p.n_users = c.n_users;
-    if (e->det) {
+    if (e->det && a.cntP == nullptr) {
         p.hotP = e->hotP;
         p.hotPb = e->hotPb;
     }
@@ -772,15 +779,19 @@ int det_ranks(cf_engine* e, const StepArgs& a) {
     if (!e->det) return CF_OK;
     const cf_config& c = e->cfg;
     const int64_t nU = (int64_t)a.B * users_per_pair(c), nV = (int64_t)a.B * items_per_pair(c);
-    CF_HIP(launch_det_ranks(a.occU, nU, a.occV, nV, c.n_users, c.n_users + c.n_items, a.rankU, a.rankV,
-                            e->det_off, e->det_keys, e->det_vals, e->det_tmp, e->det_tmp_bytes, e->stream));
+    // pos_sort: a positive's rank among its item's positives, a negative's
+    // among its item's negatives (the draw's cntP / cntV split)
+    const bool ps = a.cntP != nullptr;
+    CF_HIP(launch_det_ranks(a.occU, nU, a.occV, nV, c.n_users, c.n_users + (ps ? 2 : 1) * c.n_items, a.rankU,
+                            a.rankV, e->det_off, e->det_keys, e->det_vals, e->det_tmp, e->det_tmp_bytes, e->stream,
+                            ps ? (int64_t)a.B : 0));
     return CF_OK;
 }
 
 // deterministic mode, after the gradient launch: the sums of the sorted
 // occurrence list's 64-slot tiles that lie inside one row, for the apply
 int det_hot(cf_engine* e, const StepArgs& a) {
-    if (!e->det) return CF_OK;
+    if (!e->det || a.cntP != nullptr) return CF_OK;   // pos_sort sums no tiles
     const cf_config& c = e->cfg;
     HotArgs h{};
     h.d = c.n_factors;
@@ -809,6 +820,7 @@ int psort(cf_engine* e, const StepArgs& a) {
     q.cntU = a.cntU; q.cntV = a.cntV; q.cntP = a.cntP;
     q.offPN = e->offPN;
     q.srec = e->srec;
+    q.offU = e->det ? a.offU : nullptr;
     q.B = a.B; q.W = a.W; q.capU = a.capU;
     q.n_items = e->cfg.n_items;
     CF_HIP(launch_psort(q, e->psort_tmp, e->psort_tmp_bytes, e->stream));
@@ -879,12 +891,31 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
     if (e->prep_side) CF_HIP(hipStreamWaitEvent(e->stream, e->apply_done[k], 0));
     StepArgs a;
     CF_TRY(begin_step(e, B, nullptr, nullptr, nullptr, k, e->stream, &a));
+    // the positive-sorted gradient launch of step s fetches step s+1's pair
+    // records (StepArgs::pf_out); the draw of s+1 then reads them coalesced
+    const bool pf = e->pair_prefetch && a.srec != nullptr && e->pipeline == 1 && !e->prep_side &&
+                    a.pos_set == nullptr;
+    if (pf && e->pf_cap < B) {
+        CF_HIP(hipStreamSynchronize(e->stream));
+        for (int q = 0; q < 2; ++q) {
+            dfree(e->pf_recs[q]);
+            CF_TRY(dalloc(&e->pf_recs[q], (size_t)B));
+        }
+        e->pf_cap = B;
+    }
     for (int s = 0; s < n; ++s) {
         StepArgs nx{};
         const bool more = s + 1 < n;
         if (more) {
             nx = base_step_args(e, B, k ^ 1);
             CF_TRY(sampler_args(e, B, &nx));
+            if (pf) {
+                a.pf_out = e->pf_recs[k ^ 1];
+                a.pf_slot_base = nx.slot_base;
+                a.pf_perm = nx.perm;
+                a.pf_B = B;
+                nx.pre_pairs = e->pf_recs[k ^ 1];
+            }
         }
         CF_TRY(finish_step(e, a, B, k, loss_acc, more ? &nx : nullptr));
         a = nx;
@@ -1190,6 +1221,7 @@ int cf_destroy(cf_engine* e) {
     for (int t = 0; t < 6; ++t)   // bound tables belong to the caller
         if (e->own_tab[t]) *table_slot(e, t) = e->own_tab[t];
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
+    dfree(e->pf_recs[0]); dfree(e->pf_recs[1]);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
@@ -2126,6 +2158,11 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
         e->topk_path = (int)value;
+        return CF_OK;
+    }
+    if (n == "pair_prefetch") {
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "pair_prefetch must be 0 or 1");
+        e->pair_prefetch = (int)value;
         return CF_OK;
     }
     if (n == "prep_stream") {

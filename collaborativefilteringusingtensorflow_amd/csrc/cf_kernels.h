@@ -68,6 +68,17 @@ struct StepArgs {
     // (u << 32 | i) keys, linear probing (null: scan the user's CSR row)
     const unsigned long long* __restrict__ pos_set;
     uint64_t pos_mask;                      // capacity - 1 (power of two)
+    // pair-record prefetch (round 3, cf_set_option "pair_prefetch"): the
+    // positive-sorted gradient launch of step s also fetches step s+1's
+    // shuffled pair records -- pairs[permute(pf_slot_base + p, pf_perm)] for
+    // p < pf_B, one per 16-lane group -- into pf_out[p], so that step s+1's
+    // draw (pre_pairs = that buffer) reads them coalesced and starts at the
+    // row scan.  Same records, same batches.  null = off
+    int4* __restrict__ pf_out;
+    uint64_t pf_slot_base;
+    PermKey pf_perm;
+    int pf_B;
+    const int4* __restrict__ pre_pairs;     // the draw's record of pair p at [p] (null: pairs[permute(..)])
     int lane_draw;                          // 1: one lane per pair (neg_check 2, with the set)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -108,17 +119,18 @@ struct StepArgs {
     // (rankV[p] = its rank among the batch's positives of that item) and its
     // negatives in cntV; psort orders the pairs by positive item (order), so
     // the pairs of one gradient block that share a positive item sum its
-    // gradient in LDS and store ONE partial row per (block, item): partial k =
-    // block - offP[i] / kPsortPPB of item i goes to slotP[i * capP + k] (k <
-    // capP) or float atomics into GV.  null cntP = off
+    // gradient in LDS and store ONE partial row per (block, item): the
+    // partial of block b for item i goes to slotP[b + i] -- unique, since the
+    // runs are contiguous in item order, and item i's partials are the
+    // contiguous rows [offP[i] / kPsortPPB + i, + blocks its run spans), in
+    // block order (no cap, no atomics).  null cntP = off
     int32_t* __restrict__ cntP;         // [n_items] positives per item (0 between steps)
     // [B, psort_stride(W)] the pair at each positive-sorted position as one
     // contiguous record (u, i, j_0 .. j_{W-1}, then the ranks of u, j_0, ..
     // as 16-bit halves, clamped to 0xFFFF -- a rank only matters below the
     // slot caps, <= 256), so the gradient launch reads its ids coalesced
     const int32_t* __restrict__ srec;
-    float* __restrict__ slotP;          // [n_items * capP, d]
-    int capP;
+    float* __restrict__ slotP;          // [B / kPsortPPB + 1 + n_items, d]
     // ... and the negatives in compact slots: with pos_sort, slotV is the
     // [B * W, d] array where negative occurrence k of item j stores its
     // gradient row at offN[j] + k (offN = exclusive scan of the negatives'
@@ -214,8 +226,7 @@ struct ApplyArgs {
     // negatives' compact slot rows at slotV[offN[r] + k]
     int32_t* __restrict__ cntP;
     const int2* __restrict__ offPN;      // [n_items + 1] (offP, offN), see StepArgs
-    const float* __restrict__ slotP;
-    int capP;
+    const float* __restrict__ slotP;     // see StepArgs
     int64_t nPos;
     // pos_sort apply: visit every item row (dense_items) / every user row
     // (dense_users) instead of finding the owners among the occurrences --
@@ -358,10 +369,14 @@ hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // the earlier occurrences of its row, and off[row] = the row's first sorted
 // position; tmp / keys / vals sized by det_ranks_scratch
 size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows);
+// nPos > 0 (deterministic pos_sort): the first nPos item occurrences are the
+// positives, ranked among the positives of their item, the rest among the
+// negatives of theirs (item keys 2 * item + is_negative; n_rows = n_users + 2
+// n_items), as the draw's cntP / cntV split counts them
 hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV, int64_t nV,
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
-                            hipStream_t s);
+                            hipStream_t s, int64_t nPos = 0);
 // positive-sorted gradient: offPN = exclusive scans of (cntP, cntV) (two
 // launches of tile sums + tile scans), then the pair records at
 // srec[offP[i_p] + rankV[p]] for the B pairs; tmp sized by psort_scratch
@@ -373,6 +388,7 @@ struct PsortArgs {
     const int32_t* cntV; const int32_t* cntP;
     int2* offPN;                         // written: [n_items + 1] exclusive scans of (cntP, cntV)
     int32_t* srec;                       // [B, psort_stride(W)]
+    const int32_t* offU;                 // deterministic mode: user slot off[u] + rank (null: u * capU + rank)
     int B, W, capU;
     int64_t n_items;
 };

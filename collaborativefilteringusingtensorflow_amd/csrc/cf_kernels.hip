@@ -428,10 +428,11 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
     int64_t rb = 0, re = 0;
     if (a.sample) {
         const uint64_t slot = a.slot_base + (uint64_t)p;
-        const uint64_t idx = permute(slot, a.perm);   // shuffled pair order (sampler_ranking.py:24)
-        // one 16-B record per pair carries the user's CSR extent, so the row
-        // scan does not wait on a dependent indptr load
-        const int4 pr = a.pairs[idx];
+        // shuffled pair order (sampler_ranking.py:24); one 16-B record per pair
+        // carries the user's CSR extent, so the row scan does not wait on a
+        // dependent indptr load.  pre_pairs: the record the previous step's
+        // gradient launch fetched (StepArgs::pf_out), read coalesced
+        const int4 pr = a.pre_pairs != nullptr ? a.pre_pairs[p] : a.pairs[permute(slot, a.perm)];
         u = pr.x;
         i = pr.y;
         key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
@@ -1621,8 +1622,8 @@ struct PairRows {
 // pos_sort: the first group of a run of the block's pairs that share the
 // positive item i sums the run's gradient rows (LDS, in position order) and
 // finishes the item once for the whole run: Adagrad now if the run is the
-// item's only occurrence in the batch, else the block's partial row -> slot
-// (partial k = block - offP[i] / kPsortPPB) or, past capP, float atomics
+// item's only occurrence in the batch, else the block's partial row ->
+// slotP[block + i] (StepArgs: item i's partials are contiguous, block order)
 template <int MODEL, int EPL, int WT, int GPB>
 __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MODEL, EPL, WT>& r, int block,
                                            int grp, int gl, const float (*s_gi)[kGL * EPL],
@@ -1641,11 +1642,7 @@ __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MOD
             gapply_pre<EPL>(a.V, a.AV, r.i, a.d, gl, r.vi, r.ai, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) a.cntP[r.i] = 0;
     } else {
-        const int k = block - r.oi / kPsortPPB;
-        if (k < a.capP)
-            gstore<EPL>(a.slotP, (int64_t)r.i * a.capP + k, a.d, gl, g);
-        else
-            gatomic<EPL>(a.GV, r.i, a.d, gl, g);
+        gstore<EPL>(a.slotP, (int64_t)block + r.i, a.d, gl, g);
     }
 }
 
@@ -1666,6 +1663,22 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     for (int k = 0; k < P; ++k) {
         pp[k] = (block * P + k) * GPB + grp;
         ok[k] = pp[k] < a.B;
+    }
+    // pair-record prefetch for the next step (StepArgs::pf_out): issued
+    // first, stored last, so its latency hides under this block's pairs
+    int4 pfr = make_int4(0, 0, 0, 0);
+    int64_t pfp = -1;
+#ifndef CF_PAIR_PREFETCH
+#define CF_PAIR_PREFETCH 1   // 0: the prefetch compiled out (A/B of its cost to the kernel body)
+#endif
+    if constexpr (SORT && CF_PAIR_PREFETCH) {
+        if (a.pf_out != nullptr && gl == 0) {
+            const int64_t q = (int64_t)block * GPB + grp;
+            if (q < a.pf_B) {
+                pfp = q;
+                pfr = a.pairs[permute(a.pf_slot_base + (uint64_t)q, a.pf_perm)];
+            }
+        }
     }
 #pragma unroll
     for (int k = 0; k < P; ++k)
@@ -1711,6 +1724,9 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
 #pragma unroll
         for (int k = 0; k < GPB; ++k) t += s_loss[k];
         a.loss_partial[block] = t;
+    }
+    if constexpr (SORT && CF_PAIR_PREFETCH) {
+        if (pfp >= 0) a.pf_out[pfp] = pfr;
     }
 }
 
@@ -2387,7 +2403,8 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
     }
     const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
     const int nn = cn;   // every negative occurrence has its compact slot
-    const int npp = np < a.capP ? np : a.capP;
+    const int npp = np;  // and every (block, item) partial its row
+    const float* P0 = a.slotP + ((int64_t)(o / kPsortPPB) + r) * a.d;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
     // the negatives' compact slot rows [on, on + nn) in rank order (contiguous),
@@ -2402,7 +2419,7 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
             const int t = t0 + q;
             if (t < nt) {
                 const float* row = t < nn ? a.slotV + ((int64_t)on + t) * a.d
-                                          : a.slotP + (r * a.capP + (t - nn)) * (int64_t)a.d;
+                                          : P0 + (int64_t)(t - nn) * a.d;
                 row_ld<EPL>(row, a.d, gl, 0.f, h[q]);
             }
         }
@@ -2412,13 +2429,6 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
             }
-    }
-    if (np > a.capP) {   // partials past the positives' slot range: float atomics into GV
-        float h[EPL];
-        gload<EPL>(a.GV, r, a.d, gl, h);
-#pragma unroll
-        for (int s = 0; s < EPL; ++s) g[s] += h[s];
-        if (!reduce_only) row_zero<EPL>(a.GV + r * a.d, a.d, gl);
     }
     if (reduce_only)
         row_st<EPL>(a.GV + r * (int64_t)a.d, a.d, gl, g);
@@ -3212,6 +3222,7 @@ hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next) {
     if (a.B <= 0) return next ? launch_prep(*next, s) : hipSuccess;
     if (next && next->model != a.model) return hipErrorInvalidValue;
     if (a.srec != nullptr && fast_w(a) == 0) return hipErrorInvalidValue;   // pos_sort: phased kernel only
+    if (a.pf_out != nullptr && a.srec == nullptr) return hipErrorInvalidValue;   // only grad_sort_kernel prefetches
     switch (a.model) {
         case BPR: return launch_grad_m<BPR>(a, next, s);
         case GBPR: return launch_grad_m<GBPR>(a, next, s);

@@ -466,8 +466,9 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                results up to fp32 summation order.  0 = off; 2 = auto
  *                (default): on for batches of >= 2^18 pairs (cfg2: 7 %
  *                faster steps at 2^19, 3.5 % at 2^18, even at 2^17).
- *   "slot_max_pos" positive partial rows per item row under pos_sort (default
- *                8; later partials of a hot item add with float atomics).
+ *   "slot_max_pos" accepted for compatibility, no effect since round 3:
+ *                every (gradient block, positive item) partial has its own
+ *                row (block + item), so no partial adds with float atomics.
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
  *                item occurrences are counted like user ones, a row seen
  *                once stores its gradient row into the bound buffer, a
