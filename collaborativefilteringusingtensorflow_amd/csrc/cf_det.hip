@@ -20,16 +20,11 @@ namespace {
 
 __global__ void det_keys_kernel(const int32_t* __restrict__ occU, int64_t nU,
                                 const int32_t* __restrict__ occV, int64_t nV, int64_t n_users,
-                                int64_t nPos, int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+                                int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nt = (int64_t)gridDim.x * blockDim.x;
     for (int64_t q = t0; q < nU + nV; q += nt) {
-        if (q < nU)
-            keys[q] = occU[q];
-        else if (nPos > 0)   // pos_sort: positives and negatives of an item ranked apart
-            keys[q] = (int32_t)(n_users + 2 * (int64_t)occV[q - nU] + (q - nU >= nPos ? 1 : 0));
-        else
-            keys[q] = (int32_t)(n_users + occV[q - nU]);
+        keys[q] = q < nU ? occU[q] : (int32_t)(n_users + occV[q - nU]);
         vals[q] = (int32_t)q;
     }
 }
@@ -119,8 +114,7 @@ __global__ __launch_bounds__(256) void psort_scatter_kernel(PsortArgs a) {
         v[1] = i;
 #pragma unroll
         for (int w = 0; w < W; ++w) v[2 + w] = j[w];
-        v[2 + W] = cu == 1 ? kSlotApply : a.offU != nullptr ? a.offU[u] + ru
-                                        : ru < a.capU ? u * a.capU + ru : kSlotAtomic;
+        v[2 + W] = cu == 1 ? kSlotApply : ru < a.capU ? u * a.capU + ru : kSlotAtomic;
         v[3 + W] = (int32_t)((uint32_t)oP | (ci == 1 ? 0x80000000u : 0u));
 #pragma unroll
         for (int w = 0; w < W; ++w) v[4 + W + w] = cj[w] == 1 ? kSlotApply : oN[w] + rj[w];
@@ -273,11 +267,11 @@ size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows) {
 hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV, int64_t nV,
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
-                            hipStream_t s, int64_t nPos) {
+                            hipStream_t s) {
     const int64_t n = nU + nV;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(det_keys_kernel, dim3(grid_of(n)), dim3(256), 0, s, occU, nU, occV, nV, n_users,
-                       nPos, keys, vals);
+                       keys, vals);
     size_t bytes = tmp_bytes;
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, keys + n, vals, vals + n, (int)n, 0,
                                                       key_bits(n_rows), s);

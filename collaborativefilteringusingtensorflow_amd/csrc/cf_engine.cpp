@@ -68,6 +68,12 @@ struct cf_engine {
     int32_t* indices = nullptr;
     int4* pairs = nullptr;   // (u, i, row start, row length) per interaction
     int4* pf_recs[2] = {nullptr, nullptr};   // prefetched pair records per buffer set (StepArgs::pf_out)
+    // deterministic mode on the pos_sort path: fixed-point partials and the
+    // users' int64 overflow accumulators (StepArgs::det_fx)
+    long long* slotP64 = nullptr;
+    unsigned long long* GU64 = nullptr;
+    unsigned long long* GV64 = nullptr;
+    int fx_cap = 0;
     int pf_cap = 0;
     int pair_prefetch = 0;   // measured slower at cfg2 (gradient launch +20 us, draw -2 us): off
     unsigned long long* pos_set = nullptr;  // Pos(u) membership set of (u << 32 | i) keys
@@ -108,7 +114,7 @@ struct cf_engine {
     // in cntP, pairs visited in positive-item order, one partial row per
     // (gradient block, positive item) in slotP (StepArgs::cntP)
     int pos_sort = 2;                 // 0 off, 1 on, 2 auto: on for B >= kPsortAutoB
-    int capP = 8;                     // obsolete (slot_max_pos): partials are uncapped since round 3
+    int capP = 8;                     // partial rows per item (slot_max_pos); later ones add with atomics
     int32_t* cntP_[2] = {nullptr, nullptr};
     int2* offPN = nullptr;            // [n_items + 1] exclusive scans of (positives, negatives) per item
     int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
@@ -299,8 +305,8 @@ bool psort_possible(const cf_engine* e) {
 
 bool psort_active(const cf_engine* e, int B) {
     const cf_config& c = e->cfg;
-    // deterministic mode keeps pos_sort (sort-based ranks) except
-    // on the multi-rank item reduce
+    // deterministic mode keeps pos_sort (fixed-point sums, StepArgs::det_fx,
+    // DESIGN 3.9) except on the multi-rank item reduce
     if (!psort_possible(e) || (e->pos_sort == 2 && B < kPsortAutoB) || (e->det && c.dense_item_apply) ||
         e->hot_rep > 1 ||
         e->neg_check == 2 || e->pipeline == 2)
@@ -355,6 +361,23 @@ int ensure_slots(cf_engine* e) {
 
 int ensure_det(cf_engine* e, int B) {
     const cf_config& c = e->cfg;
+    if (psort_possible(e) && !c.dense_item_apply) {   // the fixed-point pos_sort form (StepArgs::det_fx)
+        if (B > e->fx_cap) {
+            CF_HIP(hipStreamSynchronize(e->stream));
+            CF_HIP(hipStreamSynchronize(e->side));
+            dfree(e->slotP64);
+            CF_TRY(dalloc(&e->slotP64, ((size_t)B / kPsortPPB + 1 + (size_t)c.n_items) * c.n_factors));
+            e->fx_cap = B;
+        }
+        if (!e->GU64) {
+            CF_TRY(dalloc(&e->GU64, (size_t)c.n_users * c.n_factors));
+            CF_HIP(hipMemsetAsync(e->GU64, 0, (size_t)c.n_users * c.n_factors * 8, e->stream));
+        }
+        if (!e->GV64) {
+            CF_TRY(dalloc(&e->GV64, (size_t)c.n_items * c.n_factors));
+            CF_HIP(hipMemsetAsync(e->GV64, 0, (size_t)c.n_items * c.n_factors * 8, e->stream));
+        }
+    }
     const int64_t nU = (int64_t)B * users_per_pair(c), nV = (int64_t)B * items_per_pair(c);
     const int64_t n = nU + nV;
     if (n <= e->det_cap && e->det_off) return CF_OK;
@@ -368,7 +391,7 @@ int ensure_det(cf_engine* e, int B) {
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     e->det_tmp = nullptr;
     e->det_cap = 0;
-    const int64_t rows = c.n_users + 2 * c.n_items;   // pos_sort ranks positives and negatives apart
+    const int64_t rows = c.n_users + c.n_items;
     CF_TRY(dalloc(&e->det_keys, (size_t)(2 * n)));
     CF_TRY(dalloc(&e->det_vals, (size_t)(2 * n)));
     CF_TRY(dalloc(&e->det_off, (size_t)rows));
@@ -498,7 +521,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.count_items = (!c.dense_item_apply || e->item_reduce) ? 1 : 0;
     a.items_grad_only = (c.dense_item_apply && e->item_reduce) ? 1 : 0;
     if (c.dense_item_apply && e->item_reduce == 2) a.capV = 0;  // duplicates: float atomics
-    if (e->det) {   // compact slots at off[row] + rank, no caps, no atomics
+    const bool ps = psort_active(e, B) && e->cntP_[k] && e->srec && e->order_cap >= B;
+    if (e->det && !ps) {   // compact slots at off[row] + rank, no caps, no atomics
         a.offU = e->det_off;
         a.offV = e->det_off + c.n_users;
         a.slotU = e->slotUc;
@@ -517,12 +541,19 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.stashU = e->stashU;
         a.stashB = e->stashB;
     }
-    if (psort_active(e, B) && e->cntP_[k] && e->srec && e->order_cap >= B) {
+    if (ps) {
         a.cntP = e->cntP_[k];
         a.srec = e->srec;
         a.slotP = e->slotP;
         a.slotV = e->slotN;   // negatives: compact slots offN[j] + rank
-        a.offV = nullptr;     // (deterministic mode: users keep their compact slots offU[u] + rank)
+        a.capP = e->capP;
+        if (e->det && e->slotP64 && e->fx_cap >= B && e->GU64 && e->GV64) {
+            // deterministic: the fast path's launches, every sum in fixed point
+            a.det_fx = 1;
+            a.slotP64 = e->slotP64;
+            a.GU64 = e->GU64;
+            a.GV64 = e->GV64;
+        }
     }
     a.shard_u0 = e->shard_u0;
     a.shard_u1 = e->shard_u1;
@@ -694,6 +725,10 @@ int begin_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
 ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc) {
     const cf_config& c = e->cfg;
     ApplyArgs p{};
+    p.det_fx = a.det_fx;
+    p.slotP64 = a.slotP64;
+    p.GU64 = a.GU64;
+    p.GV64 = a.GV64;
     p.d = c.n_factors;
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
@@ -712,6 +747,7 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         p.cntP = a.cntP;
         p.offPN = e->offPN;
         p.slotP = a.slotP;
+        p.capP = a.capP;
         p.nPos = B;
         // visit every row of a table that is not much larger than the batch's
         // occurrences of it (cfg2 at 2^19: 100K items / 1.05M occurrences,
@@ -776,15 +812,11 @@ int pending_clips(cf_engine* e) {
 // deterministic mode: replace the batch's atomic ranks by sort-based ones
 // (and write off[row]) before its gradient launch
 int det_ranks(cf_engine* e, const StepArgs& a) {
-    if (!e->det) return CF_OK;
+    if (!e->det || a.det_fx) return CF_OK;   // the fixed-point form needs no ranks
     const cf_config& c = e->cfg;
     const int64_t nU = (int64_t)a.B * users_per_pair(c), nV = (int64_t)a.B * items_per_pair(c);
-    // pos_sort: a positive's rank among its item's positives, a negative's
-    // among its item's negatives (the draw's cntP / cntV split)
-    const bool ps = a.cntP != nullptr;
-    CF_HIP(launch_det_ranks(a.occU, nU, a.occV, nV, c.n_users, c.n_users + (ps ? 2 : 1) * c.n_items, a.rankU,
-                            a.rankV, e->det_off, e->det_keys, e->det_vals, e->det_tmp, e->det_tmp_bytes, e->stream,
-                            ps ? (int64_t)a.B : 0));
+    CF_HIP(launch_det_ranks(a.occU, nU, a.occV, nV, c.n_users, c.n_users + c.n_items, a.rankU, a.rankV,
+                            e->det_off, e->det_keys, e->det_vals, e->det_tmp, e->det_tmp_bytes, e->stream));
     return CF_OK;
 }
 
@@ -820,7 +852,6 @@ int psort(cf_engine* e, const StepArgs& a) {
     q.cntU = a.cntU; q.cntV = a.cntV; q.cntP = a.cntP;
     q.offPN = e->offPN;
     q.srec = e->srec;
-    q.offU = e->det ? a.offU : nullptr;
     q.B = a.B; q.W = a.W; q.capU = a.capU;
     q.n_items = e->cfg.n_items;
     CF_HIP(launch_psort(q, e->psort_tmp, e->psort_tmp_bytes, e->stream));
@@ -1221,7 +1252,7 @@ int cf_destroy(cf_engine* e) {
     for (int t = 0; t < 6; ++t)   // bound tables belong to the caller
         if (e->own_tab[t]) *table_slot(e, t) = e->own_tab[t];
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
-    dfree(e->pf_recs[0]); dfree(e->pf_recs[1]);
+    dfree(e->pf_recs[0]); dfree(e->pf_recs[1]); dfree(e->slotP64); dfree(e->GU64); dfree(e->GV64);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);

@@ -79,6 +79,16 @@ struct StepArgs {
     PermKey pf_perm;
     int pf_B;
     const int4* __restrict__ pre_pairs;     // the draw's record of pair p at [p] (null: pairs[permute(..)])
+    // deterministic mode on the positive-sorted path (round 3):
+    // every sum of gradient rows is taken in 64-bit fixed point (kFxOne
+    // units), which is associative, so the result does not depend on the
+    // order the atomic ranks gave the occurrences: positive partials are
+    // int64 rows (slotP64), duplicated users past their slot cap add with
+    // int64 atomics (GU64), the per-pair losses add as integers (kFxLoss)
+    int det_fx;
+    long long* __restrict__ slotP64;        // [B / kPsortPPB + 1 + n_items, d] (as slotP)
+    unsigned long long* __restrict__ GU64;  // [n_users, d], zero between steps
+    unsigned long long* __restrict__ GV64;  // [n_items, d]: positive partials past capP, zero between steps
     int lane_draw;                          // 1: one lane per pair (neg_check 2, with the set)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -119,11 +129,13 @@ struct StepArgs {
     // (rankV[p] = its rank among the batch's positives of that item) and its
     // negatives in cntV; psort orders the pairs by positive item (order), so
     // the pairs of one gradient block that share a positive item sum its
-    // gradient in LDS and store ONE partial row per (block, item): the
-    // partial of block b for item i goes to slotP[b + i] -- unique, since the
-    // runs are contiguous in item order, and item i's partials are the
-    // contiguous rows [offP[i] / kPsortPPB + i, + blocks its run spans), in
-    // block order (no cap, no atomics).  null cntP = off
+    // gradient in LDS and store ONE partial row per (block, item): partial k =
+    // b - offP[i] / kPsortPPB of block b goes to slotP[b + i] when k < capP --
+    // unique, since the runs are contiguous in item order, and item i's
+    // partials are the contiguous rows [offP[i] / kPsortPPB + i, + min(blocks
+    // its run spans, capP)) in block order -- else it adds with float atomics
+    // into GV (deterministic mode: int64 atomics into GV64), so the apply's
+    // chain for a Zipf-head item stays capP + 1 rows.  null cntP = off
     int32_t* __restrict__ cntP;         // [n_items] positives per item (0 between steps)
     // [B, psort_stride(W)] the pair at each positive-sorted position as one
     // contiguous record (u, i, j_0 .. j_{W-1}, then the ranks of u, j_0, ..
@@ -131,6 +143,7 @@ struct StepArgs {
     // slot caps, <= 256), so the gradient launch reads its ids coalesced
     const int32_t* __restrict__ srec;
     float* __restrict__ slotP;          // [B / kPsortPPB + 1 + n_items, d]
+    int capP;
     // ... and the negatives in compact slots: with pos_sort, slotV is the
     // [B * W, d] array where negative occurrence k of item j stores its
     // gradient row at offN[j] + k (offN = exclusive scan of the negatives'
@@ -162,6 +175,11 @@ constexpr int32_t kRemoteFlag = 1 << 24;
 // per 16-lane group): partial k of an item covers the positions of block
 // offP[i] / kPsortPPB + k
 constexpr int kPsortPPB = kGroupsPerBlock;
+// fixed-point units of the deterministic pos_sort path: gradients 2^-32
+// (|sum| < 2^31), per-pair losses 2^-24 (a step's integer total < 2^53)
+constexpr float kFxOne = 4294967296.f;
+constexpr double kFxInv = 1.0 / 4294967296.0;
+constexpr double kFxLoss = 16777216.0;
 
 // A pos_sort record carries every occurrence's resolved destination --
 // psort_scatter reads the batch's final counts and offsets, so the gradient
@@ -187,6 +205,10 @@ struct XchgArgs {
 };
 
 struct ApplyArgs {
+    int det_fx;                               // fixed-point sums (StepArgs::det_fx)
+    const long long* __restrict__ slotP64;
+    unsigned long long* __restrict__ GU64;
+    unsigned long long* __restrict__ GV64;
     int d;
     float lr;
     float clip_norm;
@@ -227,6 +249,7 @@ struct ApplyArgs {
     int32_t* __restrict__ cntP;
     const int2* __restrict__ offPN;      // [n_items + 1] (offP, offN), see StepArgs
     const float* __restrict__ slotP;     // see StepArgs
+    int capP;
     int64_t nPos;
     // pos_sort apply: visit every item row (dense_items) / every user row
     // (dense_users) instead of finding the owners among the occurrences --
@@ -369,14 +392,10 @@ hipError_t launch_pack_batch(const PackArgs& a, hipStream_t s);
 // the earlier occurrences of its row, and off[row] = the row's first sorted
 // position; tmp / keys / vals sized by det_ranks_scratch
 size_t det_ranks_scratch(int64_t n_occ, int64_t n_rows);
-// nPos > 0 (deterministic pos_sort): the first nPos item occurrences are the
-// positives, ranked among the positives of their item, the rest among the
-// negatives of theirs (item keys 2 * item + is_negative; n_rows = n_users + 2
-// n_items), as the draw's cntP / cntV split counts them
 hipError_t launch_det_ranks(const int32_t* occU, int64_t nU, const int32_t* occV, int64_t nV,
                             int64_t n_users, int64_t n_rows, int32_t* rankU, int32_t* rankV,
                             int32_t* off, int32_t* keys, int32_t* vals, void* tmp, size_t tmp_bytes,
-                            hipStream_t s, int64_t nPos = 0);
+                            hipStream_t s);
 // positive-sorted gradient: offPN = exclusive scans of (cntP, cntV) (two
 // launches of tile sums + tile scans), then the pair records at
 // srec[offP[i_p] + rankV[p]] for the B pairs; tmp sized by psort_scratch
@@ -388,7 +407,6 @@ struct PsortArgs {
     const int32_t* cntV; const int32_t* cntP;
     int2* offPN;                         // written: [n_items + 1] exclusive scans of (cntP, cntV)
     int32_t* srec;                       // [B, psort_stride(W)]
-    const int32_t* offU;                 // deterministic mode: user slot off[u] + rank (null: u * capU + rank)
     int B, W, capU;
     int64_t n_items;
 };

@@ -163,6 +163,43 @@ __device__ __forceinline__ void gatomic(float* __restrict__ G, int64_t r, int d,
     }
 }
 
+// deterministic mode on the positive-sorted path (StepArgs::det_fx): row sums
+// in 64-bit fixed point -- integer adds are associative, so a sum does not
+// depend on the order the occurrences arrive in (the atomic ranks, which
+// pairs share a gradient block).  to_fx rounds once per term; |sum| < 2^31
+__device__ __forceinline__ long long to_fx(float x) { return __float2ll_rn(x * kFxOne); }
+__device__ __forceinline__ float from_fx(long long v) { return (float)((double)v * kFxInv); }
+
+template <int EPL>
+__device__ __forceinline__ void fx_ld_add(const long long* __restrict__ row, int d, int gl, long long (&t)[EPL]) {
+    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = elem_of<EPL>(s, gl, full);
+        if (e < d) t[s] += row[e];
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void fx_st(long long* __restrict__ row, int d, int gl, const long long (&t)[EPL]) {
+    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = elem_of<EPL>(s, gl, full);
+        if (e < d) row[e] = t[s];
+    }
+}
+
+template <int EPL>
+__device__ __forceinline__ void fx_atomic(unsigned long long* __restrict__ row, int d, int gl, const float (&g)[EPL]) {
+    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        const int e = elem_of<EPL>(s, gl, full);
+        if (e < d) atomicAdd(row + e, (unsigned long long)to_fx(g[s]));
+    }
+}
+
 template <int EPL>
 __device__ __forceinline__ float gdot(const float (&x)[EPL], const float (&y)[EPL]) {
     float t = 0.f;
@@ -1307,7 +1344,10 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
         gstore<EPL>(S, slot, d, gl, g);
     } else {
 #ifndef CF_EXP_NO_ATOMIC
-        gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
+        if (a.GU64 != nullptr && X == a.U)   // deterministic pos_sort: a user past its slot cap
+            fx_atomic<EPL>(a.GU64 + r * (int64_t)d, d, gl, g);
+        else
+            gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
 #endif
         if (a.items_grad_only && a.capV == 0 && X == a.V && gl == 0) cnt[r] = 0;  // see gfinish
     }
@@ -1624,10 +1664,33 @@ struct PairRows {
 // finishes the item once for the whole run: Adagrad now if the run is the
 // item's only occurrence in the batch, else the block's partial row ->
 // slotP[block + i] (StepArgs: item i's partials are contiguous, block order)
-template <int MODEL, int EPL, int WT, int GPB>
+// or, past capP, float atomics
+template <int MODEL, int EPL, int WT, int GPB, bool FX>
 __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MODEL, EPL, WT>& r, int block,
                                            int grp, int gl, const float (*s_gi)[kGL * EPL],
                                            const int* s_item) {
+    const int k = block - r.oi / kPsortPPB;   // the item's k-th partial
+    if (FX && r.ci != 1) {   // deterministic: the block's partial as an exact fixed-point sum
+        long long t[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) t[s] = to_fx(s_gi[grp][s * kGL + gl]);
+        for (int q = grp + 1; q < GPB && s_item[q] == r.i; ++q) {
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) t[s] += to_fx(s_gi[q][s * kGL + gl]);
+        }
+        if (k < a.capP) {
+            fx_st<EPL>(a.slotP64 + ((int64_t)block + r.i) * a.d, a.d, gl, t);
+        } else {   // past capP: int64 atomics, exact in any order
+            unsigned long long* row = a.GV64 + (int64_t)r.i * a.d;
+            const bool full = CF_VEC_ROWS && a.d == kGL * EPL;
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) {
+                const int e = elem_of<EPL>(s, gl, full);
+                if (e < a.d) atomicAdd(row + e, (unsigned long long)t[s]);
+            }
+        }
+        return;
+    }
     float g[EPL];
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = s_gi[grp][s * kGL + gl];
@@ -1642,11 +1705,14 @@ __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MOD
             gapply_pre<EPL>(a.V, a.AV, r.i, a.d, gl, r.vi, r.ai, g, a.lr, a.clip != 0, a.clip_norm);
         if (gl == 0) a.cntP[r.i] = 0;
     } else {
-        gstore<EPL>(a.slotP, (int64_t)block + r.i, a.d, gl, g);
+        if (k < a.capP)
+            gstore<EPL>(a.slotP, (int64_t)block + r.i, a.d, gl, g);
+        else
+            gatomic<EPL>(a.GV, r.i, a.d, gl, g);
     }
 }
 
-template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock, bool SORT = false>
+template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock, bool SORT = false, bool FX = false>
 __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     static_assert(!SORT || (P == 1 && MODEL != GBPR && GPB == kPsortPPB), "pos_sort: one pair per group");
     __shared__ double s_loss[GPB];
@@ -1712,12 +1778,16 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
         if (gl == 0) s_item[grp] = ok[0] ? pr[0].i : -1;
         __syncthreads();
         if (ok[0] && (grp == 0 || s_item[grp - 1] != pr[0].i))
-            psort_head<MODEL, EPL, WT, GPB>(a, pr[0], block, grp, gl, s_gi, s_item);
+            psort_head<MODEL, EPL, WT, GPB, FX>(a, pr[0], block, grp, gl, s_gi, s_item);
     }
 
     const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
     const float sq_g = gsum(sq);
-    if (gl == 0) s_loss[grp] = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
+    if (gl == 0) {
+        const double lp = (double)loss_g + 0.5 * (double)coef * (double)sq_g;
+        // deterministic: integer units, so the block and fold sums are exact
+        s_loss[grp] = FX ? rint(lp * kFxLoss) : lp;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
@@ -1752,9 +1822,9 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #ifndef CF_SORT_MIN_WAVES
 #define CF_SORT_MIN_WAVES 1
 #endif
-template <int MODEL, int EPL, int WT>
+template <int MODEL, int EPL, int WT, bool FX = false>
 __global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a) {
-    grad_fast_body<MODEL, EPL, WT, 1, kGroupsPerBlock, true>(a, blockIdx.x);
+    grad_fast_body<MODEL, EPL, WT, 1, kGroupsPerBlock, true, FX>(a, blockIdx.x);
 }
 
 // the same gradient blocks at one wave per workgroup (no draw blocks): a
@@ -2263,7 +2333,7 @@ __device__ __forceinline__ void slot_sum(const ApplyArgs& a, bool isU, int64_t s
 
 // HOT: the deterministic-mode launch that adds whole-tile sums (its own
 // instantiation: the tile path's registers would slow every fast-path apply)
-template <int EPL, bool HOT = false>
+template <int EPL, bool HOT = false, bool FX = false>
 __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool isU, int c, int gl) {
     int32_t* cnt = isU ? a.cntU : a.cntV;
     float* X = isU ? a.U : a.V;
@@ -2313,6 +2383,34 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
                 }
         }
         slot_sum<EPL, NF>(a, isU, s0, (int)(qb * kDetTile - gs), ns, gl, g, bsum);
+    } else if (FX && isU) {
+        // deterministic pos_sort (users): the slot rows and the int64 atomic
+        // overflow (GU64) summed exactly in fixed point, in any order
+        long long t[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) t[s] = 0;
+        for (int t0 = 0; t0 < ns; t0 += NF) {
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < ns) gload<EPL>(a.slotU, s0 + t0 + q, a.d, gl, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < ns) {
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) t[s] += to_fx(h[q][s]);
+                }
+        }
+        if (local > cap) {
+            unsigned long long* row = a.GU64 + r * (int64_t)a.d;
+            fx_ld_add<EPL>(reinterpret_cast<const long long*>(row), a.d, gl, t);
+            long long z[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) z[s] = 0;
+            fx_st<EPL>(reinterpret_cast<long long*>(row), a.d, gl, z);
+        }
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] = from_fx(t[s]);
     } else {
         slot_sum<EPL, NF>(a, isU, s0, 0, ns, gl, g, bsum);
     }
@@ -2321,7 +2419,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
 #pragma unroll
         for (int s = 0; s < EPL; ++s) g[s] = fmaf(bsum, x[s], g[s]);
     }
-    if (off == nullptr && (flagged || local > cap)) {  // the atomic sums: G, and for items the copies in use
+    if (off == nullptr && (flagged || local > cap) && !(FX && isU)) {  // the atomic sums: G, and for items the copies in use
         const int nrep = isU ? 0 : a.repV;   // copies 1..repV (unused ones are zero)
         float h[EPL];
         gload<EPL>(G, r, a.d, gl, h);
@@ -2391,7 +2489,7 @@ __device__ __forceinline__ void rows_sum(const float* __restrict__ S, int64_t s0
 #ifndef CF_APPLY_NF_PS
 #define CF_APPLY_NF_PS 8   // rows in flight per group in the pos_sort item apply
 #endif
-template <int EPL>
+template <int EPL, bool FX = false>
 __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int gl, int cn, int cp, int o,
                                               int on) {
     // multi-rank item reduce: the summed row goes to GV for the exchange
@@ -2403,7 +2501,7 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
     }
     const int np = cp > 0 ? (o + cp - 1) / kPsortPPB - o / kPsortPPB + 1 : 0;
     const int nn = cn;   // every negative occurrence has its compact slot
-    const int npp = np;  // and every (block, item) partial its row
+    const int npp = np < a.capP ? np : a.capP;
     const float* P0 = a.slotP + ((int64_t)(o / kPsortPPB) + r) * a.d;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g[s] = 0.f;
@@ -2412,7 +2510,55 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
     // NF of them in flight
     const int nt = nn + npp;
     constexpr int NF = CF_APPLY_NF_PS;
-    for (int t0 = 0; t0 < nt; t0 += NF) {
+    if constexpr (FX) {
+        // deterministic: the negatives' rows and the int64 partials summed
+        // exactly in fixed point (the order the atomic ranks gave them is moot)
+        long long t[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) t[s] = 0;
+        for (int t0 = 0; t0 < nn; t0 += NF) {
+            float h[NF][EPL];
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < nn) row_ld<EPL>(a.slotV + ((int64_t)on + t0 + q) * a.d, a.d, gl, 0.f, h[q]);
+#pragma unroll
+            for (int q = 0; q < NF; ++q)
+                if (t0 + q < nn) {
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) t[s] += to_fx(h[q][s]);
+                }
+        }
+        // the partials, NF / 2 int64 rows in flight (a Zipf-head item has
+        // hundreds: one at a time they were a serial chain of load latencies)
+        const long long* P64 = a.slotP64 + ((int64_t)(o / kPsortPPB) + r) * a.d;
+        constexpr int NF2 = NF / 2 > 0 ? NF / 2 : 1;
+        const bool full = CF_VEC_ROWS && a.d == kGL * EPL;
+        for (int t0 = 0; t0 < npp; t0 += NF2) {
+            long long h[NF2][EPL];
+#pragma unroll
+            for (int q = 0; q < NF2; ++q)
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) {
+                    const int e = elem_of<EPL>(s, gl, full);
+                    h[q][s] = (t0 + q < npp && e < a.d) ? P64[(int64_t)(t0 + q) * a.d + e] : 0ll;
+                }
+#pragma unroll
+            for (int q = 0; q < NF2; ++q)
+#pragma unroll
+                for (int s = 0; s < EPL; ++s) t[s] += h[q][s];
+        }
+        if (np > a.capP) {   // the int64 atomic overflow (GV64), re-zeroed
+            long long* row = reinterpret_cast<long long*>(a.GV64 + r * a.d);
+            fx_ld_add<EPL>(row, a.d, gl, t);
+            long long z[EPL];
+#pragma unroll
+            for (int s = 0; s < EPL; ++s) z[s] = 0;
+            fx_st<EPL>(row, a.d, gl, z);
+        }
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] = from_fx(t[s]);
+    }
+    for (int t0 = 0; t0 < (FX ? 0 : nt); t0 += NF) {
         float h[NF][EPL];
 #pragma unroll
         for (int q = 0; q < NF; ++q) {
@@ -2429,6 +2575,13 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) g[s] += h[q][s];
             }
+    }
+    if (!FX && np > a.capP) {   // partials past the positives' slot range: float atomics into GV
+        float h[EPL];
+        gload<EPL>(a.GV, r, a.d, gl, h);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g[s] += h[s];
+        if (!reduce_only) row_zero<EPL>(a.GV + r * a.d, a.d, gl);
     }
     if (reduce_only)
         row_st<EPL>(a.GV + r * (int64_t)a.d, a.d, gl, g);
@@ -2465,7 +2618,7 @@ __device__ __forceinline__ void fold_loss(const ApplyArgs& a) {
     if (threadIdx.x == 0) {
         double tt = 0.0;
         for (int w = 0; w < NWV; ++w) tt += s_red[w];
-        a.loss_acc[0] += tt;
+        a.loss_acc[0] += a.det_fx ? tt / kFxLoss : tt;   // det_fx: an exact integer sum
     }
 }
 
@@ -2484,7 +2637,7 @@ __device__ __forceinline__ void fold_loss(const ApplyArgs& a) {
 //    immutable offP, else the rank-0 negative) -- ballot-compacted and taken
 //    by the wave's four groups four at a time (no LDS, no barrier).
 // ---------------------------------------------------------------------------
-template <int EPL>
+template <int EPL, bool FX>
 __device__ __forceinline__ void apply_ps_item_block(const ApplyArgs& a, int block) {
     const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
     const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
@@ -2492,10 +2645,10 @@ __device__ __forceinline__ void apply_ps_item_block(const ApplyArgs& a, int bloc
     const int2 o0 = a.offPN[r], o1 = a.offPN[r + 1];
     const int cp = o1.x - o0.x, cn = o1.y - o0.y;
     if (cn + cp < 2) return;   // untouched, or seen once (applied by the gradient launch)
-    apply_item_ps<EPL>(a, r, gl, cn, cp, o0.x, o0.y);
+    apply_item_ps<EPL, FX>(a, r, gl, cn, cp, o0.x, o0.y);
 }
 
-template <int EPL>
+template <int EPL, bool FX>
 __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) {
     const int lane = lane_id(), gw = lane >> 4, gl = lane & (kGL - 1);
     const int64_t nUw = !a.count_users ? 0 : a.dense_users ? a.n_users : a.nU;
@@ -2540,10 +2693,10 @@ __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) 
         const int cc = __shfl(c, src, kWave);
         if (!have) continue;   // group-uniform
         if (ru) {
-            apply_row<EPL>(a, rr, true, cc, gl);
+            apply_row<EPL, false, FX>(a, rr, true, cc, gl);
         } else {
             const int2 o0 = a.offPN[rr], o1 = a.offPN[rr + 1];
-            apply_item_ps<EPL>(a, rr, gl, o1.y - o0.y, o1.x - o0.x, o0.x, o0.y);
+            apply_item_ps<EPL, FX>(a, rr, gl, o1.y - o0.y, o1.x - o0.x, o0.x, o0.y);
         }
     }
 }
@@ -2566,17 +2719,17 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 // grid: [0, nbI) dense item blocks, [nbI, nbI + nbW) wave blocks, then (with
 // DRAW) the draw + count blocks of the next step (other buffer set).  PS:
 // pos_sort's item rows (offPN), else apply_rows_item_block
-template <int EPL, bool DRAW, bool PS = true>
+template <int EPL, bool DRAW, bool PS = true, bool FX = false>
 __global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
     const int b = blockIdx.x;
     if (b == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
     if (b < nbI) {
         if constexpr (PS)
-            apply_ps_item_block<EPL>(p, b);
+            apply_ps_item_block<EPL, FX>(p, b);
         else
             apply_rows_item_block<EPL>(p, b);
     } else if (b < nbI + nbW) {
-        apply_ps_wave<EPL>(p, (int64_t)(b - nbI) * kWavesPerBlock + (threadIdx.x >> 6));
+        apply_ps_wave<EPL, FX>(p, (int64_t)(b - nbI) * kWavesPerBlock + (threadIdx.x >> 6));
     } else if constexpr (DRAW) {
         prep_any<BPR>(nx, b - nbI - nbW);
     }
@@ -3157,6 +3310,15 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
         if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
             if (np > 0) return hipErrorInvalidValue;
             const dim3 sgrid(ng);
+            if (a.det_fx) {   // deterministic: fixed-point partials and loss
+                switch (epl_for(a.d)) {
+                    case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT, true>), sgrid, block, 0, s, a); break;
+                    case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT, true>), sgrid, block, 0, s, a); break;
+                    case 4: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true>), sgrid, block, 0, s, a); break;
+                    default: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, true>), sgrid, block, 0, s, a); break;
+                }
+                return hipGetLastError();
+            }
             switch (epl_for(a.d)) {
                 case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT>), sgrid, block, 0, s, a); break;
                 case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT>), sgrid, block, 0, s, a); break;
@@ -3261,9 +3423,10 @@ static hipError_t launch_apply_h(const ApplyArgs& a, hipStream_t s) {
 }
 
 // the pos_sort apply (+ the next step's draw when nx is given); PS false: the
-// dense item rows of the slot-row / record path (apply_rows_item_block)
-template <bool PS = true>
-static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
+// dense item rows of the slot-row / record path (apply_rows_item_block); FX:
+// the deterministic pos_sort path's fixed-point sums (ApplyArgs::det_fx)
+template <bool PS = true, bool FX = false>
+static hipError_t launch_apply_ps_t(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
     const int64_t nUw = !p.count_users ? 0 : p.dense_users ? p.n_users : p.nU;
     const int64_t nVw = (p.count_items && !p.dense_items) ? p.nV : 0;
     const int64_t nbI64 = (p.count_items && p.dense_items) ? (p.n_items + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
@@ -3275,20 +3438,28 @@ static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStr
     const StepArgs n = nx ? *nx : StepArgs{};
     if (np > 0) {
         switch (epl_for(p.d)) {
-            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, true, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
         }
     } else {
         switch (epl_for(p.d)) {
-            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, false, PS>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            default: hipLaunchKernelGGL((apply_ps_kernel<8, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
         }
     }
     return hipGetLastError();
+}
+
+template <bool PS = true>
+static hipError_t launch_apply_ps(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
+    if constexpr (PS) {
+        if (p.det_fx) return launch_apply_ps_t<true, true>(p, nx, s);
+    }
+    return launch_apply_ps_t<PS, false>(p, nx, s);
 }
 
 // the slot-row / record path's dense item apply applies (the engine sets

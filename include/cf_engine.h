@@ -450,7 +450,15 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                batch order, no float atomics anywhere (the GBPR group
  *                exchange is excluded); 0 = the fast path (default), whose
  *                rank order -- and so the last bits of duplicate sums --
- *                follows the order the count atomics land.
+ *                follows the order the count atomics land.  Where pos_sort
+ *                is active (round 3) the mode keeps the fast path's launches
+ *                and takes every sum of gradient rows in 64-bit fixed point
+ *                (2^-32 units; int64 partial rows and int64 atomics), which
+ *                is exact in any order, so no sort runs.
+ *   "pair_prefetch" 1 = the pos_sort gradient launch also fetches the next
+ *                step's shuffled pair records for its draw (cf_train_steps);
+ *                measured slower at cfg2 (gradient launch +20 us, draw -2
+ *                us), so 0 (default).
  *   "pos_sort"   1 = the gradient launch visits the batch's pairs in
  *                positive-item order (a counting sort by the draw's positive
  *                counts, two short launches before it), so the pairs of one
@@ -459,16 +467,16 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                of one slot row (or float atomics) per occurrence; the apply
  *                adds the partials to the negatives' slot rows.  BPR / AMF /
  *                CML on the phased kernel (W in {1, 5}, d <= 128), not with
- *                deterministic, item_slots 1, hot_replicas > 1, pipeline 2 or
+ *                item_slots 1, hot_replicas > 1, pipeline 2 or
  *                a dense item apply other than item_reduce 1 (the option is
  *                ignored there; with item_reduce 1 the multi-rank item reduce
  *                sums the partials into the bound gradient).  Same
  *                results up to fp32 summation order.  0 = off; 2 = auto
  *                (default): on for batches of >= 2^18 pairs (cfg2: 7 %
  *                faster steps at 2^19, 3.5 % at 2^18, even at 2^17).
- *   "slot_max_pos" accepted for compatibility, no effect since round 3:
- *                every (gradient block, positive item) partial has its own
- *                row (block + item), so no partial adds with float atomics.
+ *   "slot_max_pos" positive partial rows per item row under pos_sort (default
+ *                8; later partials of a hot item add with float atomics --
+ *                int64 atomics in deterministic mode).
  *   "item_reduce" dense_item_apply engines (the multi-rank step): 1 =
  *                item occurrences are counted like user ones, a row seen
  *                once stores its gradient row into the bound buffer, a

@@ -36,13 +36,20 @@ CML_TRAJ = dict(rtol=5e-5, atol=3e-6)
 ENS_HOT = dict(rtol=2e-3, atol=1e-4)
 
 
-def assert_close(got, ref, what, rtol=RTOL, atol=ATOL):
-    """Elementwise |got - ref| <= atol + rtol |ref| over the whole array."""
+def assert_close(got, ref, what, rtol=RTOL, atol=ATOL, ref32=None):
+    """Elementwise |got - ref| <= atol + rtol |ref| over the whole array.
+    With ref32 (the same oracle trajectory run in float32, the arithmetic
+    width of TF1's CPU path) each element may also deviate by 3x the fp32
+    oracle's own deviation from float64: a row that sums hundreds of
+    cancelling gradient rows in fp32 (a Zipf-head item) moves by more than
+    1e-5 relative in ANY fp32 summation order."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     assert got.shape == ref.shape, (what, got.shape, ref.shape)
     err = np.abs(got - ref)
     bound = atol + rtol * np.abs(ref)
+    if ref32 is not None:
+        bound = bound + 3.0 * np.abs(np.asarray(ref32, np.float64) - ref)
     bad = err > bound
     worst = float(np.max(err / bound)) if err.size else 0.0
     if bad.any():

@@ -1,16 +1,18 @@
 """Deterministic mode on the positive-sorted path (round 3).
 
-With "deterministic" 1 and pos_sort active, the draw's atomic ranks are
-replaced by ranks from a stable sort of the batch's row ids -- a positive
-ranked among its item's positives, a negative among its item's negatives,
-a user among its user's occurrences, all in batch order -- so psort's
-counting sort places every pair at a fixed position, the gradient blocks
-sum the same runs in LDS, every (block, item) partial has its own row
-(block + item, no float atomics), negatives and duplicated users store in
-compact slots, and the apply sums them in a fixed order.  Two runs from the
-same state must be BITWISE identical (TF1's CPU UnsortedSegmentSum behind
-AdagradOptimizer is deterministic, bprmf.py:83-88), and the result must
-match the float64 oracle elementwise (|gpu - ref| <= 1e-6 + 1e-5 |ref|).
+With "deterministic" 1 and pos_sort active, a step runs the fast path's own
+launches (draw with its atomic ranks, psort, grad_sort_kernel, the pos_sort
+apply) and takes every sum of gradient rows in 64-bit fixed point: integer
+adds are associative, so the sums do not depend on the order the atomic
+ranks gave the occurrences or on which pairs share a gradient block.  The
+positive partials are int64 rows (past the first 8 of an item: int64
+atomics), duplicated users past their slot cap add with int64 atomics,
+negatives' and users' slot rows are converted as they are summed, and the
+per-pair losses add as integers.  Two runs from the same
+state must be BITWISE identical (TF1's CPU UnsortedSegmentSum behind
+AdagradOptimizer is deterministic, bprmf.py:83-88), and the result must match
+the float64 oracle elementwise (|gpu - ref| <= 1e-6 + 1e-5 |ref|, widened by
+the fp32 oracle's own deviation where a Zipf-head item sums ~1,000 rows).
 """
 import numpy as np
 import pytest
@@ -42,12 +44,14 @@ def skewed_graph():
     return synth_graph(40_000, 4_000, 30.0, 0.8, 20261017, n_threads=8)
 
 
-def _engine(model, graph, d, W, det, seed=17):
+def _engine(model, graph, d, W, det, seed=17, slot_max=0):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     ip, ix = graph
     e = Engine(model, len(ip) - 1, 4_000, d, n_neg=W, seed=seed, **HP[model])
     e.set_option("deterministic", 1 if det else 0)
     e.set_option("pos_sort", 1)
+    if slot_max:   # users past this many occurrences take the (int64) atomics
+        e.set_option("slot_max_user", slot_max)
     e.set_interactions(ip, ix)
     e.init_params(0.0, 0.1, truncated=True, seed=3)
     if model == "amf":
@@ -55,8 +59,8 @@ def _engine(model, graph, d, W, det, seed=17):
     return e
 
 
-def _run(model, graph, d, W, B, steps, det):
-    e = _engine(model, graph, d, W, det)
+def _run(model, graph, d, W, B, steps, det, slot_max=0):
+    e = _engine(model, graph, d, W, det, slot_max=slot_max)
     _, path = e.step_path(B)
     assert path["pos_sort"] and path["deterministic"] == bool(det), path
     e.profile(True)
@@ -68,50 +72,56 @@ def _run(model, graph, d, W, B, steps, det):
     return loss, out
 
 
-@pytest.mark.parametrize("model,d,W", [("bpr", 64, 1), ("bpr", 32, 5), ("amf", 32, 5)],
-                         ids=["bpr-w1", "bpr-w5", "amf-adv-w5"])
-def test_det_pos_sort_two_runs_bitwise_identical(skewed_graph, model, d, W):
-    a = _run(model, skewed_graph, d, W, 16384, 6, det=True)
-    b = _run(model, skewed_graph, d, W, 16384, 6, det=True)
+@pytest.mark.parametrize("model,d,W,slot_max", [("bpr", 64, 1, 0), ("bpr", 64, 1, 2), ("bpr", 32, 5, 0),
+                                                  ("amf", 32, 5, 0)],
+                         ids=["bpr-w1", "bpr-w1-user-atomics", "bpr-w5", "amf-adv-w5"])
+def test_det_pos_sort_two_runs_bitwise_identical(skewed_graph, model, d, W, slot_max):
+    a = _run(model, skewed_graph, d, W, 16384, 6, det=True, slot_max=slot_max)
+    b = _run(model, skewed_graph, d, W, 16384, 6, det=True, slot_max=slot_max)
     assert a[0] == b[0]
     for t in TABLES:
         assert np.array_equal(a[1][t], b[1][t]), t
     # the fast pos_sort path trains the same model up to fp32 summation order
-    c = _run(model, skewed_graph, d, W, 16384, 6, det=False)
+    c = _run(model, skewed_graph, d, W, 16384, 6, det=False, slot_max=slot_max)
     assert abs(c[0] - a[0]) <= 1e-5 * abs(a[0])
     for t in TABLES:
         assert_close(c[1][t], a[1][t].astype(np.float64), t, rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("W", [1, 5])
-def test_det_pos_sort_matches_oracle(skewed_graph, W):
+@pytest.mark.parametrize("W,slot_max", [(1, 0), (5, 0), (1, 2)], ids=["w1", "w5", "w1-user-atomics"])
+def test_det_pos_sort_matches_oracle(skewed_graph, W, slot_max):
     """Host-fed deterministic pos_sort steps on device-drawn batches whose Zipf
-    head spans many 16-pair gradient blocks, against the float64 oracle."""
-    e = _engine("bpr", skewed_graph, 32, W, det=True, seed=23)
+    head spans many 16-pair gradient blocks, against the float64 oracle
+    (slot_max 2: users seen more than twice add their rows with int64 atomics)."""
+    e = _engine("bpr", skewed_graph, 32, W, det=True, seed=23, slot_max=slot_max)
     B, ni = 8192, 4_000
     T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
     T32 = {t: v.astype(np.float32) for t, v in T.items()}
-    hot = 0
+    hot = hot_user = 0
     e.profile(True)
     for _ in range(4):
         pairs, negs, _ = e.sample(B)
         hot = max(hot, int(np.bincount(pairs[:, 1], minlength=ni).max()))
+        hot_user = max(hot_user, int(np.bincount(pairs[:, 0]).max()))
         lg = e.step(pairs, negs)
         lo = O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.02)
         O.bpr_step(T32["user"], T32["item"], T32["acc_user"], T32["acc_item"], pairs, negs, 0.02)
         assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
     e.profile(False)
     assert e.profile_read("psort")[1] == 4
-    assert hot >= 16 * 8   # a positive run over more than the old 8-partial cap
+    assert hot >= 16 * 8   # a positive run past the 8 partial rows: int64 atomics (GV64)
+    if slot_max:
+        assert hot_user > slot_max, hot_user
     for t in TABLES:
         assert_close(e.get_table(t), T[t], t, ref32=T32[t])
     e.close()
 
 
-def test_fast_pos_sort_uncapped_partials_match_oracle(skewed_graph):
+def test_fast_pos_sort_hot_partials_match_oracle(skewed_graph):
     """The fast path with a Zipf-head item whose run spans dozens of
-    gradient blocks: every (block, item) partial has its own row (no float
-    atomics since round 3); host-fed steps against the float64 oracle."""
+    gradient blocks: its first capP (8) partials in their compact rows
+    (slotP[block + item]), the rest on float atomics; host-fed steps against
+    the float64 oracle."""
     e = _engine("bpr", skewed_graph, 64, 1, det=False, seed=29)
     B, ni = 32768, 4_000
     T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
@@ -124,7 +134,7 @@ def test_fast_pos_sort_uncapped_partials_match_oracle(skewed_graph):
         lo = O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.02)
         O.bpr_step(T32["user"], T32["item"], T32["acc_user"], T32["acc_item"], pairs, negs, 0.02)
         assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
-    assert hot >= 16 * 32   # one run over >= 32 blocks (the round-2 cap was 8 partials)
+    assert hot >= 16 * 32   # one run over >= 32 blocks, far past the 8 partial rows
     for t in TABLES:
         assert_close(e.get_table(t), T[t], t, ref32=T32[t])
     e.close()

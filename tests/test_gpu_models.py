@@ -8,7 +8,7 @@
 * the same drivers' device-sampled path trains (metrics far above random).
 * cfg2 at full size (1M users x 100K items, d=64): one step at B=65,536 on a
   device-drawn batch, and two pipelined steps at the bench batch B=2^19
-  (pos_sort, hot positives spanning > 8 gradient blocks) against the float64 oracle,
+  (pos_sort, partials past capP on atomics) against the float64 oracle,
   elementwise |gpu - oracle| <= 1e-6 + 1e-5 |oracle| over the whole tables.
 """
 import numpy as np
@@ -174,8 +174,7 @@ def test_cfg2_bench_batch_pos_sort_matches_oracle(cfg2_graph):
     """The benched cfg2 instantiation itself: B = 2^19 pairs per step with
     pos_sort auto (on), i.e. psort + grad_sort_kernel<BPR, d 64, W 1> + the
     pos_sort apply fused with the next draw (apply_ps_kernel), where the
-    Zipf-head positives' runs span many more gradient blocks than the round-2
-    cap of 8 partials (each has its own partial row since round 3).  Three
+    Zipf-head positives' partials overflow capP into float atomics.  Three
     pipelined steps move off the initial state; then two more pipelined
     steps (cf_train_steps: the first one's apply launch draws the second's
     batch) are replayed by the float64 oracle on the same drawn batches and
@@ -197,7 +196,7 @@ def test_cfg2_bench_batch_pos_sort_matches_oracle(cfg2_graph):
     loss = e.train_steps(B, K)
     e.profile(False)
     assert e.profile_read("psort")[1] == 3 + K, "pos_sort did not run at the bench batch"
-    # the drawn batches' hot positives span > 8 blocks (the round-2 cap):
+    # the drawn batches overflow the positives' partial slots (capP = 8):
     # partial k of item i covers sorted positions of block offP[i] / 16 + k
     for pairs, _ in batches:
         cnt = np.bincount(pairs[:, 1], minlength=ni)

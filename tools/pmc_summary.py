@@ -21,8 +21,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SHORT = {"grad_fast_kernel": "step", "grad_sort_kernel": "step", "grad_lds_kernel": "step", "grad_kernel": "step",
          "apply_prep_kernel": "apply_prep", "fused_topk_pipe_kernel": "fused_topk",
-         "apply_ps_kernel<1, true>": "apply_prep", "apply_ps_kernel<2, true>": "apply_prep",
-         "apply_ps_kernel<4, true>": "apply_prep", "apply_ps_kernel<8, true>": "apply_prep",
+         "apply_ps_kernel<1, true": "apply_prep", "apply_ps_kernel<2, true": "apply_prep",
+         "apply_ps_kernel<4, true": "apply_prep", "apply_ps_kernel<8, true": "apply_prep",
          "apply_ps_kernel": "apply", "psort_tile_sum_kernel": "psort_scan", "psort_tile_scan_kernel": "psort_scan",
          "prep_kernel": "sample", "slot_kernel": "slot", "apply_kernel": "apply",
          "apply_dense_kernel": "apply_dense", "clip_full_kernel": "clip",
