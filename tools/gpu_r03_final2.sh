@@ -17,11 +17,5 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -2 $OUT/smoke.log
 timeout -k 10 500 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { echo "default bench failed"; tail -20 $OUT/bench_default.err; exit 1; }
 python -c "import json; d=json.loads(open('$OUT/bench_default.json').read().strip().splitlines()[-1]); print('default', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['pmc_key'], d.get('cpu_baseline'), d.get('ndcg10_vs_ref'))"
-for c in cfg2 cfg3 cfg4 cfg5; do
-  bash tools/gpu_profile_cfg.sh r03g_$c --config $c || exit 1
-done
-CF_DIST_BACKEND=gloo CF_SHARE_DEVICE=1 timeout -k 10 400 python bench.py --gpus 2 --steps 10 --warmup 3 \
-  --no-cpu-baseline --no-ndcg --secondary-batch 0 > $OUT/dist2_gloo.json 2> $OUT/dist2_gloo.err || { echo "gloo rehearsal failed"; tail -20 $OUT/dist2_gloo.err; exit 1; }
-python -c "import json; d=json.loads(open('$OUT/dist2_gloo.json').read().strip().splitlines()[-1]); r=d['roofline']; print('dist2', d['n_gpus'], d['value'], 'frac', r['frac'], 'traffic', r['traffic'], r['pmc_key'])"
 timeout -k 10 300 python bench.py --steps 100 --warmup 20 --no-cpu-baseline --no-ndcg --secondary-batch 0 --deterministic 1 > $OUT/cfg2_det.json 2> $OUT/cfg2_det.err || { echo "det bench failed"; tail -20 $OUT/cfg2_det.err; exit 1; }
 python -c "import json; d=json.loads(open('$OUT/cfg2_det.json').read().strip().splitlines()[-1]); print('det', d['value'], d['ms_per_step'])"
