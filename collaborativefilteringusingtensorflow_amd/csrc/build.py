@@ -18,9 +18,12 @@ ROOT = os.path.dirname(PKG)
 VARIANT = os.environ.get("CF_BUILD_VARIANT", "")
 OUT = os.path.join(PKG, "build", "variants", VARIANT) if VARIANT else os.path.join(PKG, "build")
 LIB = os.path.join(OUT, "libcf_engine.so")
-SOURCES = ["cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp", "cf_ingest.cpp",
+# cf_kernels.hip and the per-model gradient units share cf_kernels_impl.h; the
+# split lets the pool below compile the heavy instantiations in parallel
+SOURCES = ["cf_grad_bpr.hip", "cf_grad_amf.hip", "cf_grad_cml.hip", "cf_grad_gbpr.hip", "cf_grad_plr.hip",
+           "cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp", "cf_ingest.cpp",
            "cf_mt_sampler.cpp", "cf_ensemble.hip", "cf_det.hip"]
-HEADERS = ["cf_kernels.h", "cf_device.h", os.path.join(ROOT, "include", "cf_engine.h")]
+HEADERS = ["cf_kernels.h", "cf_device.h", "cf_kernels_impl.h", os.path.join(ROOT, "include", "cf_engine.h")]
 ARCH = os.environ.get("CF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
@@ -54,7 +57,7 @@ def build(force=False, verbose=True):
         for f in os.listdir(OUT):
             if f.endswith(".o") or f.endswith(".so"):
                 os.remove(os.path.join(OUT, f))
-    with cf.ThreadPoolExecutor(max_workers=4) as ex:
+    with cf.ThreadPoolExecutor(max_workers=int(os.environ.get("CF_BUILD_JOBS", "8"))) as ex:
         objs = list(ex.map(_compile, SOURCES))
     if _newer(LIB, objs):
         subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH, "-o", LIB] + objs

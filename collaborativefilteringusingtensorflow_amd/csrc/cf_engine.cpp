@@ -145,6 +145,8 @@ struct cf_engine {
     float* coefs = nullptr;   // [B, 2] CPLR tuple coefficients (cf_step_plr)
     int coefs_cap = 0;
     double* h_loss = nullptr; // pinned
+    int* fx_bad = nullptr;    // deterministic fixed-point range flag (StepArgs::fx_bad)
+    int* h_fx_bad = nullptr;  // pinned
     int32_t* h_stage = nullptr;
     size_t stage_cap = 0;
     int tuple_stride = 0;            // cf_step_plr: ids read from tuples [B, width]
@@ -359,7 +361,15 @@ int ensure_slots(cf_engine* e) {
     return CF_OK;
 }
 
-int ensure_det(cf_engine* e, int B) {
+// the deterministic step at batch size B takes the fixed-point pos_sort form
+// (StepArgs::det_fx), which needs none of the sort-based form's buffers
+bool det_fx_path(const cf_engine* e, int B) {
+    return e->det && psort_possible(e) && !e->cfg.dense_item_apply && psort_active(e, B);
+}
+
+// B: the buffers' capacity (>= the step's batch); B_step: the step's batch,
+// which decides the form
+int ensure_det(cf_engine* e, int B, int B_step) {
     const cf_config& c = e->cfg;
     if (psort_possible(e) && !c.dense_item_apply) {   // the fixed-point pos_sort form (StepArgs::det_fx)
         if (B > e->fx_cap) {
@@ -377,6 +387,11 @@ int ensure_det(cf_engine* e, int B) {
             CF_TRY(dalloc(&e->GV64, (size_t)c.n_items * c.n_factors));
             CF_HIP(hipMemsetAsync(e->GV64, 0, (size_t)c.n_items * c.n_factors * 8, e->stream));
         }
+        if (!e->fx_bad) {
+            CF_TRY(dalloc(&e->fx_bad, 1));
+            CF_HIP(hipMemsetAsync(e->fx_bad, 0, sizeof(int), e->stream));
+        }
+        if (det_fx_path(e, B_step)) return CF_OK;   // the sort-based buffers are not used
     }
     const int64_t nU = (int64_t)B * users_per_pair(c), nV = (int64_t)B * items_per_pair(c);
     const int64_t n = nU + nV;
@@ -430,7 +445,7 @@ int ensure_order(cf_engine* e, int B);
 int ensure_batch(cf_engine* e, int B) {
     CF_TRY(ensure_slots(e));
     CF_TRY(ensure_order(e, B));
-    if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap)));
+    if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap), B));
     CF_TRY(ensure_stash(e, std::max(B, e->Bcap)));
     if (B <= e->Bcap) return CF_OK;
     CF_HIP(hipStreamSynchronize(e->stream));
@@ -553,6 +568,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
             a.slotP64 = e->slotP64;
             a.GU64 = e->GU64;
             a.GV64 = e->GV64;
+            a.fx_bad = e->fx_bad;
         }
     }
     a.shard_u0 = e->shard_u0;
@@ -704,9 +720,21 @@ int stage_host_batch(cf_engine* e, const int32_t* pairs, const int32_t* negs,
 
 // Stage / position the batch of one step in buffer set k and launch its draw
 // + count (prep) on stream ps.  Returns the step's arguments in *a.
+// deterministic mode on the positive-sorted path must take the fixed-point
+// form: its buffers not being ready is an engine bug, not a reason to run the
+// float-atomic path while cf_step_path reports DETERMINISTIC
+int check_det_args(cf_engine* e, const StepArgs& a) {
+    if (e->det && a.cntP != nullptr && !a.det_fx)
+        return fail(CF_ESTATE, "deterministic pos_sort step without its fixed-point buffers");
+    if (e->det && a.cntP == nullptr && a.offU == nullptr && !e->cfg.dense_item_apply)
+        return fail(CF_ESTATE, "deterministic step without its sort-based buffers");
+    return CF_OK;
+}
+
 int begin_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
                const int32_t* groups, int k, hipStream_t ps, StepArgs* a) {
     *a = base_step_args(e, B, k);
+    CF_TRY(check_det_args(e, *a));
     if (pairs) {
         CF_TRY(stage_host_batch(e, pairs, negs, groups, B, k, ps));
         a->sample = 0;
@@ -729,6 +757,7 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.slotP64 = a.slotP64;
     p.GU64 = a.GU64;
     p.GV64 = a.GV64;
+    p.fx_bad = a.fx_bad;
     p.d = c.n_factors;
     p.lr = c.lr;
     p.clip_norm = c.clip_norm;
@@ -939,6 +968,7 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
         const bool more = s + 1 < n;
         if (more) {
             nx = base_step_args(e, B, k ^ 1);
+            CF_TRY(check_det_args(e, nx));
             CF_TRY(sampler_args(e, B, &nx));
             if (pf) {
                 a.pf_out = e->pf_recs[k ^ 1];
@@ -977,6 +1007,21 @@ int run_items_dense(cf_engine* e) {
         e->need_clip_V = false;
     }
     return CF_OK;
+}
+
+// deterministic mode: a fixed-point term or sum out of range (to_fx) during
+// the calls since the last check fails the call -- the tables then hold NaN
+// where a sum overflowed and are not a valid step (the fp32 path would show
+// inf / NaN; the int64 sums would otherwise wrap silently)
+int check_fx(cf_engine* e) {
+    if (!e->fx_bad) return CF_OK;
+    CF_HIP(hipMemcpyAsync(e->h_fx_bad, e->fx_bad, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    CF_HIP(hipStreamSynchronize(e->stream));
+    if (*e->h_fx_bad == 0) return CF_OK;
+    *e->h_fx_bad = 0;
+    CF_HIP(hipMemsetAsync(e->fx_bad, 0, sizeof(int), e->stream));
+    return fail(CF_ENUMERIC, "deterministic mode: a gradient term was not finite or outside the "
+                             "fixed-point range (|g| >= 2^20, or a row sum >= 2^30); the step is invalid");
 }
 
 int read_loss(cf_engine* e, int slot, double* out) {
@@ -1212,6 +1257,9 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     e->shard_u1 = c.n_users;
     if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
+    if (hipHostMalloc((void**)&e->h_fx_bad, sizeof(int), hipHostMallocDefault) != hipSuccess)
+        return bail(fail(CF_ENOMEM, "pinned allocation failed"));
+    *e->h_fx_bad = 0;
     hipStream_t s = e->stream;
     if (hipMemsetAsync(e->GU, 0, ud * 4, s) != hipSuccess ||
         hipMemsetAsync(e->GV, 0, id * 4, s) != hipSuccess ||
@@ -1252,7 +1300,7 @@ int cf_destroy(cf_engine* e) {
     for (int t = 0; t < 6; ++t)   // bound tables belong to the caller
         if (e->own_tab[t]) *table_slot(e, t) = e->own_tab[t];
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
-    dfree(e->pf_recs[0]); dfree(e->pf_recs[1]); dfree(e->slotP64); dfree(e->GU64); dfree(e->GV64);
+    dfree(e->pf_recs[0]); dfree(e->pf_recs[1]); dfree(e->slotP64); dfree(e->GU64); dfree(e->GV64); dfree(e->fx_bad);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
@@ -1273,6 +1321,7 @@ int cf_destroy(cf_engine* e) {
     if (e->det_tmp) (void)hipFree(e->det_tmp);
     if (e->h_xcounts) (void)hipHostFree(e->h_xcounts);
     if (e->h_loss) (void)hipHostFree(e->h_loss);
+    if (e->h_fx_bad) (void)hipHostFree(e->h_fx_bad);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
     if (e->h_bad) (void)hipHostFree(e->h_bad);
     dfree(e->d_bad);
@@ -1431,6 +1480,7 @@ int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32
     CF_TRY(run_step(e, B, pairs, negs, groups, acc));
     if (e->cfg.dense_item_apply) CF_TRY(run_items_dense(e));
     if (loss_out) CF_TRY(read_loss(e, 1, loss_out));
+    if (e->det) CF_TRY(check_fx(e));
     return CF_OK;
 }
 
@@ -1482,6 +1532,7 @@ int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_ou
         for (int s = 0; s < n_steps; ++s) CF_TRY(run_step(e, B, nullptr, nullptr, nullptr, acc));
     }
     if (loss_sum_out) CF_TRY(read_loss(e, 1, loss_sum_out));
+    if (e->det) CF_TRY(check_fx(e));
     return CF_OK;
 }
 
@@ -2275,7 +2326,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         e->det_cap = 0;              // deterministic buffers likewise
         if (e->Bcap > 0) {
             CF_TRY(ensure_slots(e));
-            if (e->det) CF_TRY(ensure_det(e, e->Bcap));
+            if (e->det) CF_TRY(ensure_det(e, e->Bcap, e->Bcap));
             CF_TRY(ensure_stash(e, e->Bcap));
         }
         return CF_OK;
@@ -2286,7 +2337,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
         e->det = (int)value;
-        if (e->det && e->Bcap > 0) CF_TRY(ensure_det(e, e->Bcap));
+        if (e->det && e->Bcap > 0) CF_TRY(ensure_det(e, e->Bcap, e->Bcap));
         return CF_OK;
     }
     if (n == "grad_path") {

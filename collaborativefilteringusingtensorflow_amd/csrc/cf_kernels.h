@@ -89,6 +89,7 @@ struct StepArgs {
     long long* __restrict__ slotP64;        // [B / kPsortPPB + 1 + n_items, d] (as slotP)
     unsigned long long* __restrict__ GU64;  // [n_users, d], zero between steps
     unsigned long long* __restrict__ GV64;  // [n_items, d]: positive partials past capP, zero between steps
+    int* __restrict__ fx_bad;               // set when a term / sum leaves the fixed-point range (to_fx)
     int lane_draw;                          // 1: one lane per pair (neg_check 2, with the set)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -180,6 +181,9 @@ constexpr int kPsortPPB = kGroupsPerBlock;
 constexpr float kFxOne = 4294967296.f;
 constexpr double kFxInv = 1.0 / 4294967296.0;
 constexpr double kFxLoss = 16777216.0;
+// the guarded range (to_fx): terms |x| < 2^20, sums |x| < 2^30 (in units: 2^62)
+constexpr float kFxTermMax = 1048576.f;
+constexpr long long kFxSumMax = 1ll << 62;
 
 // A pos_sort record carries every occurrence's resolved destination --
 // psort_scatter reads the batch's final counts and offsets, so the gradient
@@ -209,6 +213,7 @@ struct ApplyArgs {
     const long long* __restrict__ slotP64;
     unsigned long long* __restrict__ GU64;
     unsigned long long* __restrict__ GV64;
+    int* __restrict__ fx_bad;                 // StepArgs::fx_bad
     int d;
     float lr;
     float clip_norm;

@@ -114,12 +114,14 @@ class ReduceScatterItems(object):
     draw_with_apply = False  # the next draw runs beside the all-gather
 
     def __init__(self, grad, grad_slice, tables, chunk, rank, grad_bias=None, bias_slice=None,
-                 state=(), group=None):
+                 state=(), group=None, world=None):
         self.grad, self.grad_slice = grad, grad_slice
         self.grad_bias, self.bias_slice = grad_bias, bias_slice
         self.tables = list(tables)
         self.state = list(state)
         self.chunk, self.rank = int(chunk), int(rank)
+        # world 1 owns every row: nothing goes stale (None: unknown, assume > 1)
+        self.world = world
         self.row0, self.row1 = self.rank * self.chunk, (self.rank + 1) * self.chunk
         self.group = group
         # accumulators of rows other ranks own are stale after an owner
@@ -159,7 +161,7 @@ class ReduceScatterItems(object):
         # step, then the owner's Adagrad on its rows
         be.clear_item_grad()
         be.step_items_range(self.row0, self.row1, self.grad_slice, self.bias_slice)
-        self.stale = True
+        self.stale = self.world != 1
 
     def gather(self, dist, async_op):
         return _Works([self._ag(dist, t, w, async_op) for t, w in self.tables])
@@ -269,7 +271,8 @@ def _bind_rs_items(engine, n_items, d, with_bias, device, group=None):
         tables.append((b, 1))
         state.append((Ab, 1))
     items = ReduceScatterItems(grad, z(chunk * d), tables, chunk, rank, grad_bias=gb,
-                               bias_slice=z(chunk) if with_bias else None, state=state, group=group)
+                               bias_slice=z(chunk) if with_bias else None, state=state, group=group,
+                               world=world)
     items._keep = (V, AV) + ((b, Ab) if with_bias else ())
     engine._stale_guard = items   # get_table refuses stale accumulators until sync_state
     return items
@@ -408,8 +411,12 @@ class GroupExchangeStep(object):
         x = self.items
         # one rank has no remote members to overlap with (the split only adds
         # a launch and an apply there); a rank with none to fetch (ns == 0)
-        # runs its whole gradient at once beside the rows it serves
-        if not (self.split and self.world > 1 and hasattr(be, "xchg_grad_part")):
+        # runs its whole gradient at once beside the rows it serves.
+        # split == "force" takes the split step (both gradient parts, the
+        # asynchronous collectives) at any world size -- the one-rank RCCL
+        # test of its stream ordering (tests/test_gpu_group_exchange.py)
+        force = self.split == "force"
+        if not (self.split and (self.world > 1 or force) and hasattr(be, "xchg_grad_part")):
             _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group)
             be.xchg_grad()
             _a2a(dist, be.serve_grads[:nr], be.grads[:ns], rc, sc, self.group)
@@ -424,7 +431,7 @@ class GroupExchangeStep(object):
         # them (exact sum-before-update, gbprmf.py:101-106)
         overlap = x.overlap(dist)
         w = _a2a(dist, be.rows[:ns], be.serve_rows[:nr], sc, rc, self.group, async_op=overlap)
-        if ns > 0:
+        if ns > 0 or force:
             be.xchg_grad_part(1)
             if w is not None:
                 w.wait()

@@ -61,9 +61,13 @@ enum cf_status {
     CF_EHIP = -2,     /* HIP runtime error (message has the HIP text)  */
     CF_ESTATE = -3,   /* call out of order (e.g. no interactions set)  */
     CF_ENOMEM = -4,   /* device or host allocation failed              */
-    CF_EAGAIN = -5    /* cf_xchg_adopt: no batch of that size drawn ahead
+    CF_EAGAIN = -5,   /* cf_xchg_adopt: no batch of that size drawn ahead
                          (none drawn, dropped, or drawn at another B and
                          now discarded): draw one (cf_xchg_draw) and retry */
+    CF_ENUMERIC = -6  /* deterministic mode: a gradient term was not finite
+                         or left the fixed-point range (|g| >= 2^20, a row
+                         sum >= 2^30); the step is invalid (the fp32 path
+                         would carry the inf / NaN into the tables)       */
 };
 
 /* parameter tables addressable by cf_set_table / cf_get_table */

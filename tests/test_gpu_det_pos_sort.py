@@ -11,13 +11,16 @@ negatives' and users' slot rows are converted as they are summed, and the
 per-pair losses add as integers.  Two runs from the same
 state must be BITWISE identical (TF1's CPU UnsortedSegmentSum behind
 AdagradOptimizer is deterministic, bprmf.py:83-88), and the result must match
-the float64 oracle elementwise (|gpu - ref| <= 1e-6 + 1e-5 |ref|, widened by
-the fp32 oracle's own deviation where a Zipf-head item sums ~1,000 rows).
+the float64 oracle: every host-fed step from the engine's own pre-step tables
+within the a-priori fp32 bound of oracle/fp32_bound.py (which covers the
+2^-32 fixed-point terms), and the trajectory within 1e-6 + 1e-5 |ref| plus
+the same bound carried over the steps (a Zipf-head item sums ~1,000 rows).
 """
 import numpy as np
 import pytest
 
-from oracle import cf_oracle as O
+from conftest import LocalStepCheck
+from conftest import assert_close as _assert_close
 
 pytestmark = pytest.mark.gpu
 
@@ -25,17 +28,33 @@ TABLES = ("user", "item", "acc_user", "acc_item")
 HP = {"bpr": dict(reg=0.02), "amf": dict(reg=0.05, reg_adv=1.0)}
 
 
-def assert_close(got, ref, name, rtol=1e-5, atol=1e-6, ref32=None):
-    """Elementwise |got - ref| <= atol + rtol |ref|; with ref32 (the same
-    oracle run in float32, the arithmetic width of TF1's CPU path) each
-    element may also deviate by twice the fp32 oracle's own deviation --
-    a Zipf-head item here sums ~1,000 gradient rows per step in fp32."""
-    got = np.asarray(got, dtype=np.float64)
-    bound = atol + rtol * np.abs(ref)
-    if ref32 is not None:
-        bound = bound + 2.0 * np.abs(ref32.astype(np.float64) - ref)
-    err = np.abs(got - ref) - bound
-    assert err.max() <= 0.0, (name, float(np.abs(got - ref).max()))
+def assert_close(got, ref, name, rtol=1e-5, atol=1e-6, bound=None):
+    """Elementwise |got - ref| <= atol + rtol |ref| (+ the carried a-priori
+    fp32 bound where given)."""
+    return _assert_close(got, ref, name, rtol=rtol, atol=atol, bound=bound)
+
+
+def _host_fed(e, B, n, ni, reg=0.02):
+    """n host-fed steps on device-drawn batches: each step checked locally
+    (conftest.LocalStepCheck), the trajectory against the float64 oracle
+    within the strict band plus the carried a-priori bound."""
+    from oracle import fp32_bound as FB
+    T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
+    E = FB.zero_bounds(T["user"], T["item"], acc_exact=True)
+    local = LocalStepCheck(reg)
+    hot = hot_user = 0
+    for _ in range(n):
+        pairs, negs, _ = e.sample(B)
+        hot = max(hot, int(np.bincount(pairs[:, 1], minlength=ni).max()))
+        hot_user = max(hot_user, int(np.bincount(pairs[:, 0]).max()))
+        local.before(e)
+        lg = e.step(pairs, negs)
+        local.after(e, pairs, negs, lg)
+        lo = FB.bpr_step_bounded(T["user"], T["item"], T["acc_user"], T["acc_item"], E, pairs, negs, reg)
+        assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
+    for t in TABLES:
+        assert_close(e.get_table(t), T[t], t, bound=E[t])
+    return hot, hot_user
 
 
 @pytest.fixture(scope="module")
@@ -94,26 +113,13 @@ def test_det_pos_sort_matches_oracle(skewed_graph, W, slot_max):
     head spans many 16-pair gradient blocks, against the float64 oracle
     (slot_max 2: users seen more than twice add their rows with int64 atomics)."""
     e = _engine("bpr", skewed_graph, 32, W, det=True, seed=23, slot_max=slot_max)
-    B, ni = 8192, 4_000
-    T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
-    T32 = {t: v.astype(np.float32) for t, v in T.items()}
-    hot = hot_user = 0
     e.profile(True)
-    for _ in range(4):
-        pairs, negs, _ = e.sample(B)
-        hot = max(hot, int(np.bincount(pairs[:, 1], minlength=ni).max()))
-        hot_user = max(hot_user, int(np.bincount(pairs[:, 0]).max()))
-        lg = e.step(pairs, negs)
-        lo = O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.02)
-        O.bpr_step(T32["user"], T32["item"], T32["acc_user"], T32["acc_item"], pairs, negs, 0.02)
-        assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
+    hot, hot_user = _host_fed(e, 8192, 4, 4_000)
     e.profile(False)
     assert e.profile_read("psort")[1] == 4
     assert hot >= 16 * 8   # a positive run past the 8 partial rows: int64 atomics (GV64)
     if slot_max:
         assert hot_user > slot_max, hot_user
-    for t in TABLES:
-        assert_close(e.get_table(t), T[t], t, ref32=T32[t])
     e.close()
 
 
@@ -123,18 +129,42 @@ def test_fast_pos_sort_hot_partials_match_oracle(skewed_graph):
     (slotP[block + item]), the rest on float atomics; host-fed steps against
     the float64 oracle."""
     e = _engine("bpr", skewed_graph, 64, 1, det=False, seed=29)
-    B, ni = 32768, 4_000
-    T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
-    T32 = {t: v.astype(np.float32) for t, v in T.items()}
-    hot = 0
-    for _ in range(3):
-        pairs, negs, _ = e.sample(B)
-        hot = max(hot, int(np.bincount(pairs[:, 1], minlength=ni).max()))
-        lg = e.step(pairs, negs)
-        lo = O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, 0.02)
-        O.bpr_step(T32["user"], T32["item"], T32["acc_user"], T32["acc_item"], pairs, negs, 0.02)
-        assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
+    hot, _ = _host_fed(e, 32768, 3, 4_000)
     assert hot >= 16 * 32   # one run over >= 32 blocks, far past the 8 partial rows
-    for t in TABLES:
-        assert_close(e.get_table(t), T[t], t, ref32=T32[t])
     e.close()
+
+
+@pytest.mark.parametrize("how", ["huge", "inf"])
+def test_det_fixed_point_range_guard(skewed_graph, how):
+    """A diverged item table (rows of 1e25, or inf) makes every duplicated
+    item's gradient term leave the fixed-point range: the deterministic call
+    fails with CF_ENUMERIC instead of leaving wrapped integers in the table
+    (the fast path carries the inf / NaN into the tables, as TF1's fp32 path
+    would).  The flag is cleared by the failing call: the engine steps again
+    once the tables are valid."""
+    from collaborativefilteringusingtensorflow_amd import _native as N
+    e = _engine("bpr", skewed_graph, 32, 1, det=True, seed=31)
+    V = e.get_table("item")
+    bad = V.copy()
+    bad[: 200] = 1e25 if how == "huge" else np.inf
+    e.set_table("item", bad)
+    pairs, negs, _ = e.sample(8192)
+    with pytest.raises(N.NativeError, match="CF_ENUMERIC"):
+        e.step(pairs, negs)
+    e.set_table("item", V)
+    e.set_table("acc_item", np.full_like(V, 0.1))
+    with pytest.raises(N.NativeError, match="CF_ENUMERIC"):
+        e.set_table("item", bad)
+        e.train_steps(8192, 2)
+    e.set_table("item", V)
+    e.set_table("acc_item", np.full_like(V, 0.1))
+    e.init_params(0.0, 0.1, truncated=True, seed=3)
+    loss = e.train_steps(8192, 2)          # valid again: no stale flag
+    assert np.isfinite(loss)
+    # the fast path takes the same state without an error and shows the divergence
+    f = _engine("bpr", skewed_graph, 32, 1, det=False, seed=31)
+    f.set_table("item", bad)
+    f.step(pairs, negs)
+    assert not np.isfinite(f.get_table("item")[:200]).all() or how == "huge"
+    e.close()
+    f.close()

@@ -32,14 +32,16 @@ def _free_port():
 
 
 def _worker(rank, world, port, fold, batches, U0, V0, b0, q, sampled, exchange="allreduce",
-            pipelined=True, split=True, grad_path=0):
+            pipelined=True, split=True, grad_path=0, backend="gloo"):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
     from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_group_exchange,
                                                                        shard_users, local_csr)
     from collaborativefilteringusingtensorflow_amd.engine import Engine
-    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+    if backend == "nccl":   # RCCL accepts a one-rank communicator on device 0
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, init_method="tcp://127.0.0.1:%d" % port, rank=rank,
                             world_size=world)
     ip, ix = fold["train_indptr"], fold["train_indices"]
     bounds = [shard_users(ip, world, r)[0] for r in range(world)] + [943]
@@ -91,16 +93,16 @@ SIZES = (64, 64, 48, 48, 64, 32, 32, 64)
 
 
 def _run(fold1, batches, U0, V0, b0, sampled=False, exchange="allreduce", pipelined=True, split=True,
-         grad_path=0):
+         grad_path=0, world=2, backend="gloo"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, fold1, batches, U0, V0, b0, q, sampled, exchange,
-                                               pipelined, split, grad_path))
-             for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fold1, batches, U0, V0, b0, q, sampled, exchange,
+                                               pipelined, split, grad_path, backend))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -124,7 +126,18 @@ def test_two_rank_group_exchange_lds_kernel(fold1, streams, split):
     _two_rank_global_step(fold1, streams, "gbpr_b100_g1_w5", "allreduce", split, 64, 3)
 
 
-def _two_rank_global_step(fold1, streams, stream, exchange, split, d, grad_path):
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
+def test_one_rank_rccl_forced_split_step(fold1, streams, exchange):
+    """The split exchange step on RCCL (nccl backend, one rank on device 0,
+    split forced): its collectives are asynchronous there -- the member-row
+    all-to-all runs beside gradient part 1, the item reduce beside the
+    member-gradient all-to-all and the user finish -- so this checks their
+    stream ordering against the float64 oracle (gloo, used by every multi-rank
+    test, runs them synchronously)."""
+    _two_rank_global_step(fold1, streams, "gbpr_b100_g1_w5", exchange, "force", 16, 0, world=1, backend="nccl")
+
+
+def _two_rank_global_step(fold1, streams, stream, exchange, split, d, grad_path, world=2, backend="gloo"):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(12)
     U0 = O.init_table(rng, (943, d))
@@ -132,7 +145,8 @@ def _two_rank_global_step(fold1, streams, stream, exchange, split, d, grad_path)
     b0 = O.init_table(rng, (1682,))
     batches = [(streams[stream + "/pairs"][s], streams[stream + "/negs"][s],
                 streams[stream + "/groups"][s]) for s in range(8)]
-    res = _run(fold1, batches, U0, V0, b0, exchange=exchange, split=split, grad_path=grad_path)
+    res = _run(fold1, batches, U0, V0, b0, exchange=exchange, split=split, grad_path=grad_path, world=world,
+               backend=backend)
     U, V, b = U0.astype(np.float64), V0.astype(np.float64), b0.astype(np.float64)
     AU, AV, Ab = np.full_like(U, 0.1), np.full_like(V, 0.1), np.full_like(b, 0.1)
     lo = 0.0
@@ -147,7 +161,8 @@ def _two_rank_global_step(fold1, streams, stream, exchange, split, d, grad_path)
         assert_close(br, b, ("bias", rank))
         assert_close(AVr, AV, ("acc_item", rank))
         assert_close(Abr, Ab, ("acc_bias", rank))
-    assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
+    if world > 1:
+        assert np.array_equal(res[0][4], res[1][4]) and np.array_equal(res[0][5], res[1][5])
 
 
 def test_two_rank_device_sampled_groups_span_shards(fold1):

@@ -5,16 +5,20 @@ orders the pairs by positive item, and the gradient launch sums the pairs of
 one block that share a positive item in LDS: one partial row per (block,
 item) instead of one slot row (or float atomics) per occurrence.  The step is
 still TF1's dedup-sum + SparseApplyAdagrad (bprmf.py:74-88), so every case is
-checked against the float64 oracle at the north star's 1e-5, elementwise
-(|gpu - oracle| <= 1e-6 + 1e-5 |oracle| on every element of every table; the
-per-step loss within 1e-5) on the reference's captured batches, plus hot items
-whose partials overflow their slot range, items seen only as positives, and
-the device-sampled pipeline (draw fused into the apply launch).
+checked against the float64 oracle: each BPR / AMF step from the engine's own
+pre-step tables within the a-priori fp32 bound of oracle/fp32_bound.py
+(conftest.LocalStepCheck), and the trajectory at the north star's 1e-5,
+elementwise (|gpu - oracle| <= 1e-6 + 1e-5 |oracle| on every element of every
+table; the per-step loss within 1e-5) on the reference's captured batches,
+plus hot items whose partials overflow their slot range (their trajectory
+band adds the same a-priori bound carried over the steps), items seen only
+as positives, and the device-sampled pipeline (draw fused into the apply
+launch).
 """
 import numpy as np
 import pytest
 
-from conftest import CML_TRAJ, assert_close, get_stream
+from conftest import CML_TRAJ, LocalStepCheck, assert_close, get_stream
 from oracle import cf_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -43,7 +47,15 @@ def psort_launches(e):
     return e.profile_read("psort")[1]
 
 
-def run_steps(model, fold1, batches, d, opts, amf_switch=None, **kw):
+def run_steps(model, fold1, batches, d, opts, amf_switch=None, forward_bound=False, **kw):
+    """Engine steps on host-fed batches.  BPR / AMF: every step against the
+    float64 oracle from the engine's own pre-step tables within the a-priori
+    fp32 bound (conftest.LocalStepCheck); the whole trajectory against the
+    float64 oracle in the strict band -- plus, with ``forward_bound``, the
+    same a-priori bound carried over the steps (oracle/fp32_bound.py): a
+    Zipf-head row's fp32 rounding, amplified over steps, leaves the strict
+    band in every summation order, the float32 oracle's own included."""
+    from oracle import fp32_bound as FB
     W = batches[0][1].shape[1]
     U, V = tables(fold1, d, 3, truncated=(model != "cml"))
     e = make(model, fold1, d, W, opts, **kw)
@@ -53,8 +65,11 @@ def run_steps(model, fold1, batches, d, opts, amf_switch=None, **kw):
     e.profile(True)
     U64, V64 = U.astype(np.float64), V.astype(np.float64)
     AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
-    # BPR: the same trajectory in float32 grounds the hot rows' tolerance
-    T32 = [x.astype(np.float32) for x in (U64, V64, AU, AV)] if model == "bpr" else None
+    E = FB.zero_bounds(U64, V64) if forward_bound else None
+    local = None
+    if model in ("bpr", "amf"):
+        local = LocalStepCheck(kw["reg"], adversarial=None if model == "bpr" else False,
+                               reg_adv=kw.get("reg_adv", 1.0))
     adv = False
     for s, (pairs, negs) in enumerate(batches):
         if amf_switch is not None and s == amf_switch:
@@ -62,10 +77,17 @@ def run_steps(model, fold1, batches, d, opts, amf_switch=None, **kw):
             adv = True
             AU[...] = 0.1
             AV[...] = 0.1
+            local.T, local.adversarial = None, True
+        if local is not None:
+            local.before(e)
         lg = e.step(pairs, negs)
+        if local is not None:
+            local.after(e, pairs, negs, lg, "step %d" % s)
         if model == "bpr":
-            lo = O.bpr_step(U64, V64, AU, AV, pairs, negs, kw["reg"])
-            O.bpr_step(*T32, pairs, negs, kw["reg"])
+            if E is not None:
+                lo = FB.bpr_step_bounded(U64, V64, AU, AV, E, pairs, negs, kw["reg"])
+            else:
+                lo = O.bpr_step(U64, V64, AU, AV, pairs, negs, kw["reg"])
         elif model == "amf":
             lo = O.amf_step(U64, V64, AU, AV, pairs, negs, kw["reg"], adv, reg_adv=kw.get("reg_adv", 1.0))
         else:
@@ -75,8 +97,8 @@ def run_steps(model, fold1, batches, d, opts, amf_switch=None, **kw):
     e.profile(False)
     n_ps = psort_launches(e)
     tol = CML_TRAJ if model == "cml" else {}
-    for q, (t, o) in enumerate((("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV))):
-        assert_close(e.get_table(t), o, t, ref32=T32[q] if T32 else None, **tol)
+    for t, o in (("user", U64), ("item", V64), ("acc_user", AU), ("acc_item", AV)):
+        assert_close(e.get_table(t), o, t, bound=None if E is None else E[t], **tol)
     e.close()
     return n_ps
 
@@ -154,7 +176,7 @@ def test_pos_sort_hot_item(fold1, cap, slot_max, n_pos, n_neg_hot):
     rng = np.random.RandomState(n_pos + n_neg_hot + cap)
     batches = [hot_batch(fold1, rng, n_pos, n_neg_hot) for _ in range(3)]
     n = run_steps("bpr", fold1, batches, 16, {"pos_sort": 1, "slot_max_pos": cap, "slot_max": slot_max},
-                  reg=0.02)
+                  forward_bound=True, reg=0.02)
     assert n == 3
 
 

@@ -1,5 +1,6 @@
 """Print VGPR / LDS / occupancy per kernel of one source file (compile-time,
-no GPU):  python tools/kernel_regs.py cf_kernels.hip [name-filter]"""
+no GPU):  python tools/kernel_regs.py cf_grad_bpr.hip [name-filter]
+(gradient kernels: cf_grad_<model>.hip; draw / apply: cf_kernels.hip)"""
 import os
 import re
 import subprocess
