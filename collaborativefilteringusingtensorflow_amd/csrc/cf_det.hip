@@ -124,6 +124,25 @@ __global__ __launch_bounds__(256) void psort_scatter_kernel(PsortArgs a) {
 #pragma unroll
         for (int k = 0; k < RS / 4; ++k) r[k] = make_int4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
+    // the draw's phantoms (StepArgs::spec_ph): a speculatively counted first
+    // candidate that the row scan rejected holds rank ph.y among item ph.x's
+    // negatives.  Its compact slot row is zeroed, so the apply's sum of the
+    // item's negative rows is unchanged (x + 0 = x); an item that only the
+    // phantom touched (count 1) is applied by no one, so its count is reset
+    // here -- nothing reads cntV of this buffer set after the scans
+    if (a.spec_n != nullptr) {
+        const int np = *a.spec_n;
+        for (int k = t0; k < np; k += nt) {
+            const int2 ph = a.spec_ph[k];
+            const int2 o0 = a.offPN[ph.x], o1 = a.offPN[ph.x + 1];
+            if ((o1.x - o0.x) + (o1.y - o0.y) == 1) {
+                a.cntVw[ph.x] = 0;
+            } else {
+                float* row = a.slotN + ((int64_t)o0.y + ph.y) * a.d;
+                for (int e = 0; e < a.d; ++e) row[e] = 0.f;
+            }
+        }
+    }
 }
 
 // offPN[r] = (offP[r], offN[r]), the exclusive scans of cntP (positives per

@@ -68,6 +68,10 @@ struct cf_engine {
     int32_t* indices = nullptr;
     int4* pairs = nullptr;   // (u, i, row start, row length) per interaction
     int4* pf_recs[2] = {nullptr, nullptr};   // prefetched pair records per buffer set (StepArgs::pf_out)
+    // speculative negative counts (StepArgs::spec_ph), per buffer set
+    int2* spec_ph_[2] = {nullptr, nullptr};
+    int* spec_n_[2] = {nullptr, nullptr};
+    int spec_neg = 1;   // cf_set_option "spec_neg"
     // deterministic mode on the pos_sort path: fixed-point partials and the
     // users' int64 overflow accumulators (StepArgs::det_fx)
     long long* slotP64 = nullptr;
@@ -475,11 +479,24 @@ int ensure_order(cf_engine* e, int B) {
     dfree(e->srec);
     dfree(e->slotN);
     dfree(e->slotP);
+    for (int q = 0; q < 2; ++q) {
+        dfree(e->spec_ph_[q]);
+        dfree(e->spec_n_[q]);
+    }
     CF_TRY(dalloc(&e->srec, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg)));
     // one partial row per (gradient block, positive item): row block + item
     CF_TRY(dalloc(&e->slotP, ((size_t)std::max(B, e->Bcap) / kPsortPPB + 1 + (size_t)e->cfg.n_items) *
                                  e->cfg.n_factors));
-    CF_TRY(dalloc(&e->slotN, (size_t)std::max(B, e->Bcap) * e->cfg.n_neg * e->cfg.n_factors));
+    // compact negative slots offN[j] + rank: the counts include the draw's
+    // phantoms (StepArgs::spec_ph, at most one per negative), whose ranks
+    // leave holes, so the slots span up to twice the batch's negatives
+    CF_TRY(dalloc(&e->slotN, (size_t)std::max(B, e->Bcap) * e->cfg.n_neg * 2 * e->cfg.n_factors));
+    // at most one phantom per negative (StepArgs::spec_ph)
+    for (int q = 0; q < 2; ++q) {
+        CF_TRY(dalloc(&e->spec_ph_[q], (size_t)std::max(B, e->Bcap) * e->cfg.n_neg));
+        CF_TRY(dalloc(&e->spec_n_[q], 1));
+        CF_HIP(hipMemsetAsync(e->spec_n_[q], 0, sizeof(int), e->stream));
+    }
     // in-range ids from the start (a given-up fused scatter leaves old records)
     CF_HIP(hipMemsetAsync(e->srec, 0, (size_t)std::max(B, e->Bcap) * psort_stride(e->cfg.n_neg) * 4, e->stream));
     e->order_cap = std::max(B, e->Bcap);
@@ -562,6 +579,13 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.slotP = e->slotP;
         a.slotV = e->slotN;   // negatives: compact slots offN[j] + rank
         a.capP = e->capP;
+        // speculative negative counts need the dense item apply of pos_sort
+        // (every item row visited: a phantom holding rank 0 cannot hide an
+        // item from an owner rule) -- the same test as apply_args
+        if (e->spec_neg && a.count_items && c.n_items <= 2 * (int64_t)B * items_per_pair(c)) {
+            a.spec_ph = e->spec_ph_[k];
+            a.spec_n = e->spec_n_[k];
+        }
         if (e->det && e->slotP64 && e->fx_cap >= B && e->GU64 && e->GV64) {
             // deterministic: the fast path's launches, every sum in fixed point
             a.det_fx = 1;
@@ -883,6 +907,11 @@ int psort(cf_engine* e, const StepArgs& a) {
     q.srec = e->srec;
     q.B = a.B; q.W = a.W; q.capU = a.capU;
     q.n_items = e->cfg.n_items;
+    q.spec_ph = a.spec_ph;
+    q.spec_n = a.spec_n;
+    q.slotN = e->slotN;
+    q.cntVw = a.cntV;
+    q.d = e->cfg.n_factors;
     CF_HIP(launch_psort(q, e->psort_tmp, e->psort_tmp_bytes, e->stream));
     return CF_OK;
 }
@@ -1056,6 +1085,7 @@ int discard_pending(cf_engine* e) {
     if (a.count_users) CF_HIP(launch_uncount(a.occU, nU, a.cntU, e->stream));
     if (a.count_items) CF_HIP(launch_uncount(a.occV, nV, a.cntV, e->stream));
     if (a.count_items && a.cntP) CF_HIP(launch_uncount(a.occV, e->pend_B, a.cntP, e->stream));
+    if (a.spec_n) CF_HIP(launch_uncount_spec(a.spec_ph, a.spec_n, a.cntV, e->stream));
     e->epoch = e->pend_epoch;
     e->batch = e->pend_batch;
     e->sampler_B = e->pend_sampler_B;
@@ -2242,8 +2272,16 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         e->topk_path = (int)value;
         return CF_OK;
     }
+    if (n == "spec_neg") {   // speculative negative counts in the pos_sort draw (StepArgs::spec_ph)
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "spec_neg must be 0 or 1");
+        CF_TRY(discard_pending(e));   // a drawn-ahead batch was counted under the old setting
+        e->spec_neg = (int)value;
+        return CF_OK;
+    }
     if (n == "pair_prefetch") {
         if (value < 0 || value > 1) return fail(CF_EINVAL, "pair_prefetch must be 0 or 1");
+        if (value == 1 && !pair_prefetch_built())
+            return fail(CF_EINVAL, "pair_prefetch: this build has the prefetch compiled out (-DCF_PAIR_PREFETCH=1)");
         e->pair_prefetch = (int)value;
         return CF_OK;
     }

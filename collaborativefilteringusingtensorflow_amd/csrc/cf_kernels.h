@@ -90,6 +90,17 @@ struct StepArgs {
     unsigned long long* __restrict__ GU64;  // [n_users, d], zero between steps
     unsigned long long* __restrict__ GV64;  // [n_items, d]: positive partials past capP, zero between steps
     int* __restrict__ fx_bad;               // set when a term / sum leaves the fixed-point range (to_fx)
+    // speculative negative counts (round 4; pos_sort with the dense item
+    // apply): the draw issues the returning count atomic of each negative's
+    // FIRST candidate before the row scan that accepts or rejects it, so the
+    // atomic's latency overlaps the scan instead of following it.  A rejected
+    // first candidate (probability |Pos(u)| / n_items) leaves a phantom
+    // occurrence (item, rank) in spec_ph: psort zeroes its compact slot row
+    // (or resets the count of an item the phantom alone touched), the
+    // gradient launch re-zeroes spec_n for the next draw into this buffer
+    // set, and a discarded draw uncounts the phantoms.  null = off
+    int2* __restrict__ spec_ph;             // [B * W]
+    int* __restrict__ spec_n;
     int lane_draw;                          // 1: one lane per pair (neg_check 2, with the set)
     // tables (updated in place for rows seen once in the batch)
     float* __restrict__ U; float* __restrict__ AU; float* __restrict__ GU;
@@ -414,8 +425,19 @@ struct PsortArgs {
     int32_t* srec;                       // [B, psort_stride(W)]
     int B, W, capU;
     int64_t n_items;
+    // speculative negative counts (StepArgs::spec_ph): the phantoms' compact
+    // slot rows of slotN are zeroed, a phantom-only item's count reset
+    const int2* spec_ph;
+    const int* spec_n;
+    float* slotN;
+    int32_t* cntVw;
+    int d;
 };
 hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
+// a discarded draw's phantoms (StepArgs::spec_ph): uncount them, re-zero spec_n
+hipError_t launch_uncount_spec(const int2* ph, int* n, int32_t* cnt, hipStream_t s);
+// grad_sort_kernel carries the pair-record prefetch (StepArgs::pf_out)
+bool pair_prefetch_built();
 hipError_t launch_build_pos_set(const int4* pairs, int64_t nnz, unsigned long long* set,
                                 uint64_t mask, hipStream_t s);
 hipError_t launch_build_pairs(const int64_t* indptr, const int32_t* indices, int64_t n_users,

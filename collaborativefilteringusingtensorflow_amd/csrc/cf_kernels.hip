@@ -468,6 +468,23 @@ __global__ void uncount_kernel(const int32_t* __restrict__ occ, int64_t n, int32
     }
 }
 
+// a discarded draw's phantoms (StepArgs::spec_ph): one block uncounts them,
+// then re-zeroes the phantom count after every lane has read it
+__global__ __launch_bounds__(kBlock) void uncount_spec_kernel(const int2* __restrict__ ph, int* __restrict__ n,
+                                                               int32_t* __restrict__ cnt) {
+    const int np = *n;
+    for (int k = threadIdx.x; k < np; k += kBlock) atomicSub(&cnt[ph[k].x], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) *n = 0;
+}
+
+hipError_t launch_uncount_spec(const int2* ph, int* n, int32_t* cnt, hipStream_t s) {
+    hipLaunchKernelGGL(uncount_spec_kernel, dim3(1), dim3(kBlock), 0, s, ph, n, cnt);
+    return hipGetLastError();
+}
+
+bool pair_prefetch_built() { return CF_PAIR_PREFETCH != 0; }
+
 hipError_t launch_uncount(const int32_t* occ, int64_t n, int32_t* cnt, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(uncount_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, occ, n, cnt);

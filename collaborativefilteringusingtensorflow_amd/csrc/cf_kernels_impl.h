@@ -492,7 +492,11 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         // carries the user's CSR extent, so the row scan does not wait on a
         // dependent indptr load.  pre_pairs: the record the previous step's
         // gradient launch fetched (StepArgs::pf_out), read coalesced
+#ifdef CF_EXP_DRAW_NOREC   // attribution only (wrong batches): no record load
+        const int4 pr = make_int4((int)(slot % 1000000), (int)(slot % 100000), (int)((slot * 50) % 40000000), 50);
+#else
         const int4 pr = a.pre_pairs != nullptr ? a.pre_pairs[p] : a.pairs[permute(slot, a.perm)];
+#endif
         u = pr.x;
         i = pr.y;
         key = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
@@ -502,6 +506,20 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         u = a.occU[p];
         i = a.occV[p];
     }
+    // the user's and the positive's returning count atomics need only the
+    // record: issued first, they are in flight during the row scan (their
+    // ranks are stored at the end).  pos_sort: the positive's rank among the
+    // batch's positives of i (the negatives count in cntV), psort's key
+    int rk_u = 0, rk_i = 0;
+#ifdef CF_EXP_DRAW_NOATOM   // attribution only (wrong ranks): no count atomics
+    if (false) {
+#else
+    if (gl == 0) {
+#endif
+        if (a.count_users) rk_u = atomicAdd(&a.cntU[u], 1);
+        if (a.count_items) rk_i = atomicAdd(a.cntP != nullptr ? &a.cntP[i] : &a.cntV[i], 1);
+    }
+    const bool spec = a.sample && a.spec_n != nullptr && a.count_items && a.pos_set == nullptr;
     for (int w0 = 0; w0 < W; w0 += PGL) {
         const int nw = (W - w0 < PGL) ? (W - w0) : PGL;
         const int w = w0 + gl;
@@ -528,12 +546,20 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             const int nl = C * nw;
             int32_t jl = -1;
             if (gl < nl) jl = draw_item(key, ((uint64_t)(w0 + gl % nw) << 32) + (uint64_t)(gl / nw), a.n_items);
+            // speculative count of attempt 0 (lane w - w0 < nw holds it), in
+            // flight during the scan (StepArgs::spec_ph)
+            int rk_s = 0;
+#ifndef CF_EXP_DRAW_NOATOM
+            if (spec && gl < nw) rk_s = atomicAdd(&a.cntV[jl], 1);
+#endif
             uint32_t hit = 0;
             {
                 int32_t cand[PGL];
 #pragma unroll
                 for (int k = 0; k < PGL; ++k) cand[k] = __shfl(jl, k, PGL);
+#ifndef CF_EXP_DRAW_NOSCAN   // attribution only (wrong batches): no row scan
                 hit = gor8(row_hits(a.indices, rb, re, gl, cand, nl));
+#endif
             }
             // lane w < nw: the first accepted attempt of negative w
             bool done = false;
@@ -558,15 +584,21 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
                 if ((h2 >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
                 pending = h2;
             }
-            if (gl < nw) a.occV[B + p * W + w] = j;
+            if (gl < nw) {
+                a.occV[B + p * W + w] = j;
+                if (spec) {
+                    if (j != jl) {   // attempt 0 was a positive: a phantom, then the real count
+                        a.spec_ph[atomicAdd(a.spec_n, 1)] = make_int2(jl, rk_s);
+                        rk_s = atomicAdd(&a.cntV[j], 1);
+                    }
+                    a.rankV[B + p * W + w] = rk_s;
+                }
+            }
+            if (spec) continue;   // counted above
         } else if (gl < nw) {
             j = a.occV[B + p * W + w];
         }
-#ifdef CF_EXP_NORET_ALL   // attribution: every count atomic non-returning, no ranks (wrong results)
-        if (a.count_items && gl < nw) { atomicAdd(&a.cntV[j], 1); a.rankV[B + p * W + w] = 0; }
-#else
         if (a.count_items && gl < nw) a.rankV[B + p * W + w] = atomicAdd(&a.cntV[j], 1);
-#endif
     }
     if (MODEL == GBPR) {
         for (int k = gl; k < G; k += PGL) {
@@ -592,22 +624,8 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             a.occU[p] = u;
             a.occV[p] = i;
         }
-#ifdef CF_EXP_NORET_ALL
-        if (a.count_users) { atomicAdd(&a.cntU[u], 1); a.rankU[p] = 0; }
-        if (a.count_items) { atomicAdd(&a.cntV[i], 1); a.rankV[p] = 0; }
-#else
-        if (a.count_users) a.rankU[p] = atomicAdd(&a.cntU[u], 1);
-#endif
-#if defined(CF_EXP_NORET_ALL)
-#elif defined(CF_EXP_NORET)
-        if (a.count_items) { atomicAdd(&a.cntV[i], 1); a.rankV[p] = 0; }
-#elif defined(CF_EXP_NO_ICOUNT)
-        if (a.count_items) a.rankV[p] = 0;
-#else
-        // pos_sort: the positive's rank among the batch's positives of i (the
-        // negatives count in cntV), the key of psort's counting sort
-        if (a.count_items) a.rankV[p] = atomicAdd(a.cntP != nullptr ? &a.cntP[i] : &a.cntV[i], 1);
-#endif
+        if (a.count_users) a.rankU[p] = rk_u;
+        if (a.count_items) a.rankV[p] = rk_i;
     }
 }
 
@@ -1758,7 +1776,11 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     int4 pfr = make_int4(0, 0, 0, 0);
     int64_t pfp = -1;
 #ifndef CF_PAIR_PREFETCH
-#define CF_PAIR_PREFETCH 1   // 0: the prefetch compiled out (A/B of its cost to the kernel body)
+// 1: the prefetch compiled in.  Its registers take grad_sort_kernel<BPR, 4, 1>
+// from 75 to 81 VGPRs, 6 -> 5 waves / SIMD: the cfg2 gradient launch ran
+// 197.3 us with it, 179.9 us without (same box, round 4,
+// profiles/r04/ab_occupancy/); the engine refuses the option unless built in
+#define CF_PAIR_PREFETCH 0
 #endif
     if constexpr (SORT && CF_PAIR_PREFETCH) {
         if (a.pf_out != nullptr && gl == 0) {
@@ -1798,6 +1820,9 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     for (int k = 0; k < P; ++k)
         if (ok[k]) pr[k].template update<SORT>(a, gl, loss_g, sq, SORT ? &s_gi[grp][0] : nullptr);
     if constexpr (SORT) {
+        // psort consumed this buffer set's phantoms: re-zero the count for
+        // the set's next draw (StepArgs::spec_ph)
+        if (block == 0 && threadIdx.x == 0 && a.spec_n != nullptr) *a.spec_n = 0;
         if (gl == 0) s_item[grp] = ok[0] ? pr[0].i : -1;
         __syncthreads();
         if (ok[0] && (grp == 0 || s_item[grp - 1] != pr[0].i))
@@ -2742,10 +2767,26 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 // grid: [0, nbI) dense item blocks, [nbI, nbI + nbW) wave blocks, then (with
 // DRAW) the draw + count blocks of the next step (other buffer set).  PS:
 // pos_sort's item rows (offPN), else apply_rows_item_block
+// The draw blocks are interleaved with the apply blocks (minor_block,
+// round 4): the apply is bandwidth-bound (~4.9 TB/s), the draw latency-bound
+// (~1 TB/s), and with the draw after every apply block the two overlapped
+// for only ~16 us of a 187 us launch at cfg2 (apply 84 us and draw 119 us
+// as separate launches).  -DCF_APPLY_DRAW_TAIL=1: the old order.
+#ifndef CF_APPLY_DRAW_TAIL
+#define CF_APPLY_DRAW_TAIL 0
+#endif
 template <int EPL, bool DRAW, bool PS = true, bool FX = false>
 __global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
-    const int b = blockIdx.x;
-    if (b == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
+    int b = blockIdx.x;
+    if (blockIdx.x == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
+    if constexpr (DRAW && !CF_APPLY_DRAW_TAIL) {
+        int idx;
+        if (minor_block(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)) {
+            prep_any<BPR>(nx, idx);
+            return;
+        }
+        b = idx;
+    }
     if (b < nbI) {
         if constexpr (PS)
             apply_ps_item_block<EPL, FX>(p, b);

@@ -459,10 +459,19 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                and takes every sum of gradient rows in 64-bit fixed point
  *                (2^-32 units; int64 partial rows and int64 atomics), which
  *                is exact in any order, so no sort runs.
+ *   "spec_neg"   1 (default) = where pos_sort is active with its dense item
+ *                apply (n_items <= 2 B (1 + W)), the draw issues each
+ *                negative's count atomic for its FIRST candidate before the
+ *                row scan that accepts or rejects it (its latency overlaps
+ *                the scan); a rejected first candidate leaves a phantom
+ *                occurrence whose slot row psort zeroes.  Same batches, same
+ *                sums up to fp32 order; 0 = count after the scan.
  *   "pair_prefetch" 1 = the pos_sort gradient launch also fetches the next
  *                step's shuffled pair records for its draw (cf_train_steps);
- *                measured slower at cfg2 (gradient launch +20 us, draw -2
- *                us), so 0 (default).
+ *                measured slower at cfg2 (its registers cost the gradient
+ *                launch a wave per SIMD), so 0 (default), and the default
+ *                build compiles it out: 1 then fails with CF_EINVAL (build
+ *                with -DCF_PAIR_PREFETCH=1).
  *   "pos_sort"   1 = the gradient launch visits the batch's pairs in
  *                positive-item order (a counting sort by the draw's positive
  *                counts, two short launches before it), so the pairs of one

@@ -272,3 +272,34 @@ def test_pos_sort_auto_by_batch_size():
     for t in T:
         assert_close(e.get_table(t), T[t], t)
     e.close()
+
+
+@pytest.mark.parametrize("W", [1, 5])
+def test_spec_neg_equals_plain_draw(fold1, W):
+    """Speculative negative counts (cf_set_option "spec_neg", StepArgs::spec_ph):
+    on ml-100k a heavy user's row holds up to ~40 % of the 1,682 items, so many
+    first candidates are rejected and leave phantom occurrences (zeroed slot
+    rows, phantom-only items' counts reset).  The draw is the same stream, so
+    spec on and off train the same model up to fp32 summation order -- also
+    across a discarded drawn-ahead batch (the batch size changes mid-run)."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    out = []
+    for spec in (0, 1):
+        e = Engine("bpr", 943, 1682, 32, n_neg=W, reg=0.05, seed=41)
+        e.set_option("item_slots", 0)
+        e.set_option("pos_sort", 1)
+        e.set_option("spec_neg", spec)
+        e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+        e.init_params(0.0, 0.1, truncated=True, seed=2)
+        e.profile(True)
+        loss = e.train_steps(2048, 12)
+        loss += e.train_steps(1024, 6)     # the pending 2048-pair draw is discarded
+        loss += e.train_steps(2048, 6)
+        e.profile(False)
+        assert e.profile_read("psort")[1] == 24
+        out.append((loss, {t: e.get_table(t) for t in ("user", "item", "acc_user", "acc_item")}))
+        e.close()
+    (l0, T0), (l1, T1) = out
+    assert abs(l1 - l0) <= 1e-5 * abs(l0)
+    for t in T0:
+        assert_close(T1[t], T0[t], t)

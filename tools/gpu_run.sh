@@ -27,7 +27,7 @@ die() { echo "$1"; exit ${2:-1}; }
 
 step_tests() {
   timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest ${PYTEST_ARGS:-tests -m gpu} -q -rf \
-      --timeout ${TEST_TIMEOUT:-300} --timeout-method thread > $OUT/pytest.log 2>&1
+      --timeout ${TEST_TIMEOUT:-150} --timeout-method thread > $OUT/pytest.log 2>&1
   local rc=$?
   tail -12 $OUT/pytest.log
   # 0 passed, 1 some tests failed: go on; anything else (abort, timeout, fault) stops here
