@@ -383,6 +383,17 @@ __device__ __forceinline__ int32_t draw_item(uint64_t key, uint64_t ctr, int64_t
 constexpr int kPrepGL = CF_PREP_GL;
 constexpr int kPrepPairsPerBlock = kBlock / kPrepGL;
 constexpr int kPrepChunks = CF_PREP_CHUNKS;
+// W = 1 (cfg2): 4 lanes per pair (round 4).  Four candidates per row scan
+// still leave a rejection of all of them at |Pos(u)|^4 / n_items^4, and a
+// wave draws 16 pairs instead of 8 -- half the draw's waves, whose integer
+// hashing (permute, draw_item) is paid per wave-instruction whatever the
+// lanes.  Each lane keeps 64 / 4 = 16 row chunks in flight (one scan covers
+// 64 ids, as the 8-lane group's 8 x 8).  W = 5 keeps 8 lanes: all five
+// negatives' first attempts in one scan.
+#ifndef CF_PREP_GL_W1
+#define CF_PREP_GL_W1 4
+#endif
+__host__ __device__ constexpr int prep_chunks(int pgl) { return pgl == kPrepGL ? kPrepChunks : 64 / pgl; }
 // row scan in 16-B loads (4 ids per lane per chunk): measured SLOWER at cfg2
 // (same box, r03: draw alone 183 vs 119 us, 0.489 vs 0.399 ms/step;
 // profiles/r03/ab_draw_vec_sortw.txt) -- the masked 4 x 8 compare per chunk
@@ -396,10 +407,11 @@ constexpr int kPrepChunks = CF_PREP_CHUNKS;
 #endif
 constexpr int kPrepVChunks = CF_PREP_VCHUNKS;
 
-// OR over the kPrepGL lanes of a draw group
+// OR over the PGL lanes of a draw group
+template <int PGL = kPrepGL>
 __device__ __forceinline__ uint32_t gor8(uint32_t v) {
 #pragma unroll
-    for (int o = kPrepGL / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
+    for (int o = PGL / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
     return v;
 }
 
@@ -428,8 +440,11 @@ __device__ __forceinline__ bool is_positive(const StepArgs& a, int u, int32_t j)
 // before rb, kPrepVChunks chunks in flight -- a 51-id row is two load
 // instructions instead of seven 4-B ones (the indices allocation is padded
 // by 4 ids, so an int4 never leaves it); ids outside [rb, re) never match.
+template <int PGL = kPrepGL>
 __device__ __forceinline__ uint32_t row_hits(const int32_t* __restrict__ ind, int64_t rb, int64_t re, int gl,
-                                             const int32_t (&cand)[kPrepGL], int ncand) {
+                                             const int32_t (&cand)[PGL], int ncand) {
+    constexpr int kPrepGL = PGL;                   // the group's lanes
+    constexpr int kPrepChunks = prep_chunks(PGL);  // chunks in flight per lane
     uint32_t hit = 0;
 #if CF_PREP_VEC
     constexpr int CW = 4 * kPrepGL;   // ids per chunk
@@ -474,11 +489,10 @@ __device__ __forceinline__ uint32_t row_hits(const int32_t* __restrict__ ind, in
     return hit;
 }
 
-template <int MODEL>
+template <int MODEL, int PGL = kPrepGL>
 __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
-    constexpr int PGL = kPrepGL;
     const int gl = threadIdx.x & (PGL - 1);
-    const int p = block * kPrepPairsPerBlock + (threadIdx.x / PGL);
+    const int p = block * (kBlock / PGL) + (threadIdx.x / PGL);
     if (p >= a.B) return;  // whole group leaves; no block barrier below
     const int W = a.W;
     const int G = (MODEL == GBPR) ? a.G : 0;
@@ -558,7 +572,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
 #pragma unroll
                 for (int k = 0; k < PGL; ++k) cand[k] = __shfl(jl, k, PGL);
 #ifndef CF_EXP_DRAW_NOSCAN   // attribution only (wrong batches): no row scan
-                hit = gor8(row_hits(a.indices, rb, re, gl, cand, nl));
+                hit = gor8<PGL>(row_hits<PGL>(a.indices, rb, re, gl, cand, nl));
 #endif
             }
             // lane w < nw: the first accepted attempt of negative w
@@ -573,14 +587,14 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             }
             // rare: every tested attempt of some negative was a positive ->
             // continue its sequence at attempt C, one candidate per lane
-            uint32_t pending = gor8((gl < nw && !done) ? (1u << gl) : 0u);
+            uint32_t pending = gor8<PGL>((gl < nw && !done) ? (1u << gl) : 0u);
             uint64_t ctr = ((uint64_t)w << 32) + (uint64_t)C;
             if ((pending >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
             while (pending != 0u) {  // group-uniform
                 int32_t cand[PGL];
 #pragma unroll
                 for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
-                uint32_t h2 = gor8(row_hits(a.indices, rb, re, gl, cand, nw)) & pending;
+                uint32_t h2 = gor8<PGL>(row_hits<PGL>(a.indices, rb, re, gl, cand, nw)) & pending;
                 if ((h2 >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
                 pending = h2;
             }
@@ -940,11 +954,15 @@ __device__ __forceinline__ void prep_any(const StepArgs& a, int block) {
         prep_body_np<MODEL>(a, block);
         return;
     }
-    prep_body<MODEL>(a, block);
+    if (a.W == 1)
+        prep_body<MODEL, CF_PREP_GL_W1>(a, block);
+    else
+        prep_body<MODEL>(a, block);
 }
 
 __host__ __device__ __forceinline__ int prep_pairs_per_block(const StepArgs& a) {
-    return lane_prep(a) ? kBlock : multi_prep(a) ? kPrepPairs * kPrepPairsPerBlock : kPrepPairsPerBlock;
+    return lane_prep(a) ? kBlock : multi_prep(a) ? kPrepPairs * kPrepPairsPerBlock
+                                 : a.W == 1 ? kBlock / CF_PREP_GL_W1 : kPrepPairsPerBlock;
 }
 
 template <int MODEL>

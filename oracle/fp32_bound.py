@@ -192,3 +192,121 @@ def reset_acc(AU, AV, E):
     AV[...] = ACC_INIT
     E["acc_user"][...] = ACC0_ERR
     E["acc_item"][...] = ACC0_ERR
+
+
+# ----------------------------------------------------------------------------
+# CML  (cml.py:55-129; = cf_oracle.cml_step)
+# ----------------------------------------------------------------------------
+def _clip_bounded(X, EX, clip_norm):
+    """tf.clip_by_norm(X, c, axes=[1]) on every row (cml.py:119-129), exact
+    math in float64 (a row with |x| <= c is left exactly as it is), and the
+    bound of an fp32 clip of rows within EX of X: the clip is 1-Lipschitz in
+    L2, so an element moves by at most the row's ||EX||_2; the norm's and the
+    scaling's rounding (and a row the fp32 norm puts on the other side of c)
+    by (gamma(d + 4) + 3u) (|x| + e).  A row whose norm is below c by more
+    than its error bound is not clipped on either side: E unchanged (the
+    engine leaves an untouched row bit-identical)."""
+    d = X.shape[1]
+    n = np.sqrt(np.sum(X * X, axis=1, keepdims=True))
+    en = np.sqrt(np.sum(EX * EX, axis=1, keepdims=True))
+    rel = gamma(d + 4) + 3.0 * U32
+    maybe = (n + en) * (1.0 + rel) >= clip_norm
+    scale = np.where(n > clip_norm, clip_norm / np.where(n > 0, n, 1.0), 1.0)
+    X *= scale
+    EX[...] = np.where(maybe, en + rel * (np.abs(X) / scale + EX), EX)
+
+
+def cml_step_bounded(U, V, AU, AV, E, pairs, negs, margin, reg_cov, clip_norm,
+                     use_rank_weight=True, lr=0.1, n_items=None):
+    """One CML step (cml.py:55-129; = cf_oracle.cml_step) on the float64 tables
+    in place, and E advanced to bound the float32 result.
+
+    CML has discontinuities: the hinge (z > 0), the rank weight's indicators
+    (dp - dn_w + margin > 0) and the argmin's ties (TF's _MinOrMaxGrad splits
+    the gradient among exact ties).  A pair whose z, indicators or minimum are
+    within their own rounding bound of a threshold may legitimately take
+    either branch in fp32: every row it touches gets E = inf (excluded from
+    the check; the tests assert how few there are).  Otherwise the branches
+    are those of the float64 step and the bound follows the BPR one.
+    Magnitudes of the item gradients count |U_u| + |V| (not the difference
+    U_u - V) so that the item-record form alpha U_u + beta V is
+    covered.  Returns the pre-update loss."""
+    pairs = np.asarray(pairs)
+    Bn = pairs.shape[0]
+    negs = np.asarray(negs).reshape(Bn, -1)
+    W = negs.shape[1]
+    d = U.shape[1]
+    if n_items is None:
+        n_items = V.shape[0]
+    u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+    Uu, Vi, Vj = U[u_idx], V[i_idx], V[negs]
+    eU, eVi, eVj = E["user"][u_idx], E["item"][i_idx], E["item"][negs]
+    du = Uu - Vi
+    e_du = eU + eVi + U32 * np.abs(du)
+    dp = np.sum(du * du, axis=1)
+    e_dp = np.sum((2.0 * np.abs(du) + e_du) * e_du, axis=1) + gamma(d) * np.sum((np.abs(du) + e_du) ** 2, axis=1)
+    dnv = Uu[:, None, :] - Vj
+    e_dnv = eU[:, None, :] + eVj + U32 * np.abs(dnv)
+    dn = np.sum(dnv * dnv, axis=-1)
+    e_dn = (np.sum((2.0 * np.abs(dnv) + e_dnv) * e_dnv, axis=-1)
+            + gamma(d) * np.sum((np.abs(dnv) + e_dnv) ** 2, axis=-1))
+    m = dn.min(axis=1)
+    e_m = e_dn.max(axis=1)
+    # branch ambiguity
+    amb = np.zeros(Bn, dtype=bool)
+    t = dp[:, None] - dn + margin
+    e_t = e_dp[:, None] + e_dn + 2.0 * U32 * (dp[:, None] + dn + abs(margin))
+    if use_rank_weight:
+        amb |= np.any(np.abs(t) <= e_t, axis=1)
+    z = dp - m + margin
+    e_z = e_dp + e_m + 2.0 * U32 * (dp + m + abs(margin))
+    amb |= np.abs(z) <= e_z
+    ties = dn == m[:, None]
+    near = (np.abs(dn - m[:, None]) <= e_dn + e_m[:, None]) & ~ties
+    amb |= np.any(near, axis=1)
+    if use_rank_weight:
+        imp = (t > 0).astype(np.float64)
+        r = imp.mean(axis=1) * n_items
+        lw = np.log(r + 1.0)
+        e_lw = 3.0 * U32 + 2.0 * U32 * np.abs(lw)
+    else:
+        lw = np.ones(Bn)
+        e_lw = np.zeros(Bn)
+    loss = np.sum(np.maximum(z, 0.0) * lw)
+    pos = z > 0
+    a = pos * lw
+    e_a = pos * e_lw
+    cnt = ties.sum(axis=1, keepdims=True).astype(np.float64)
+    share = ties / cnt
+    e_share = U32 * share
+    coef = 2.0 * a[:, None] * share                                   # [B,W]
+    e_coef = 2.0 * (e_a[:, None] * share + a[:, None] * e_share) + 2.0 * U32 * coef
+    rc = reg_cov if reg_cov > 0 else 0.0
+    A2, eA2 = 2.0 * a[:, None], 2.0 * e_a[:, None]
+    mU, mVi, mVj = np.abs(Uu) + eU, np.abs(Vi) + eVi, np.abs(Vj) + eVj
+    # gradients (cf_oracle.cml_step) and their bounds
+    gU = A2 * du - (coef[:, :, None] * dnv).sum(axis=1) + rc * Uu
+    eGU = (eA2 * np.abs(du) + A2 * e_du
+           + (e_coef[:, :, None] * np.abs(dnv) + coef[:, :, None] * e_dnv).sum(axis=1) + rc * eU
+           + gamma(W + 4) * ((A2 + eA2) * (mU + mVi)
+                             + ((coef + e_coef)[:, :, None] * (mU[:, None, :] + mVj)).sum(axis=1) + rc * mU))
+    gVi = -A2 * du + rc * Vi
+    eGVi = (eA2 * np.abs(du) + A2 * e_du + rc * eVi
+            + gamma(4) * ((A2 + eA2) * (mU + mVi) + rc * mVi))
+    gVj = coef[:, :, None] * dnv + rc * Vj
+    eGVj = (e_coef[:, :, None] * np.abs(dnv) + coef[:, :, None] * e_dnv + rc * eVj
+            + gamma(4) * ((coef + e_coef)[:, :, None] * (mU[:, None, :] + mVj) + rc * mVj))
+    if rc > 0:
+        loss += rc * 0.5 * (np.sum(Uu * Uu) + np.sum(Vi * Vi) + np.sum(Vj * Vj))
+    # an ambiguous pair's rows: no bound (nor where a carried inf met a 0)
+    eGU, eGVi, eGVj = (np.nan_to_num(x, nan=np.inf) for x in (eGU, eGVi, eGVj))
+    eGU[amb] = np.inf
+    eGVi[amb] = np.inf
+    eGVj[amb] = np.inf
+    _dedup_adagrad_bounded(U, AU, E["user"], E["acc_user"], u_idx, gU, eGU, lr)
+    _dedup_adagrad_bounded(V, AV, E["item"], E["acc_item"], np.concatenate([i_idx, negs.reshape(-1)]),
+                           np.concatenate([gVi, gVj.reshape(-1, d)]),
+                           np.concatenate([eGVi, eGVj.reshape(-1, d)]), lr)
+    _clip_bounded(U, E["user"], clip_norm)
+    _clip_bounded(V, E["item"], clip_norm)
+    return float(loss)

@@ -78,7 +78,7 @@ BPR_TABLES = ("user", "item", "acc_user", "acc_item")
 
 
 class LocalStepCheck:
-    """Step-local parity of the BPR / AMF step.
+    """Step-local parity of the BPR / AMF / CML step.
 
     Before each engine step, ``before(e)`` reads the engine's own float32
     tables; ``after(e, pairs, negs, loss)`` runs the float64 oracle one step
@@ -86,11 +86,18 @@ class LocalStepCheck:
     oracle/fp32_bound.py, and requires every element of every table within E
     (untouched rows bit-identical) and the loss within 1e-5.  No constant in
     E is fitted to a GPU result; a hot row with one occurrence dropped or
-    added twice lands 7-28x outside it (tests/test_fp32_bound.py)."""
+    added twice lands 7-29x outside it (tests/test_fp32_bound.py).  CML: a
+    pair within rounding of one of its branch thresholds (hinge, rank-weight
+    indicators, argmin ties) may take either branch in fp32, so its rows are
+    excluded (E = inf) -- at most ``max_excluded`` of the touched rows."""
 
-    def __init__(self, reg, adversarial=None, reg_adv=1.0):
+    def __init__(self, reg=None, adversarial=None, reg_adv=1.0, model="bpr", max_excluded=0.01, **cml):
+        self.model = model
         self.reg, self.adversarial, self.reg_adv = reg, adversarial, reg_adv
+        self.cml = cml
+        self.max_excluded = max_excluded
         self.worst = 0.0
+        self.excluded = 0
         self.T = None
 
     def before(self, e):
@@ -101,18 +108,26 @@ class LocalStepCheck:
         from oracle import fp32_bound as FB
         L = {t: self.T[t].astype(np.float64) for t in BPR_TABLES}
         E = FB.zero_bounds(L["user"], L["item"], acc_exact=True)
-        lo = FB.bpr_step_bounded(L["user"], L["item"], L["acc_user"], L["acc_item"], E,
-                                 np.asarray(pairs), np.asarray(negs), self.reg,
-                                 adversarial=self.adversarial, reg_adv=self.reg_adv)
+        args = (L["user"], L["item"], L["acc_user"], L["acc_item"], E, np.asarray(pairs), np.asarray(negs))
+        if self.model == "cml":
+            lo = FB.cml_step_bounded(*args, **self.cml)
+        else:
+            lo = FB.bpr_step_bounded(*args, self.reg, adversarial=self.adversarial, reg_adv=self.reg_adv)
         assert abs(loss - lo) <= 1e-5 * abs(lo) + 1e-6, (what, loss, lo)
         self.T = {t: e.get_table(t) for t in BPR_TABLES}
         for t in BPR_TABLES:
-            self.worst = max(self.worst, assert_within(self.T[t], L[t], E[t], "%s local %s" % (what, t)))
+            fin = np.isfinite(E[t])
+            touched = (E[t] != 0).any(axis=1)
+            bad_rows = (~fin).any(axis=1)
+            self.excluded += int(bad_rows.sum())
+            assert bad_rows.sum() <= max(2, self.max_excluded * touched.sum()), (what, t, int(bad_rows.sum()))
+            self.worst = max(self.worst, assert_within(self.T[t][~bad_rows], L[t][~bad_rows], E[t][~bad_rows],
+                                                       "%s local %s" % (what, t)))
         log = os.environ.get("CF_BOUND_LOG")
-        if log:   # the worst |gpu - oracle| / E so far, per test (DESIGN 4)
+        if log:   # the worst |gpu - oracle| / E so far, per test (DESIGN 4.1)
             with open(log, "a") as f:
-                f.write("%s %s %.4f\n" % (os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], what,
-                                         self.worst))
+                f.write("%s %s %.4f %d\n" % (os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], what,
+                                            self.worst, self.excluded))
         return lo
 
 

@@ -179,3 +179,67 @@ def test_forward_bound_covers_fp32_trajectory(streams):
         FB.bpr_step_bounded(*L, E, st["pairs"][s], st["negs"][s], 0.1)
         for q, k in enumerate(FB.TABLES):
             assert (np.abs(T[q].astype(np.float64) - L[q]) <= E[k]).all(), (s, k)
+
+
+def _cml_local(before, after, pairs, negs, **hp):
+    L = [t.astype(np.float64) for t in before]
+    E = FB.zero_bounds(L[0], L[1], acc_exact=True)
+    FB.cml_step_bounded(*L, E, pairs, negs, **hp)
+    worst, excluded = 0.0, 0
+    for q, k in enumerate(FB.TABLES):
+        err = np.abs(after[q].astype(np.float64) - L[q])
+        fin = np.isfinite(E[k])
+        excluded += int((~fin).any(axis=1).sum())
+        assert np.all(err[fin & (E[k] == 0)] == 0), k
+        nz = fin & (E[k] > 0)
+        if nz.any():
+            worst = max(worst, float((err[nz] / E[k][nz]).max()))
+    return worst, excluded, L, E
+
+
+CML_HP = dict(margin=1.0, reg_cov=1.0, clip_norm=1.0, use_rank_weight=True)
+
+
+@pytest.mark.parametrize("name,d", [("rank_b50_w5", 50), ("rank_b100_w5", 128)])
+def test_cml_bound_holds_on_reference_streams(streams, name, d):
+    """The float32 oracle's CML steps (hinge, rank weight, argmin, clip of
+    every row) stay inside the local bound, and no pair is near a branch."""
+    st = get_stream(streams, name)
+    rng = np.random.RandomState(3)
+    T = [O.init_table(rng, (943, d), truncated=False), O.init_table(rng, (1682, d), truncated=False),
+         np.full((943, d), 0.1, np.float32), np.full((1682, d), 0.1, np.float32)]
+    worst = 0.0
+    for s in range(20):
+        before = [t.copy() for t in T]
+        O.cml_step(*T, st["pairs"][s], st["negs"][s], **CML_HP)
+        w, excluded, _, _ = _cml_local(before, T, st["pairs"][s], st["negs"][s], **CML_HP)
+        assert excluded == 0
+        worst = max(worst, w)
+    assert worst <= 1.0, worst
+
+
+def test_cml_bound_catches_one_occurrence_on_a_hot_row():
+    """A CML item negative in 300 pairs: one of its occurrences dropped from
+    the dedup-sum lands outside the bound."""
+    rng = np.random.RandomState(8)
+    nu, ni, d, B, W = 400, 300, 16, 600, 5
+    T = [O.init_table(rng, (nu, d), truncated=False), O.init_table(rng, (ni, d), truncated=False),
+         np.full((nu, d), 0.1, np.float32), np.full((ni, d), 0.1, np.float32)]
+    pairs = np.stack([rng.randint(nu, size=B), rng.randint(ni, size=B)], 1).astype(np.int32)
+    negs = rng.randint(ni, size=(B, W)).astype(np.int32)
+    negs[:300, 0] = 7
+    before = [t.copy() for t in T]
+    # the float32 step with one occurrence of item 7 missing from its sum
+    U, V, AU, AV = T
+    keep = np.ones(B, dtype=bool)
+    keep[int(rng.randint(300))] = False
+    L32 = [t.copy() for t in before]
+    O.cml_step(*L32, pairs, negs, **CML_HP)                       # the correct float32 step
+    T2 = [t.copy() for t in before]
+    O.cml_step(*T2, pairs[keep], negs[keep], **CML_HP)            # item 7 loses one occurrence
+    w_ok, _, L, E = _cml_local(before, L32, pairs, negs, **CML_HP)
+    assert w_ok <= 1.0
+    # the row itself barely moves (Adagrad's first step is ~lr * sign(G) for a
+    # large summed G, then the clip), its accumulator G^2 does
+    ratio = np.abs(T2[3][7].astype(np.float64) - L[3][7]) / E["acc_item"][7]
+    assert ratio.max() > 3.0, ratio.max()

@@ -66,10 +66,12 @@ def run_steps(model, fold1, batches, d, opts, amf_switch=None, forward_bound=Fal
     U64, V64 = U.astype(np.float64), V.astype(np.float64)
     AU, AV = np.full_like(U64, 0.1), np.full_like(V64, 0.1)
     E = FB.zero_bounds(U64, V64) if forward_bound else None
-    local = None
     if model in ("bpr", "amf"):
         local = LocalStepCheck(kw["reg"], adversarial=None if model == "bpr" else False,
                                reg_adv=kw.get("reg_adv", 1.0))
+    else:
+        local = LocalStepCheck(model="cml", margin=kw["margin"], reg_cov=kw["reg_cov"],
+                               clip_norm=kw["clip_norm"], use_rank_weight=kw["use_rank_weight"])
     adv = False
     for s, (pairs, negs) in enumerate(batches):
         if amf_switch is not None and s == amf_switch:
@@ -78,11 +80,9 @@ def run_steps(model, fold1, batches, d, opts, amf_switch=None, forward_bound=Fal
             AU[...] = 0.1
             AV[...] = 0.1
             local.T, local.adversarial = None, True
-        if local is not None:
-            local.before(e)
+        local.before(e)
         lg = e.step(pairs, negs)
-        if local is not None:
-            local.after(e, pairs, negs, lg, "step %d" % s)
+        local.after(e, pairs, negs, lg, "step %d" % s)
         if model == "bpr":
             if E is not None:
                 lo = FB.bpr_step_bounded(U64, V64, AU, AV, E, pairs, negs, kw["reg"])
