@@ -361,6 +361,9 @@ def main():
                     help="cf_set_option bias_slots (GBPR item bias: 1 slots, 0 atomics; -1 default)")
     ap.add_argument("--pos-sort", type=int, default=-1,
                     help="cf_set_option pos_sort (gradient pairs in positive-item order; -1 default)")
+    ap.add_argument("--item-pieces", type=int, default=-1,
+                    help="the multi-rank item reduce + all-reduce in this many pieces of item rows "
+                         "(-1 = auto: 4 at N > 1 with the all-reduce exchange, else 1)")
     ap.add_argument("--spec-neg", type=int, default=-1,
                     help="cf_set_option spec_neg (speculative negative counts in the pos_sort draw)")
     ap.add_argument("--pair-prefetch", type=int, default=-1,
@@ -511,8 +514,13 @@ def main():
                                                exchange=args.item_exchange, item_csr=item_csr)
         del item_csr
     elif sharded:
+        pieces = args.item_pieces
+        if pieces < 0:   # piece q's all-reduce runs while piece q+1 is reduced
+            pieces = 4 if (world > 1 and args.item_exchange == "allreduce" and cfg["model"] != "gbpr") else 1
         step, _items = make_gpu_sharded(eng, ni, d, cfg["model"] == "gbpr",
-                                        torch.device("cuda", local_rank), exchange=args.item_exchange)
+                                        torch.device("cuda", local_rank), exchange=args.item_exchange,
+                                        pieces=pieces)
+        dist_pieces = pieces
     if sharded:
         def run(k, b=B):
             for _ in range(k):
@@ -667,6 +675,7 @@ def main():
     if sharded:
         dist_info = {"world_size_formed": dist.get_world_size(), "backend": dist.get_backend(),
                      "item_exchange": args.item_exchange,
+                     "item_pieces": locals().get("dist_pieces", 1),
                      "launched_by_bench": os.environ.get("CF_BENCH_LAUNCHED") == "1"}
     out = {
         "metric": "BPR triplets/sec/GPU (d=64) + achieved HBM GB/s; NDCG@10 vs ref",

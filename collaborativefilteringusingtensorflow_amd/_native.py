@@ -97,6 +97,8 @@ SIGNATURES = {
     "cf_bind_table": (ctypes.c_int, [_P, _I32, _P, _I64]),
     "cf_step_local_grad": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_step_local_apply": (ctypes.c_int, [_P, _I32]),
+    "cf_step_item_reduce": (ctypes.c_int, [_P, _I32]),
+    "cf_item_piece_rows": (ctypes.c_int, [_P, _I32, _I32, _PI64, _PI64]),
     "cf_take_loss": (ctypes.c_int, [_P, _PD]),
     "cf_step_plr": (ctypes.c_int, [_P, _PI32, _I32, _PF, _I32, _PD]),
     "cf_set_shard": (ctypes.c_int, [_P, _I32, _I32, _PI64]),

@@ -195,6 +195,12 @@ struct cf_engine {
     int lg_stage = 0;
     StepArgs lg_args{};
     int lg_set = 0, lg_B = 0;
+    // the multi-rank item reduce in pieces (cf_set_option "item_pieces"):
+    // cf_step_item_reduce(q, P) reduces item rows piece q; lg_pieces_left of
+    // the current local step are still to come
+    int item_pieces = 1;
+    int lg_pieces_left = 0;
+    bool lg_pieces_deferred = false;
     bool pend = false;
     StepArgs pend_args{};
     int pend_set = 0, pend_B = 0;
@@ -816,6 +822,8 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
         p.dense_users = 0;
     }
     p.n_users = c.n_users;
+    p.item_r0 = 0;
+    p.item_r1 = c.n_items;
     if (e->det && a.cntP == nullptr) {
         p.hotP = e->hotP;
         p.hotPb = e->hotPb;
@@ -1692,13 +1700,22 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
     CF_TRY(det_hot(e, a));
     e->last_occV = a.occV;
     e->last_nV = (int64_t)B * items_per_pair(e->cfg);
+    e->lg_pieces_left = 0;
+    e->lg_pieces_deferred = false;
     if (a.items_grad_only && a.capV > 0) {
         // duplicated item rows: slot rows summed into the bound buffer now, so
         // it holds this rank's complete item gradient when the all-reduce starts
         ApplyArgs p = apply_args(e, a, B, k, nullptr);
         p.count_users = 0;
-        ProfScope ps(e, CF_K_ITEM_REDUCE);
-        CF_HIP(launch_apply(p, e->stream));
+        if (e->item_pieces > 1 && p.dense_items) {
+            // in pieces of item rows, each launched by cf_step_item_reduce just
+            // before the caller's collective of that piece
+            e->lg_pieces_left = e->item_pieces;
+            e->lg_pieces_deferred = true;
+        } else {
+            ProfScope ps(e, CF_K_ITEM_REDUCE);
+            CF_HIP(launch_apply(p, e->stream));
+        }
     }
     e->lg_args = a;
     e->lg_set = k;
@@ -1707,9 +1724,47 @@ int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int3
     return CF_OK;
 }
 
+// item rows [piece * chunk, (piece + 1) * chunk) of the local step's item
+// reduce, chunk = n_items / n_pieces rounded up to 16 (kGroupsPerBlock)
+static void piece_rows(int64_t n_items, int piece, int n_pieces, int64_t* r0, int64_t* r1) {
+    int64_t chunk = (n_items + n_pieces - 1) / n_pieces;
+    chunk = (chunk + kGroupsPerBlock - 1) / kGroupsPerBlock * kGroupsPerBlock;
+    *r0 = std::min<int64_t>((int64_t)piece * chunk, n_items);
+    *r1 = std::min<int64_t>(*r0 + chunk, n_items);
+}
+
+int cf_item_piece_rows(cf_engine* e, int32_t piece, int32_t n_pieces, int64_t* row0, int64_t* row1) {
+    CF_TRY(check_engine(e));
+    if (n_pieces < 1 || piece < 0 || piece >= n_pieces || !row0 || !row1) return fail(CF_EINVAL, "bad piece");
+    piece_rows(e->cfg.n_items, piece, n_pieces, row0, row1);
+    return CF_OK;
+}
+
+int cf_step_item_reduce(cf_engine* e, int32_t piece) {
+    CF_TRY(check_engine(e));
+    if (e->lg_stage != 1) return fail(CF_ESTATE, "cf_step_local_grad must come first");
+    const int P = e->item_pieces;
+    if (piece < 0 || piece >= P) return fail(CF_EINVAL, "piece must be 0 .. item_pieces-1");
+    // the local step reduced its items whole (item_pieces 1, or not the
+    // dense pos_sort apply): every piece is already complete
+    if (!e->lg_pieces_deferred) return CF_OK;
+    if (piece != P - e->lg_pieces_left) return fail(CF_ESTATE, "item-reduce pieces run in order 0 .. item_pieces-1");
+    ApplyArgs p = apply_args(e, e->lg_args, e->lg_B, e->lg_set, nullptr);
+    p.count_users = 0;
+    piece_rows(e->cfg.n_items, piece, P, &p.item_r0, &p.item_r1);
+    if (p.item_r1 > p.item_r0) {
+        ProfScope ps(e, CF_K_ITEM_REDUCE);
+        CF_HIP(launch_apply(p, e->stream));
+    }
+    e->lg_pieces_left -= 1;
+    return CF_OK;
+}
+
 int cf_step_local_apply(cf_engine* e, int32_t next_B) {
     CF_TRY(check_engine(e));
     if (e->lg_stage != 1) return fail(CF_ESTATE, "cf_step_local_grad must come first");
+    if (e->lg_pieces_left > 0)
+        return fail(CF_ESTATE, "cf_step_item_reduce pieces of this step are still pending");
     if (next_B < 0) return fail(CF_EINVAL, "next_B must be >= 0");
     const int k = e->lg_set;
     ApplyArgs p = apply_args(e, e->lg_args, e->lg_B, k, e->loss);
@@ -2270,6 +2325,12 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     if (n == "topk_path") {
         if (value < 0 || value > 2) return fail(CF_EINVAL, "topk_path must be 0, 1 or 2");
         e->topk_path = (int)value;
+        return CF_OK;
+    }
+    if (n == "item_pieces") {   // the multi-rank item reduce in pieces (cf_step_item_reduce)
+        if (value < 1 || value > 64) return fail(CF_EINVAL, "item_pieces must be 1 .. 64");
+        if (e->lg_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+        e->item_pieces = (int)value;
         return CF_OK;
     }
     if (n == "spec_neg") {   // speculative negative counts in the pos_sort draw (StepArgs::spec_ph)

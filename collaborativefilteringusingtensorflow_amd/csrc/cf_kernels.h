@@ -271,6 +271,9 @@ struct ApplyArgs {
     // (dense_users) instead of finding the owners among the occurrences --
     // when the table is not much larger than the batch's occurrences of it
     int dense_items, dense_users;
+    // dense item rows [item_r0, item_r1) only (the multi-rank item reduce in
+    // pieces, cf_step_item_reduce; default the whole table)
+    int64_t item_r0, item_r1;
     int64_t n_users;
     int32_t* __restrict__ cntU;
     int32_t* __restrict__ cntV;

@@ -178,6 +178,8 @@ bool grad_lds(const StepArgs& a) { return lds_path(a); }
 
 int grad_blocks(const StepArgs& a, bool with_draw) {
     if (!with_draw && lds_path(a)) return (a.B + kGroupsPerBlock - 1) / kGroupsPerBlock;
+    if (a.srec != nullptr)   // grad_sort_kernel: CF_SORT_TILES tiles of kPsortPPB positions per block
+        return (a.B + CF_SORT_TILES * kPsortPPB - 1) / (CF_SORT_TILES * kPsortPPB);
     const int fw = fast_w(a);
     const int B = a.B;
     const int gpb = (CF_GRAD_WAVE_BLOCKS && !with_draw) ? kWave / kGL : kGroupsPerBlock;
@@ -249,7 +251,8 @@ template <bool PS = true, bool FX = false>
 static hipError_t launch_apply_ps_t(const ApplyArgs& p, const StepArgs* nx, hipStream_t s) {
     const int64_t nUw = !p.count_users ? 0 : p.dense_users ? p.n_users : p.nU;
     const int64_t nVw = (p.count_items && !p.dense_items) ? p.nV : 0;
-    const int64_t nbI64 = (p.count_items && p.dense_items) ? (p.n_items + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
+    const int64_t nbI64 = (p.count_items && p.dense_items)
+                              ? (p.item_r1 - p.item_r0 + kGroupsPerBlock - 1) / kGroupsPerBlock : 0;
     const int64_t nbW64 = (nUw + nVw + kBlock - 1) / kBlock;
     const int np = prep_blocks(nx);
     if (nbI64 + nbW64 + np > INT32_MAX) return hipErrorInvalidValue;

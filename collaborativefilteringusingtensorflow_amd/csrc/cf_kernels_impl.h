@@ -393,7 +393,10 @@ constexpr int kPrepChunks = CF_PREP_CHUNKS;
 #ifndef CF_PREP_GL_W1
 #define CF_PREP_GL_W1 4
 #endif
-__host__ __device__ constexpr int prep_chunks(int pgl) { return pgl == kPrepGL ? kPrepChunks : 64 / pgl; }
+#ifndef CF_PREP_CHUNKS_W1
+#define CF_PREP_CHUNKS_W1 (64 / CF_PREP_GL_W1)
+#endif
+__host__ __device__ constexpr int prep_chunks(int pgl) { return pgl == kPrepGL ? kPrepChunks : CF_PREP_CHUNKS_W1; }
 // row scan in 16-B loads (4 ids per lane per chunk): measured SLOWER at cfg2
 // (same box, r03: draw alone 183 vs 119 us, 0.489 vs 0.399 ms/step;
 // profiles/r03/ab_draw_vec_sortw.txt) -- the masked 4 x 8 compare per chunk
@@ -1773,10 +1776,13 @@ __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MOD
 
 template <int MODEL, int EPL, int WT, int P, int GPB = kGroupsPerBlock, bool SORT = false, bool FX = false>
 __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
-    static_assert(!SORT || (P == 1 && MODEL != GBPR && GPB == kPsortPPB), "pos_sort: one pair per group");
+    // pos_sort: P positive-sorted tiles of GPB positions per block (pair k of
+    // group grp is position (block P + k) GPB + grp), each tile with its own
+    // LDS run sums, so P tiles' rows are in flight before the first computes
+    static_assert(!SORT || (MODEL != GBPR && GPB == kPsortPPB), "pos_sort: tiles of kPsortPPB positions");
     __shared__ double s_loss[GPB];
-    __shared__ float s_gi[SORT ? GPB : 1][SORT ? kGL * EPL : 1];
-    __shared__ int s_item[SORT ? GPB : 1];
+    __shared__ float s_gi[SORT ? P * GPB : 1][SORT ? kGL * EPL : 1];
+    __shared__ int s_item[SORT ? P * GPB : 1];
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
     float loss_g = 0.f;
@@ -1836,15 +1842,20 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
         if (ok[k]) pr[k].template load_acc<SORT>(a, gl);
 #pragma unroll
     for (int k = 0; k < P; ++k)
-        if (ok[k]) pr[k].template update<SORT>(a, gl, loss_g, sq, SORT ? &s_gi[grp][0] : nullptr);
+        if (ok[k]) pr[k].template update<SORT>(a, gl, loss_g, sq, SORT ? &s_gi[k * GPB + grp][0] : nullptr);
     if constexpr (SORT) {
         // psort consumed this buffer set's phantoms: re-zero the count for
         // the set's next draw (StepArgs::spec_ph)
         if (block == 0 && threadIdx.x == 0 && a.spec_n != nullptr) *a.spec_n = 0;
-        if (gl == 0) s_item[grp] = ok[0] ? pr[0].i : -1;
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (gl == 0) s_item[k * GPB + grp] = ok[k] ? pr[k].i : -1;
         __syncthreads();
-        if (ok[0] && (grp == 0 || s_item[grp - 1] != pr[0].i))
-            psort_head<MODEL, EPL, WT, GPB, FX>(a, pr[0], block, grp, gl, s_gi, s_item);
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (ok[k] && (grp == 0 || s_item[k * GPB + grp - 1] != pr[k].i))
+                psort_head<MODEL, EPL, WT, GPB, FX>(a, pr[k], block * P + k, grp, gl, s_gi + k * GPB,
+                                                    s_item + k * GPB);
     }
 
     const float coef = (MODEL == CML) ? (a.reg_cov > 0.f ? a.reg_cov : 0.f) : a.reg;
@@ -1888,9 +1899,13 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #ifndef CF_SORT_MIN_WAVES
 #define CF_SORT_MIN_WAVES 1
 #endif
+// CF_SORT_TILES positive-sorted tiles per block (grad_fast_body)
+#ifndef CF_SORT_TILES
+#define CF_SORT_TILES 1
+#endif
 template <int MODEL, int EPL, int WT, bool FX = false>
 __global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a) {
-    grad_fast_body<MODEL, EPL, WT, 1, kGroupsPerBlock, true, FX>(a, blockIdx.x);
+    grad_fast_body<MODEL, EPL, WT, CF_SORT_TILES, kGroupsPerBlock, true, FX>(a, blockIdx.x);
 }
 
 // the same gradient blocks at one wave per workgroup (no draw blocks): a
@@ -2706,8 +2721,8 @@ __device__ __forceinline__ void fold_loss(const ApplyArgs& a) {
 template <int EPL, bool FX>
 __device__ __forceinline__ void apply_ps_item_block(const ApplyArgs& a, int block) {
     const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
-    const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
-    if (r >= a.n_items) return;
+    const int64_t r = a.item_r0 + (int64_t)block * kGroupsPerBlock + grp;
+    if (r >= a.item_r1) return;
     const int2 o0 = a.offPN[r], o1 = a.offPN[r + 1];
     const int cp = o1.x - o0.x, cn = o1.y - o0.y;
     if (cn + cp < 2) return;   // untouched, or seen once (applied by the gradient launch)
@@ -2775,8 +2790,8 @@ __device__ __forceinline__ void apply_ps_wave(const ApplyArgs& a, int64_t wave) 
 template <int EPL>
 __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int block) {
     const int grp = threadIdx.x >> 4, gl = threadIdx.x & (kGL - 1);
-    const int64_t r = (int64_t)block * kGroupsPerBlock + grp;
-    if (r >= a.n_items) return;
+    const int64_t r = a.item_r0 + (int64_t)block * kGroupsPerBlock + grp;
+    if (r >= a.item_r1) return;
     const int c = a.cntV[r];
     if (c < 2) return;   // untouched, or seen once (applied by the gradient launch)
     apply_row<EPL>(a, r, false, c, gl);
@@ -3198,7 +3213,7 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
     if constexpr (MODEL != GBPR && P == 1) {
         if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
             if (np > 0) return hipErrorInvalidValue;
-            const dim3 sgrid(ng);
+            const dim3 sgrid((a.B + CF_SORT_TILES * kPsortPPB - 1) / (CF_SORT_TILES * kPsortPPB));
             if (a.det_fx) {   // deterministic: fixed-point partials and loss
                 switch (epl_for(a.d)) {
                     case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT, true>), sgrid, block, 0, s, a); break;

@@ -74,14 +74,31 @@ class AllReduceItems(object):
     name = "allreduce"
     draw_with_apply = True   # the next draw rides in the user-apply launch
 
-    def __init__(self, grad, group=None):
+    def __init__(self, grad, group=None, pieces=1, row_width=None, n_rows=None):
         self.grad = grad
         self.group = group
+        # the item reduce in pieces of item rows (cf_step_item_reduce): piece
+        # q's all-reduce is issued as soon as that piece is reduced, so it runs
+        # while the next piece reduces; rows of row_width elements, then a
+        # tail (GBPR's item bias) reduced with the last piece
+        self.pieces = int(pieces)
+        self.row_width = row_width
+        self.n_rows = n_rows
 
     def overlap(self, dist):
         return self.grad.is_cuda and dist.get_backend(self.group) != "gloo"
 
-    def reduce(self, dist, async_op):
+    def reduce(self, dist, async_op, be=None):
+        if self.pieces > 1 and be is not None and hasattr(be, "step_item_reduce"):
+            w, works = self.row_width, []
+            for q in range(self.pieces):
+                be.step_item_reduce(q)
+                r0, r1 = be.item_piece_rows(q, self.pieces)
+                if r1 > r0:
+                    works.append(dist.all_reduce(self.grad[r0 * w:r1 * w], group=self.group, async_op=async_op))
+            if self.grad.numel() > self.n_rows * w:   # the bias tail
+                works.append(dist.all_reduce(self.grad[self.n_rows * w:], group=self.group, async_op=async_op))
+            return _Works(works if async_op else [])
         return dist.all_reduce(self.grad, group=self.group, async_op=async_op)
 
     def apply(self, be):
@@ -150,7 +167,7 @@ class ReduceScatterItems(object):
         # in place: this rank's chunk of the output is the input
         return dist.all_gather_into_tensor(full, full[lo:hi], group=self.group, async_op=async_op)
 
-    def reduce(self, dist, async_op):
+    def reduce(self, dist, async_op, be=None):
         w = [self._rs(dist, self.grad_slice, self.grad, async_op)]
         if self.grad_bias is not None:
             w.append(self._rs(dist, self.bias_slice, self.grad_bias, async_op))
@@ -218,7 +235,7 @@ class ShardedStep(object):
         # GPU), so only RCCL gets the asynchronous collectives
         overlap = x.overlap(dist)
         nb = batch_size if (pairs is None and self.draw_ahead) else 0
-        work = x.reduce(dist, overlap)
+        work = x.reduce(dist, overlap, be)
         be.step_local_apply(nb if x.draw_with_apply else 0)
         if overlap and work is not None:
             work.wait()
@@ -278,12 +295,14 @@ def _bind_rs_items(engine, n_items, d, with_bias, device, group=None):
     return items
 
 
-def make_gpu_sharded(engine, n_items, d, with_bias, device, exchange="allreduce", process_group=None):
+def make_gpu_sharded(engine, n_items, d, with_bias, device, exchange="allreduce", process_group=None,
+                     pieces=1):
     """Bind the item-gradient buffer(s) to the engine, run the engine on
     torch's current stream so RCCL orders after it, and return the step
     callable and its item exchange.  ``exchange``: "allreduce" (dense
     all-reduce + replicated item Adagrad) or "rs_ag" (reduce-scatter ->
-    owner Adagrad -> all-gather)."""
+    owner Adagrad -> all-gather).  ``pieces`` > 1 (allreduce): the item
+    reduce and its all-reduce in that many pieces of item rows."""
     import torch
     share_stream(engine, device)
     if exchange == "rs_ag":
@@ -292,7 +311,9 @@ def make_gpu_sharded(engine, n_items, d, with_bias, device, exchange="allreduce"
         n = n_items * d + (n_items if with_bias else 0)
         grad = torch.zeros(n, dtype=torch.float32, device=device)
         engine.bind_item_grad(grad.data_ptr(), n)
-        items = AllReduceItems(grad, process_group)
+        if pieces > 1:
+            engine.set_option("item_pieces", pieces)
+        items = AllReduceItems(grad, process_group, pieces=pieces, row_width=d, n_rows=n_items)
     else:
         raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
     return ShardedStep(engine, items, process_group), items
@@ -540,7 +561,9 @@ def make_gpu_group_exchange(engine, world, rank, bounds, indptr, indices, n_item
         n = n_items * d + n_items
         grad = torch.zeros(n, dtype=torch.float32, device=device)
         engine.bind_item_grad(grad.data_ptr(), n)
-        items = AllReduceItems(grad, process_group)
+        if pieces > 1:
+            engine.set_option("item_pieces", pieces)
+        items = AllReduceItems(grad, process_group, pieces=pieces, row_width=d, n_rows=n_items)
     else:
         raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
     ip_t, ix_t = item_csr if item_csr is not None else item_users(indptr, indices, n_items)

@@ -270,6 +270,18 @@ class Engine(object):
     def step_local_apply(self, next_batch_size=0):
         N.check(self._L.cf_step_local_apply(self._h, int(next_batch_size)), "cf_step_local_apply")
 
+    def step_item_reduce(self, piece):
+        """Piece `piece` of the local step's item reduce (cf_set_option
+        "item_pieces" > 1; include/cf_engine.h cf_step_item_reduce)."""
+        N.check(self._L.cf_step_item_reduce(self._h, int(piece)), "cf_step_item_reduce")
+
+    def item_piece_rows(self, piece, n_pieces):
+        """Item rows [row0, row1) of piece `piece` of n_pieces."""
+        r0, r1 = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._L.cf_item_piece_rows(self._h, int(piece), int(n_pieces), ctypes.byref(r0),
+                                           ctypes.byref(r1)), "cf_item_piece_rows")
+        return int(r0.value), int(r1.value)
+
     def step_items(self):
         N.check(self._L.cf_step_items(self._h), "cf_step_items")
 

@@ -251,6 +251,18 @@ int cf_step_local(cf_engine* eng, int32_t B, const int32_t* host_pairs,
 int cf_step_local_grad(cf_engine* eng, int32_t B, const int32_t* host_pairs,
                        const int32_t* host_negs, const int32_t* host_groups);
 int cf_step_local_apply(cf_engine* eng, int32_t next_B);
+/* The item reduce of cf_step_local_grad in pieces (round 4):
+ * with cf_set_option("item_pieces", P > 1) on the pos_sort path,
+ * cf_step_local_grad leaves the duplicated item rows unsummed and the caller
+ * runs cf_step_item_reduce(eng, q) for q = 0 .. P-1, in order, each followed
+ * by the all-reduce of that piece's rows [row0, row1) of the bound buffer
+ * (cf_item_piece_rows), so piece q's collective runs while piece q+1 is
+ * reduced.  cf_step_local_apply fails with CF_ESTATE while pieces are left.
+ * Replaces the reduce inside cf_step_local_grad (the same launch, cut by item
+ * rows; TF1 sums every duplicate before the update, gbprmf.py:101-106,
+ * bprmf.py:83-88). */
+int cf_step_item_reduce(cf_engine* eng, int32_t piece);
+int cf_item_piece_rows(cf_engine* eng, int32_t piece, int32_t n_pieces, int64_t* row0, int64_t* row1);
 /* Phase 2, after the buffer holds the cross-rank sum: dense item Adagrad
  * (and CML clip of updated rows); zeroes the buffer. */
 int cf_step_items(cf_engine* eng);
@@ -459,6 +471,8 @@ int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                and takes every sum of gradient rows in 64-bit fixed point
  *                (2^-32 units; int64 partial rows and int64 atomics), which
  *                is exact in any order, so no sort runs.
+ *   "item_pieces" P = 1 (default) .. 64: the multi-rank item reduce in P
+ *                pieces of item rows (cf_step_item_reduce).
  *   "spec_neg"   1 (default) = where pos_sort is active with its dense item
  *                apply (n_items <= 2 B (1 + W)), the draw issues each
  *                negative's count atomic for its FIRST candidate before the

@@ -56,6 +56,40 @@ class SplitOracleShard(OracleShard):
         self.O.dedup_adagrad(self.U, self.AU, ur, ug, self.lr)
 
 
+class PiecesOracleShard(SplitOracleShard):
+    """The item reduce in pieces (cf_step_item_reduce): the item gradient of
+    the local step lands in the bound buffer one piece of item rows at a time,
+    each piece's all-reduce issued right after it (AllReduceItems(pieces=P))."""
+
+    def __init__(self, U_local, V, reg, pieces, lr=0.1):
+        super(PiecesOracleShard, self).__init__(U_local, V, reg, lr)
+        self.pieces = pieces
+
+    def step_local_grad(self, batch_size=None, pairs=None, negs=None, groups=None):
+        _, _, self._users, self._items = self.O.bpr_loss_grads(self.U, self.V, pairs, negs, self.reg)
+        self._left = self.pieces
+
+    def item_piece_rows(self, q, n):   # the engine's rule: chunk rounded up to 16 rows
+        n_items = self.V.shape[0]
+        chunk = -(-n_items // n)
+        chunk = -(-chunk // 16) * 16
+        r0 = min(q * chunk, n_items)
+        return r0, min(r0 + chunk, n_items)
+
+    def step_item_reduce(self, q):
+        assert q == self.pieces - self._left
+        self._left -= 1
+        vr, vg = self._items
+        r0, r1 = self.item_piece_rows(q, self.pieces)
+        m = (vr >= r0) & (vr < r1)
+        G = self.item_grad.numpy().reshape(self.V.shape)
+        np.add.at(G, vr[m], vg[m])
+
+    def step_local_apply(self, next_batch_size=0):
+        assert self._left == 0
+        super(PiecesOracleShard, self).step_local_apply(next_batch_size)
+
+
 class RSOracleShard(SplitOracleShard):
     """Item-range ownership (ReduceScatterItems): the item table, its
     accumulator and the gradient live in buffers padded to world * chunk
@@ -109,6 +143,12 @@ def _worker(rank, world, port, fold, batches, U0, V0, q, split=False):
         items = ReduceScatterItems(be.item_grad, torch.zeros(be.chunk * d, dtype=torch.float64),
                                    [(be.Vfull, d)], be.chunk, rank, state=[(be.AVfull, d)])
         step = ShardedStep(be, items)
+    elif isinstance(split, str) and split.startswith("pieces"):
+        from collaborativefilteringusingtensorflow_amd.distributed import AllReduceItems
+        P = int(split[6:])
+        be = PiecesOracleShard(U0[u0:u1], V0, reg=0.05, pieces=P)
+        step = ShardedStep(be, AllReduceItems(be.item_grad, pieces=P, row_width=V0.shape[1],
+                                              n_rows=V0.shape[0]))
     else:
         be = (SplitOracleShard if split else OracleShard)(U0[u0:u1], V0, reg=0.05)
         step = ShardedStep(be, be.item_grad)
@@ -144,7 +184,8 @@ def test_shard_users_balances_nnz(fold1):
         assert lp[0] == 0 and lp[-1] == len(lx)
 
 
-@pytest.mark.parametrize("world,split", [(2, False), (2, True), (2, "rs_ag"), (3, "rs_ag")])
+@pytest.mark.parametrize("world,split", [(2, False), (2, True), (2, "rs_ag"), (3, "rs_ag"), (2, "pieces4"),
+                                         (3, "pieces7")])
 def test_sharded_step_equals_global_step(fold1, streams, world, split):
     from oracle import cf_oracle as O
     rng = np.random.RandomState(4)

@@ -215,3 +215,54 @@ def test_draw_ahead_split_step_equals_plain_split_step(fold1, exchange, W, psort
     assert a[3] == b[3]
     assert np.array_equal(a[4], b[4]) and np.array_equal(a[5], b[5])
     assert abs(a[6] - b[6]) <= 1e-6 * abs(b[6])
+
+
+def _pieces_worker(port, fold, q, pieces_list):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import make_gpu_sharded
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    ip, ix = fold["train_indptr"], fold["train_indices"]
+    out = []
+    for P in pieces_list:
+        e = Engine("bpr", 943, 1682, 32, n_neg=1, reg=0.05, dense_item_apply=True, seed=91)
+        e.set_option("pos_sort", 1)
+        e.set_interactions(ip, ix)
+        e.init_params(0.0, 0.1, seed=6)
+        step, _ = make_gpu_sharded(e, 1682, 32, False, torch.device("cuda", 0), pieces=P)
+        e.profile_reset()
+        e.profile(True)
+        for _ in range(7):
+            step(batch_size=2048)
+        torch.cuda.synchronize()
+        e.profile(False)
+        out.append((P, e.profile_read("item_reduce")[1], e.get_table("user"), e.get_table("item"),
+                    e.get_table("acc_item"), e.take_loss()))
+        e.close()
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_one_rank_rccl_item_reduce_in_pieces(fold1):
+    """The item reduce in pieces of item rows (cf_step_item_reduce,
+    AllReduceItems(pieces=P)), each piece's all-reduce issued on RCCL right
+    after it: the same sums per item row as the whole reduce, so the tables
+    are bitwise those of pieces=1 (device-sampled, pos_sort's dense item
+    apply; one rank on device 0)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_pieces_worker, args=(_free_port(), fold1, q, (1, 3, 7)))
+    p.start()
+    res = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    base = res[0]
+    assert base[1] == 7                       # one whole reduce per step
+    for P, n_red, U, V, AV, loss in res[1:]:
+        assert n_red == 7 * P, (P, n_red)     # deferred: P piece launches per step
+        assert np.array_equal(U, base[2]) and np.array_equal(V, base[3]) and np.array_equal(AV, base[4])
+        assert loss == base[5]
