@@ -2020,7 +2020,10 @@ __device__ __forceinline__ void pacc_ld(const float* __restrict__ A, int64_t r, 
 #ifndef CF_LDS_WAVES
 #define CF_LDS_WAVES 1
 #endif
-#define CF_LDS_ATTR __attribute__((amdgpu_waves_per_eu(CF_LDS_WAVES, 8)))
+#ifndef CF_LDS_WAVES_GBPR
+#define CF_LDS_WAVES_GBPR 4   // GBPR at d = 64: 132 VGPRs at the compiler's budget, 4 waves needs <= 128
+#endif
+#define CF_LDS_ATTR __attribute__((amdgpu_waves_per_eu(MODEL == GBPR ? CF_LDS_WAVES_GBPR : CF_LDS_WAVES, 8)))
 // one negative's LDS reads are not hoisted above the previous negative's
 // terms (the scheduler would otherwise keep all five rows live)
 #ifndef CF_LDS_FENCE
@@ -2047,6 +2050,14 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
     static_assert(MODEL == BPR || MODEL == AMF || MODEL == CML || MODEL == GBPR, "no tuples here");
     // 40 KB (d = 128) / 20 KB (d = 64) per block; the loss partials reuse it
     __shared__ float s_v[kGroupsPerBlock * WT * ROW];
+    // GBPR (ACC_EARLY): the negatives' accumulator rows staged the same way
+    // (round 4) instead of held in 20 VGPRs -- 40 KB per block, four blocks per
+    // CU, and the registers for four waves per SIMD
+#ifndef CF_LDS_STAGE_ACC
+#define CF_LDS_STAGE_ACC 1
+#endif
+    constexpr bool STAGE_ACC = ACC_EARLY && CF_LDS_STAGE_ACC;
+    __shared__ float s_a[STAGE_ACC ? kGroupsPerBlock * WT * ROW : 1];
     const int lane = threadIdx.x & (kWave - 1);
     const int gl = threadIdx.x & (kGL - 1);
     const int grp = threadIdx.x >> 4;
@@ -2094,7 +2105,9 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
         for (int w = 0; w < WT; ++w)
             if (gl == w) jsel = j[w];
         float* wbase = s_v + (threadIdx.x >> 6) * RPW * ROW;
+        float* abase = s_a + (STAGE_ACC ? (threadIdx.x >> 6) * RPW * ROW : 0);
         const int c4 = (lane % LPR) * 4;
+        const bool stage_acc = STAGE_ACC && !a.items_grad_only;
 #pragma unroll
         for (int k = 0; k < RPW / RPI; ++k) {
             const int r = RPI * k + lane / LPR;
@@ -2104,6 +2117,12 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(a.V + (int64_t)jj * d + c4),
                     (__attribute__((address_space(3))) void*)(wbase + RPI * k * ROW), 16, 0, 0);
+            // every negative's accumulator row (at 1M items nearly all are
+            // their row's only occurrence; no count is needed to issue it)
+            if (stage_acc && jj >= 0)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(a.AV + (int64_t)jj * d + c4),
+                    (__attribute__((address_space(3))) void*)(abase + RPI * k * ROW), 16, 0, 0);
         }
     }
     // counts and the u / i rows, then slots and the accumulator rows of the
@@ -2131,8 +2150,10 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
             for (int w = 0; w < WT; ++w) bj[w] = a.b[j[w]];
         }
     }
-    int64_t su = -1, si = -1, sg = -1, sj[WT];
-    float au[EPL], ai[EPL], ag[MODEL == GBPR ? EPL : 1], aje[ACC_EARLY ? WT : 1][EPL];
+    // slot rows as int32 (n_users * capU and n_items * capV < 2^31 wherever
+    // this kernel runs: 10M x 2, 1M x 32 at cfg4): 8 VGPRs fewer than int64
+    int32_t su = -1, si = -1, sg = -1, sj[WT];
+    float au[EPL], ai[EPL], ag[MODEL == GBPR ? EPL : 1], aje[ACC_EARLY && !STAGE_ACC ? WT : 1][EPL];
     float abi = 0.f, abj[WT];   // GBPR: bias accumulators of rows seen once
     const bool item_acc = !a.items_grad_only;
 #pragma unroll
@@ -2151,7 +2172,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
 #pragma unroll
             for (int w = 0; w < WT; ++w) abj[w] = (item_acc && cj[w] == 1) ? a.Ab[j[w]] : 0.f;
         }
-        if constexpr (ACC_EARLY) {
+        if constexpr (ACC_EARLY && !STAGE_ACC) {
 #pragma unroll
             for (int w = 0; w < WT; ++w) pacc_ld<EPL>(a.AV, j[w], d, gl, par, item_acc && cj[w] == 1, aje[w]);
         }
@@ -2338,7 +2359,15 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) gj[s] = -cw[w] * uu[s];   // no L2 on V[j] (gbprmf.py:59-64)
                 if (gl == 0) bias_finish_pre(a, j[w], cj[w], -cw[w] + a.reg * bj[w], sj[w], bj[w], abj[w]);
-                pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], 0.f, 0, gl, par, vj, aje[ACC_EARLY ? w : 0], gj);
+                if constexpr (STAGE_ACC) {
+                    float aj[EPL];
+#pragma unroll
+                    for (int s = 0; s < EPL; ++s) aj[s] = 1.f;
+                    if (item_acc && cj[w] == 1) prow_ld<EPL>(s_a + grp * WT * ROW + w * ROW, gl, par, aj);
+                    pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], 0.f, 0, gl, par, vj, aj, gj);
+                } else {
+                    pifinish<EPL>(a, j[w], cj[w], sj[w], p, -cw[w], 0.f, 0, gl, par, vj, aje[ACC_EARLY ? w : 0], gj);
+                }
             }
         }
     }
