@@ -561,9 +561,7 @@ def make_gpu_group_exchange(engine, world, rank, bounds, indptr, indices, n_item
         n = n_items * d + n_items
         grad = torch.zeros(n, dtype=torch.float32, device=device)
         engine.bind_item_grad(grad.data_ptr(), n)
-        if pieces > 1:
-            engine.set_option("item_pieces", pieces)
-        items = AllReduceItems(grad, process_group, pieces=pieces, row_width=d, n_rows=n_items)
+        items = AllReduceItems(grad, process_group)
     else:
         raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
     ip_t, ix_t = item_csr if item_csr is not None else item_users(indptr, indices, n_items)
