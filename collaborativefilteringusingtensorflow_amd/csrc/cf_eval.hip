@@ -294,6 +294,14 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
     return r * kFusedMaxD + ((((kk >> 2) ^ (r & 31)) << 2) | (kk & 3));
 }
 
+#ifndef CF_FUSED_PREFILTER
+// 1: the 16 prefilter compares first, the LDS reads only where a lane of the
+// wave passed -- measured even (cfg5 83.5 vs 84.8, cfg3 77.8 vs 75.9 TFLOP/s,
+// r04k; it spills 16-80 B at the 256-VGPR limit), so 0: the cost of the
+// candidate phase (84.7 -> 112.5 without it, CF_FUSED_EXP_NOCAND) is not the
+// mask reads
+#define CF_FUSED_PREFILTER 0
+#endif
 #ifndef CF_FUSED_BPREFETCH
 #define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
@@ -485,6 +493,44 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                 thi[q] = R < nu ? (uint32_t)(thr[R] >> 32) : 0xFFFFFFFFu;
             }
         }
+#if CF_FUSED_PREFILTER
+        // round 4: the register prefilter for all 16 scores first -- no LDS
+        // read -- and the train mask, the exact threshold and the insertion
+        // only where some lane of the wave passed (rare once the thresholds
+        // have risen).  Attribution: the candidate phase cost the pass 84.7 ->
+        // 112.5 TFLOP/s (CF_FUSED_EXP_NOCAND), its 16 mask reads per lane
+        // per tile were issued whatever the prefilter said.
+        const float bj_ = (MODEL == GBPR) ? bt[jl] : 0.f;
+        uint32_t pass = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+            float s = acc[q];
+            if (MODEL == GBPR) s += bj_;
+            if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];   // -|u - v|^2
+            // key > thr[R] implies fk >= thi[q]: a pure prefilter
+            pass |= (float_key(s) >= thi[q]) ? (1u << q) : 0u;
+        }
+        if (__ballot(pass != 0u) != 0ull) {   // wave-uniform
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                if (!((pass >> q) & 1u)) continue;
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                float s = acc[q];
+                if (MODEL == GBPR) s += bj_;
+                if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];
+                const uint32_t fk = float_key(s);
+                if (R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
+                    const unsigned long long key = ((unsigned long long)fk << 32) |
+                                                   (0xFFFFFFFFull - (unsigned long long)J);
+                    if (key > thr[R]) {
+                        const int pos = atomicAdd(&cnt[R], 1);
+                        buf[R * kFusedCap + pos] = key;
+                    }
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -502,6 +548,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                 }
             }
         }
+#endif
 #else
         if (acc[0] == 12345.f && J == 7) cnt[0] = 1;   // keep the MFMA result live
 #endif

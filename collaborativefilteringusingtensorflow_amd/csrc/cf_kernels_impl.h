@@ -2021,7 +2021,7 @@ __device__ __forceinline__ void pacc_ld(const float* __restrict__ A, int64_t r, 
 #define CF_LDS_WAVES 1
 #endif
 #ifndef CF_LDS_WAVES_GBPR
-#define CF_LDS_WAVES_GBPR 4   // GBPR at d = 64: 132 VGPRs at the compiler's budget, 4 waves needs <= 128
+#define CF_LDS_WAVES_GBPR 1   // 4 (with CF_LDS_STAGE_ACC: 128 VGPRs, 12-B spill) measured slower (r04j)
 #endif
 #define CF_LDS_ATTR __attribute__((amdgpu_waves_per_eu(MODEL == GBPR ? CF_LDS_WAVES_GBPR : CF_LDS_WAVES, 8)))
 // one negative's LDS reads are not hoisted above the previous negative's
@@ -2054,7 +2054,7 @@ __global__ __launch_bounds__(kBlock) CF_LDS_ATTR void grad_lds_kernel(StepArgs a
     // (round 4) instead of held in 20 VGPRs -- 40 KB per block, four blocks per
     // CU, and the registers for four waves per SIMD
 #ifndef CF_LDS_STAGE_ACC
-#define CF_LDS_STAGE_ACC 1
+#define CF_LDS_STAGE_ACC 0   // 1 measured slower at cfg4 (131.6 vs 126.2 us with 4 waves, 12-B spill; r04j)
 #endif
     constexpr bool STAGE_ACC = ACC_EARLY && CF_LDS_STAGE_ACC;
     __shared__ float s_a[STAGE_ACC ? kGroupsPerBlock * WT * ROW : 1];

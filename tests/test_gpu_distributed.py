@@ -251,8 +251,9 @@ def test_one_rank_rccl_item_reduce_in_pieces(fold1):
     """The item reduce in pieces of item rows (cf_step_item_reduce,
     AllReduceItems(pieces=P)), each piece's all-reduce issued on RCCL right
     after it: the same sums per item row as the whole reduce, so the tables
-    are bitwise those of pieces=1 (device-sampled, pos_sort's dense item
-    apply; one rank on device 0)."""
+    are those of pieces=1 up to the fast path's run-to-run fp32 order of
+    duplicate sums (its ranks come from count atomics; device-sampled,
+    pos_sort's dense item apply; one rank on device 0)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_pieces_worker, args=(_free_port(), fold1, q, (1, 3, 7)))
@@ -264,5 +265,7 @@ def test_one_rank_rccl_item_reduce_in_pieces(fold1):
     assert base[1] == 7                       # one whole reduce per step
     for P, n_red, U, V, AV, loss in res[1:]:
         assert n_red == 7 * P, (P, n_red)     # deferred: P piece launches per step
-        assert np.array_equal(U, base[2]) and np.array_equal(V, base[3]) and np.array_equal(AV, base[4])
-        assert loss == base[5]
+        for got, ref, name in ((U, base[2], "user"), (V, base[3], "item"), (AV, base[4], "acc_item")):
+            err = np.abs(got.astype(np.float64) - ref)
+            assert (err <= 1e-6 + 1e-5 * np.abs(ref)).all(), (P, name, float(err.max()))
+        assert abs(loss - base[5]) <= 1e-6 * abs(base[5])
