@@ -259,19 +259,32 @@ static hipError_t launch_apply_ps_t(const ApplyArgs& p, const StepArgs* nx, hipS
     const int nbI = (int)nbI64, nbW = (int)std::max<int64_t>(nbW64, nbI64 == 0 ? 1 : 0);   // block 0 folds the loss
     const dim3 grid(nbI + nbW + np), block(kBlock);
     const StepArgs n = nx ? *nx : StepArgs{};
+    const bool full = CF_ASSUME_FULL_APPLY && p.d == kGL * epl_for(p.d);
     if (np > 0) {
         switch (epl_for(p.d)) {
             case 1: hipLaunchKernelGGL((apply_ps_kernel<1, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
             case 2: hipLaunchKernelGGL((apply_ps_kernel<2, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4:
+                if (full) hipLaunchKernelGGL((apply_ps_kernel<4, true, PS, FX, true>), grid, block, 0, s, p, n, nbI, nbW);
+                else hipLaunchKernelGGL((apply_ps_kernel<4, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW);
+                break;
+            default:
+                if (full) hipLaunchKernelGGL((apply_ps_kernel<8, true, PS, FX, true>), grid, block, 0, s, p, n, nbI, nbW);
+                else hipLaunchKernelGGL((apply_ps_kernel<8, true, PS, FX>), grid, block, 0, s, p, n, nbI, nbW);
+                break;
         }
     } else {
         switch (epl_for(p.d)) {
             case 1: hipLaunchKernelGGL((apply_ps_kernel<1, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
             case 2: hipLaunchKernelGGL((apply_ps_kernel<2, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
-            case 4: hipLaunchKernelGGL((apply_ps_kernel<4, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
-            default: hipLaunchKernelGGL((apply_ps_kernel<8, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW); break;
+            case 4:
+                if (full) hipLaunchKernelGGL((apply_ps_kernel<4, false, PS, FX, true>), grid, block, 0, s, p, n, nbI, nbW);
+                else hipLaunchKernelGGL((apply_ps_kernel<4, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW);
+                break;
+            default:
+                if (full) hipLaunchKernelGGL((apply_ps_kernel<8, false, PS, FX, true>), grid, block, 0, s, p, n, nbI, nbW);
+                else hipLaunchKernelGGL((apply_ps_kernel<8, false, PS, FX>), grid, block, 0, s, p, n, nbI, nbW);
+                break;
         }
     }
     return hipGetLastError();

@@ -1899,12 +1899,25 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #ifndef CF_SORT_MIN_WAVES
 #define CF_SORT_MIN_WAVES 1
 #endif
+#ifndef CF_ASSUME_FULL_ROWS
+#define CF_ASSUME_FULL_ROWS 1
+#endif
+// the same for apply_ps_kernel: measured even at cfg2/4/5 (round 4) -- the
+// apply hoists more loads (79 -> 92 VGPRs, one wave per SIMD less), off
+#ifndef CF_ASSUME_FULL_APPLY
+#define CF_ASSUME_FULL_APPLY 0
+#endif
 // CF_SORT_TILES positive-sorted tiles per block (grad_fast_body)
 #ifndef CF_SORT_TILES
 #define CF_SORT_TILES 1
 #endif
-template <int MODEL, int EPL, int WT, bool FX = false>
+template <int MODEL, int EPL, int WT, bool FX = false, bool FULL = false>
 __global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a) {
+    // FULL: the launcher takes this instantiation only for full rows (d ==
+    // 16 EPL), so every per-element `e < d` guard folds away -- each guarded
+    // load / store was an exec-mask save, a branch and a restore: 1,907 ->
+    // 1,285 instructions at cfg2 (round 4)
+    if constexpr (FULL) __builtin_assume(a.d == kGL * EPL);
     grad_fast_body<MODEL, EPL, WT, CF_SORT_TILES, kGroupsPerBlock, true, FX>(a, blockIdx.x);
 }
 
@@ -2837,8 +2850,10 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 #ifndef CF_APPLY_DRAW_TAIL
 #define CF_APPLY_DRAW_TAIL 0
 #endif
-template <int EPL, bool DRAW, bool PS = true, bool FX = false>
+template <int EPL, bool DRAW, bool PS = true, bool FX = false, bool FULL = false>
 __global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
+    // FULL: full rows (d == 16 EPL), the `e < d` guards fold away (grad_sort_kernel)
+    if constexpr (FULL) __builtin_assume(p.d == kGL * EPL);
     int b = blockIdx.x;
     if (blockIdx.x == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
     if constexpr (DRAW && !CF_APPLY_DRAW_TAIL) {
@@ -3243,11 +3258,15 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
         if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
             if (np > 0) return hipErrorInvalidValue;
             const dim3 sgrid((a.B + CF_SORT_TILES * kPsortPPB - 1) / (CF_SORT_TILES * kPsortPPB));
+            const bool full = CF_ASSUME_FULL_ROWS && a.d == kGL * epl_for(a.d);
             if (a.det_fx) {   // deterministic: fixed-point partials and loss
                 switch (epl_for(a.d)) {
                     case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT, true>), sgrid, block, 0, s, a); break;
                     case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT, true>), sgrid, block, 0, s, a); break;
-                    case 4: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true>), sgrid, block, 0, s, a); break;
+                    case 4:
+                        if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true, true>), sgrid, block, 0, s, a);
+                        else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true>), sgrid, block, 0, s, a);
+                        break;
                     default: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, true>), sgrid, block, 0, s, a); break;
                 }
                 return hipGetLastError();
@@ -3255,8 +3274,14 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
             switch (epl_for(a.d)) {
                 case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT>), sgrid, block, 0, s, a); break;
                 case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT>), sgrid, block, 0, s, a); break;
-                case 4: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT>), sgrid, block, 0, s, a); break;
-                default: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT>), sgrid, block, 0, s, a); break;
+                case 4:
+                    if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, false, true>), sgrid, block, 0, s, a);
+                    else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT>), sgrid, block, 0, s, a);
+                    break;
+                default:
+                    if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, false, true>), sgrid, block, 0, s, a);
+                    else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT>), sgrid, block, 0, s, a);
+                    break;
             }
             return hipGetLastError();
         }

@@ -11,6 +11,10 @@
 #   prof   rocprofv3 kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes of
 #          one bench configuration per "tag:args" in $PROF (';' list)
 #          -> gpurun_out/prof_<tag>/ (tools/gpu_profile_cfg.sh)
+#   pmc    one rocprofv3 --pmc pass per "name:counters" in $PMC_SETS (';' list,
+#          counters space-separated, each pass within the per-block limits:
+#          8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD) over bench.py $PMC_ARGS
+#          -> $OUT/pmc_<name>/ (tools/pmc_summary.py or read the CSV)
 #   ab     the default build against build/variants/*/ with every "name:args"
 #          of $VARIANT_OPTS (';' list)                              -> $OUT/ab_<variant>_<name>.json
 #
@@ -68,6 +72,18 @@ step_prof() {
   done
 }
 
+step_pmc() {
+  local spec name ctrs
+  local ARGS=${PMC_ARGS:---steps 30 --warmup 5 --no-cpu-baseline --no-ndcg --secondary-batch 0 --no-profile}
+  IFS=';' read -ra SPECS <<< "${PMC_SETS}"
+  for spec in "${SPECS[@]}"; do
+    name=${spec%%:*}; ctrs=${spec#*:}
+    timeout -s KILL 240 rocprofv3 --pmc $ctrs --output-format csv -d $OUT/pmc_$name -o run -- python bench.py $ARGS \
+        > $OUT/pmc_$name.log 2>&1 || { tail -20 $OUT/pmc_$name.log; die "pmc pass $name failed"; }
+    echo "pmc $name done"
+  done
+}
+
 step_ab() {
   local lib v o on oa
   local ARGS=${AB_ARGS:---steps 200 --warmup 20 --no-cpu-baseline --no-ndcg --secondary-batch 0}
@@ -99,6 +115,7 @@ for s in $STEPS; do
     smoke) step_smoke ;;
     bench) step_bench ;;
     prof) step_prof ;;
+    pmc) step_pmc ;;
     ab) step_ab ;;
     *) die "unknown step $s" ;;
   esac
