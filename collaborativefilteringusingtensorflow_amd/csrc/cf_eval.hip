@@ -302,6 +302,14 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 // mask reads
 #define CF_FUSED_PREFILTER 0
 #endif
+#ifndef CF_FUSED_FCMP
+// 1 (round 4): the register prefilter compares the float score against the
+// float form of its row's threshold word -- one v_cmp per score, no key
+// conversion, no per-row (R < nu) mask -- and the wave takes the exact path
+// only when some lane passed some score (rare once the thresholds have
+// risen); 0: the key-word prefilter per score, each with its own branch
+#define CF_FUSED_FCMP 1
+#endif
 #ifndef CF_FUSED_BPREFETCH
 #define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
@@ -328,7 +336,11 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
     // the score words of the thresholds of this lane's 16 output rows, kept in
     // registers: a score whose key word is below its row's cannot enter the
     // list, so most scores are rejected without touching LDS
+#if CF_FUSED_FCMP
+    float thf[16];   // key_float of the threshold word; +inf for rows past nu
+#else
     uint32_t thi[16];
+#endif
     int thi_ver = -1;
     const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
 
@@ -485,6 +497,48 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         const int jl = wc * 32 + c;
         const int64_t J = j0 + jl;
 #ifndef CF_FUSED_EXP_NOCAND
+#if CF_FUSED_FCMP
+        if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
+            thi_ver = thr_ver;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;   // < kFusedUsers
+                const float t = key_float((uint32_t)(thr[R] >> 32));
+                thf[q] = R < nu ? t : INFINITY;
+            }
+        }
+        // key(s) > thr[R] implies s >= key_float(thr word) in float order; a
+        // NaN score or threshold passes (!(s < t)), so this only prefilters
+        const float bj_ = (MODEL == GBPR) ? bt[jl] : 0.f;
+        bool anyp = false;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            float s = acc[q];
+            if (MODEL == GBPR) s += bj_;
+            if (MODEL == CML) {
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                s = 2.f * s - vnorm - unorm[R];   // -|u - v|^2
+            }
+            anyp |= !(s < thf[q]);
+        }
+        if (__ballot(anyp) != 0ull) {   // wave-uniform
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                float s = acc[q];
+                if (MODEL == GBPR) s += bj_;
+                if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];
+                if (!(s < thf[q]) && R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
+                    const unsigned long long key = ((unsigned long long)float_key(s) << 32) |
+                                                   (0xFFFFFFFFull - (unsigned long long)J);
+                    if (key > thr[R]) {
+                        const int pos = atomicAdd(&cnt[R], 1);
+                        buf[R * kFusedCap + pos] = key;
+                    }
+                }
+            }
+        }
+#else
         if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
             thi_ver = thr_ver;
 #pragma unroll
@@ -493,7 +547,10 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                 thi[q] = R < nu ? (uint32_t)(thr[R] >> 32) : 0xFFFFFFFFu;
             }
         }
-#if CF_FUSED_PREFILTER
+#endif
+#if CF_FUSED_FCMP
+        // (above)
+#elif CF_FUSED_PREFILTER
         // round 4: the register prefilter for all 16 scores first -- no LDS
         // read -- and the train mask, the exact threshold and the insertion
         // only where some lane of the wave passed (rare once the thresholds
