@@ -1803,7 +1803,7 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
 // 1: the prefetch compiled in.  Its registers take grad_sort_kernel<BPR, 4, 1>
 // from 75 to 81 VGPRs, 6 -> 5 waves / SIMD: the cfg2 gradient launch ran
 // 197.3 us with it, 179.9 us without (same box, round 4,
-// profiles/r04/ab_occupancy/); the engine refuses the option unless built in
+// profiles/r04/ab_occupancy/ab_r04_ab1.txt); the engine refuses the option unless built in
 #define CF_PAIR_PREFETCH 0
 #endif
     if constexpr (SORT && CF_PAIR_PREFETCH) {
