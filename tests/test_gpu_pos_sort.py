@@ -260,9 +260,16 @@ def test_pos_sort_auto_by_batch_size():
     e.profile(False)
     n_big = psort_launches(e) - n_small
     assert n_small == 1 and n_big == K
+    # the strict band plus the a-priori fp32 bound carried over the K steps
+    # (oracle/fp32_bound.py): 8K Zipf items at 2^18 pairs put
+    # thousands of occurrences on the head rows, whose fp32 sums leave the
+    # strict band in some summation orders (round 4: acc_item at 1.011x of it,
+    # profiles/r04/red_runs/)
+    from oracle import fp32_bound as FB
+    E = FB.zero_bounds(T["user"], T["item"], acc_exact=True)
     lo = 0.0
     for pairs, negs in batches:
-        lo += O.bpr_step(T["user"], T["item"], T["acc_user"], T["acc_item"], pairs, negs, reg)
+        lo += FB.bpr_step_bounded(T["user"], T["item"], T["acc_user"], T["acc_item"], E, pairs, negs, reg)
     assert abs(loss - lo) <= RTOL * abs(lo), (loss, lo)
     # the batches really overflow capP (8 partials) on their hottest positives
     cnt = np.bincount(batches[0][0][:, 1], minlength=ni)
@@ -270,7 +277,7 @@ def test_pos_sort_auto_by_batch_size():
     nparts = np.where(cnt > 0, (off + cnt - 1) // 16 - off // 16 + 1, 0)
     assert nparts.max() > 8, nparts.max()
     for t in T:
-        assert_close(e.get_table(t), T[t], t)
+        assert_close(e.get_table(t), T[t], t, bound=E[t])
     e.close()
 
 
