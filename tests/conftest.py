@@ -48,6 +48,9 @@ def assert_close(got, ref, what, rtol=RTOL, atol=ATOL, bound=None):
         tol = tol + bound
     bad = err > tol
     worst = float(np.max(err / tol)) if err.size else 0.0
+    if os.environ.get("CF_BAND_LOG"):   # margin survey: worst |d| / band per assertion
+        with open(os.environ["CF_BAND_LOG"], "a") as f:
+            f.write("%s\t%s\t%.4f\n" % (os.environ.get("PYTEST_CURRENT_TEST", "?"), what, worst))
     if bad.any():
         k = np.unravel_index(int(np.argmax(err / tol)), err.shape)
         raise AssertionError("%s: %d elements out of |d| <= %g + %g|ref|%s; worst d/bound %.3f at %s "
