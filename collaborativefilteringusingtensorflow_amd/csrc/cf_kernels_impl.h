@@ -135,19 +135,53 @@ __device__ __forceinline__ void row_zero(float* __restrict__ row, int d, int gl)
     for (int s = 0; s < EPL; ++s) z[s] = 0.f;
     row_st<EPL>(row, d, gl, z);
 }
+// the sum over a 16-lane group, identical in every lane of it.  A group is
+// one DPP row, so (round 4) the butterfly runs on DPP: quad_perm [1,0,3,2]
+// and [2,3,0,1] sum each quad, row_half_mirror adds the other quad of the
+// half-row (every lane of a quad holds the same value by then, so any
+// partner in it gives the same sum) and row_mirror the other half-row --
+// four VALU ops with a DPP operand instead of four ds_bpermute round trips
+// through the LDS crossbar.  Called group-uniformly (no lane of the row is
+// inactive).  CF_DPP_GSUM 0: the xor butterfly on __shfl_xor.
+#ifndef CF_DPP_GSUM
+#define CF_DPP_GSUM 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float gsum(float v) {
+#if CF_DPP_GSUM
+    v += dpp_f<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f<0x141>(v);   // row_half_mirror
+    v += dpp_f<0x140>(v);   // row_mirror
+#else
     v += __shfl_xor(v, 8, 64);
     v += __shfl_xor(v, 4, 64);
     v += __shfl_xor(v, 2, 64);
     v += __shfl_xor(v, 1, 64);
+#endif
     return v;
 }
 
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+// OR over a 16-lane group (one DPP row), the same steps as gsum
 __device__ __forceinline__ uint32_t gor(uint32_t v) {
+#if CF_DPP_GSUM
+    v |= dpp_u<0xB1>(v);
+    v |= dpp_u<0x4E>(v);
+    v |= dpp_u<0x141>(v);
+    v |= dpp_u<0x140>(v);
+#else
     v |= (uint32_t)__shfl_xor((int)v, 8, 64);
     v |= (uint32_t)__shfl_xor((int)v, 4, 64);
     v |= (uint32_t)__shfl_xor((int)v, 2, 64);
     v |= (uint32_t)__shfl_xor((int)v, 1, 64);
+#endif
     return v;
 }
 
@@ -410,12 +444,37 @@ __host__ __device__ constexpr int prep_chunks(int pgl) { return pgl == kPrepGL ?
 #endif
 constexpr int kPrepVChunks = CF_PREP_VCHUNKS;
 
-// OR over the PGL lanes of a draw group
+// OR over the PGL lanes of a draw group.  A group of 4 or 8 lanes lies in
+// one DPP row: quad_perm steps OR each quad, row_half_mirror the other quad
+// of an 8-lane group (round 4; CF_DPP_DRAW 0: __shfl_xor)
+#ifndef CF_DPP_DRAW
+#define CF_DPP_DRAW 1
+#endif
 template <int PGL = kPrepGL>
 __device__ __forceinline__ uint32_t gor8(uint32_t v) {
+    if constexpr (CF_DPP_DRAW && (PGL == 4 || PGL == 8)) {
+        v |= dpp_u<0xB1>(v);   // quad_perm [1,0,3,2]
+        v |= dpp_u<0x4E>(v);   // quad_perm [2,3,0,1]
+        if constexpr (PGL == 8) v |= dpp_u<0x141>(v);   // row_half_mirror
+        return v;
+    }
 #pragma unroll
     for (int o = PGL / 2; o >= 1; o >>= 1) v |= (uint32_t)__shfl_xor((int)v, o, 64);
     return v;
+}
+// lane k of the caller's PGL-lane group, broadcast (k compile-time after
+// unrolling); a 4-lane group is a quad: quad_perm [k,k,k,k]
+template <int PGL>
+__device__ __forceinline__ int32_t gbcast(int32_t v, int k) {
+    if constexpr (CF_DPP_DRAW && PGL == 4) {
+        switch (k) {
+            case 0: return (int32_t)dpp_u<0x00>((uint32_t)v);
+            case 1: return (int32_t)dpp_u<0x55>((uint32_t)v);
+            case 2: return (int32_t)dpp_u<0xAA>((uint32_t)v);
+            default: return (int32_t)dpp_u<0xFF>((uint32_t)v);
+        }
+    }
+    return __shfl(v, k, PGL);
 }
 
 constexpr unsigned long long kPosEmpty = ~0ull;
@@ -573,21 +632,22 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             {
                 int32_t cand[PGL];
 #pragma unroll
-                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(jl, k, PGL);
+                for (int k = 0; k < PGL; ++k) cand[k] = gbcast<PGL>(jl, k);
 #ifndef CF_EXP_DRAW_NOSCAN   // attribution only (wrong batches): no row scan
                 hit = gor8<PGL>(row_hits<PGL>(a.indices, rb, re, gl, cand, nl));
 #endif
             }
             // lane w < nw: the first accepted attempt of negative w
-            bool done = false;
+            // (the winning lane found from the group-uniform hit mask first:
+            // one shuffle instead of one per attempt)
+            int win = -1;
             for (int c = 0; c < C; ++c) {
                 const int src = c * nw + (gl % nw);
-                const int32_t cv = __shfl(jl, src, PGL);
-                if (!done && gl < nw && !((hit >> src) & 1u)) {
-                    j = cv;
-                    done = true;
-                }
+                if (win < 0 && !((hit >> src) & 1u)) win = src;
             }
+            const int32_t cv = __shfl(jl, win < 0 ? 0 : win, PGL);
+            const bool done = win >= 0;
+            if (done && gl < nw) j = cv;
             // rare: every tested attempt of some negative was a positive ->
             // continue its sequence at attempt C, one candidate per lane
             uint32_t pending = gor8<PGL>((gl < nw && !done) ? (1u << gl) : 0u);
@@ -596,7 +656,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             while (pending != 0u) {  // group-uniform
                 int32_t cand[PGL];
 #pragma unroll
-                for (int k = 0; k < PGL; ++k) cand[k] = __shfl(j, k, PGL);
+                for (int k = 0; k < PGL; ++k) cand[k] = gbcast<PGL>(j, k);
                 uint32_t h2 = gor8<PGL>(row_hits<PGL>(a.indices, rb, re, gl, cand, nw)) & pending;
                 if ((h2 >> gl) & 1u) j = draw_item(key, ctr++, a.n_items);
                 pending = h2;
@@ -837,7 +897,7 @@ __device__ __forceinline__ void prep_body_np(const StepArgs& a, int block) {
 #pragma unroll
         for (int k = 0; k < NP; ++k)
 #pragma unroll
-            for (int c = 0; c < PGL; ++c) cand[k][c] = __shfl(jl[k], c, PGL);
+            for (int c = 0; c < PGL; ++c) cand[k][c] = gbcast<PGL>(jl[k], c);
         for (int c0 = 0; c0 < maxchunk; c0 += kPrepChunks) {
             int32_t el[NP][kPrepChunks];
 #pragma unroll
@@ -879,7 +939,7 @@ __device__ __forceinline__ void prep_body_np(const StepArgs& a, int block) {
         while (pending != 0u) {  // group-uniform
             int32_t cand[PGL];
 #pragma unroll
-            for (int c = 0; c < PGL; ++c) cand[c] = __shfl(j[k], c, PGL);
+            for (int c = 0; c < PGL; ++c) cand[c] = gbcast<PGL>(j[k], c);
             uint32_t h2 = 0;
             for (int c0 = 0; c0 < nchunk[k]; c0 += kPrepChunks) {
                 int32_t el[kPrepChunks];
