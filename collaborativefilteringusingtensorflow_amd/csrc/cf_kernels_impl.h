@@ -2910,8 +2910,13 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 #ifndef CF_APPLY_DRAW_TAIL
 #define CF_APPLY_DRAW_TAIL 0
 #endif
+// minimum waves per SIMD the pos_sort apply is built for: 7 (72 VGPRs, 12-B
+// spill) measured even-to-slower at cfg2 (round 4, profiles/r04/ab/ab_r04w_occupancy.txt)
+#ifndef CF_APPLY_MIN_WAVES
+#define CF_APPLY_MIN_WAVES 1
+#endif
 template <int EPL, bool DRAW, bool PS = true, bool FX = false, bool FULL = false>
-__global__ __launch_bounds__(kBlock) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
+__global__ __launch_bounds__(kBlock, CF_APPLY_MIN_WAVES) void apply_ps_kernel(ApplyArgs p, StepArgs nx, int nbI, int nbW) {
     // FULL: full rows (d == 16 EPL), the `e < d` guards fold away (grad_sort_kernel)
     if constexpr (FULL) __builtin_assume(p.d == kGL * EPL);
     int b = blockIdx.x;
