@@ -81,8 +81,11 @@ SIGNATURES = {
     "cf_init_params": (ctypes.c_int, [_P, _F, _F, _I32, _U64]),
     "cf_set_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
     "cf_get_table": (ctypes.c_int, [_P, _I32, _PF, _I64]),
+    "cf_set_params": (ctypes.c_int, [_P, _PF, _PF, _PF, _PF, _PF, _PF]),
+    "cf_get_params": (ctypes.c_int, [_P, _PF, _PF, _PF, _PF, _PF, _PF]),
     "cf_step": (ctypes.c_int, [_P, _PI32, _PI32, _PI32, _I32, _PD]),
     "cf_train_steps": (ctypes.c_int, [_P, _I32, _I32, _PD]),
+    "cf_train_epoch": (ctypes.c_int, [_P, _I32, _PD]),
     "cf_sample": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
     "cf_get_sampler_state": (ctypes.c_int, [_P, _PI64, _PI64]),
     "cf_set_sampler_state": (ctypes.c_int, [_P, _I64, _I64]),
@@ -113,7 +116,8 @@ SIGNATURES = {
     "cf_xchg_grad_part": (ctypes.c_int, [_P, _I32]),
     "cf_xchg_finish_items": (ctypes.c_int, [_P]),
     "cf_xchg_finish": (ctypes.c_int, [_P, _I64]),
-    "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _PI32, _PF]),
+    "cf_score_topk": (ctypes.c_int, [_P, _PI32, _I32, _I32, _P, _PI32, _PF]),
+    "cf_score_topk_ex": (ctypes.c_int, [_P, _PI32, _I32, _I32, _I32, _P, _PI32, _PF]),
     "cf_set_option": (ctypes.c_int, [_P, ctypes.c_char_p, _I64]),
     "cf_profile_enable": (ctypes.c_int, [_P, _I32]),
     "cf_profile_read": (ctypes.c_int, [_P, _I32, _PD, _PI64]),

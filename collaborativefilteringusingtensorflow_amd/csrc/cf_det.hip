@@ -115,6 +115,9 @@ __global__ __launch_bounds__(256) void psort_scatter_kernel(PsortArgs a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) v[2 + w] = j[w];
         v[2 + W] = cu == 1 ? kSlotApply : ru < a.capU ? u * a.capU + ru : kSlotAtomic;
+        // deterministic mode: a user past its cap gets its compact int64 row
+        // once, from its rank-capU occurrence (read by the next launches)
+        if (a.hotU != nullptr && ru == a.capU) a.hotU[u] = atomicAdd(a.hot_n, 1);
         v[3 + W] = (int32_t)((uint32_t)oP | (ci == 1 ? 0x80000000u : 0u));
 #pragma unroll
         for (int w = 0; w < W; ++w) v[4 + W + w] = cj[w] == 1 ? kSlotApply : oN[w] + rj[w];

@@ -57,6 +57,9 @@ void dfree(T*& p) {
 
 }  // namespace
 
+// deterministic range flags kept per step (cf_engine::fx_bad)
+constexpr int kFxSlots = 1024;
+
 struct cf_engine {
     cf_config cfg{};
     hipStream_t stream = nullptr;
@@ -75,7 +78,10 @@ struct cf_engine {
     // deterministic mode on the pos_sort path: fixed-point partials and the
     // users' int64 overflow accumulators (StepArgs::det_fx)
     long long* slotP64 = nullptr;
-    unsigned long long* GU64 = nullptr;
+    unsigned long long* GU64 = nullptr;   // [hot_cap, d] compact rows of users past their slot cap
+    int32_t* hotU = nullptr;              // [n_users] a hot user's compact row (psort)
+    int* hot_n = nullptr;                 // rows handed out this batch
+    int64_t hot_cap = 0;
     unsigned long long* GV64 = nullptr;
     int fx_cap = 0;
     int pf_cap = 0;
@@ -124,7 +130,8 @@ struct cf_engine {
     int32_t* srec = nullptr;          // [order_cap, psort_stride(n_neg)] sorted pair records
     int order_cap = 0;
     float* slotP = nullptr;           // [order_cap / kPsortPPB + 1 + n_items, d] (StepArgs::slotP)
-    float* slotN = nullptr;           // [order_cap * n_neg, d] compact negative slot rows (offN[j] + rank)
+    float* slotN = nullptr;           // [slotN_rows, d] compact negative slot rows (offN[j] + rank)
+    int64_t slotN_rows = 0;           // order_cap * n_neg, doubled when speculative counts can apply
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
     bool slots_ready = false;
@@ -149,8 +156,12 @@ struct cf_engine {
     float* coefs = nullptr;   // [B, 2] CPLR tuple coefficients (cf_step_plr)
     int coefs_cap = 0;
     double* h_loss = nullptr; // pinned
-    int* fx_bad = nullptr;    // deterministic fixed-point range flag (StepArgs::fx_bad)
-    int* h_fx_bad = nullptr;  // pinned
+    // deterministic fixed-point range flags (StepArgs::fx_bad), one word per
+    // step since the last check_fx (step k of the call: word min(k, kFxSlots-1)),
+    // so a failing call names its first bad step
+    int* fx_bad = nullptr;
+    int* h_fx_bad = nullptr;  // pinned [kFxSlots]
+    int fx_step = 0;
     int32_t* h_stage = nullptr;
     size_t stage_cap = 0;
     int tuple_stride = 0;            // cf_step_plr: ids read from tuples [B, width]
@@ -236,6 +247,8 @@ struct cf_engine {
     // eval workspace
     uint32_t* keys = nullptr;
     size_t keys_cap = 0;
+    uint64_t* item_mask = nullptr;   // cf_score_topk's caller mask, one bit per item
+    int64_t mask_words = 0;
 
     int topk_path = 0;  // cf_set_option("topk_path")
     int fused_variant = 0;  // cf_set_option("fused_variant")
@@ -387,19 +400,29 @@ int ensure_det(cf_engine* e, int B, int B_step) {
             CF_HIP(hipStreamSynchronize(e->side));
             dfree(e->slotP64);
             CF_TRY(dalloc(&e->slotP64, ((size_t)B / kPsortPPB + 1 + (size_t)c.n_items) * c.n_factors));
+            // users past their slot cap: at most one per capU + 1 user
+            // occurrences of the batch, each one compact int64 row (was one
+            // row per user of the table: 512 MB at cfg2, round-3 ADVICE)
+            dfree(e->GU64);
+            const int64_t hc = (int64_t)B * users_per_pair(c) / (e->capU + 1) + 1;
+            CF_TRY(dalloc(&e->GU64, (size_t)hc * c.n_factors));
+            CF_HIP(hipMemsetAsync(e->GU64, 0, (size_t)hc * c.n_factors * 8, e->stream));
+            e->hot_cap = hc;
             e->fx_cap = B;
         }
-        if (!e->GU64) {
-            CF_TRY(dalloc(&e->GU64, (size_t)c.n_users * c.n_factors));
-            CF_HIP(hipMemsetAsync(e->GU64, 0, (size_t)c.n_users * c.n_factors * 8, e->stream));
+        if (!e->hotU) {
+            CF_TRY(dalloc(&e->hotU, (size_t)c.n_users));
+            CF_TRY(dalloc(&e->hot_n, 1));
+            CF_HIP(hipMemsetAsync(e->hot_n, 0, sizeof(int), e->stream));
         }
         if (!e->GV64) {
             CF_TRY(dalloc(&e->GV64, (size_t)c.n_items * c.n_factors));
             CF_HIP(hipMemsetAsync(e->GV64, 0, (size_t)c.n_items * c.n_factors * 8, e->stream));
         }
         if (!e->fx_bad) {
-            CF_TRY(dalloc(&e->fx_bad, 1));
-            CF_HIP(hipMemsetAsync(e->fx_bad, 0, sizeof(int), e->stream));
+            CF_TRY(dalloc(&e->fx_bad, (size_t)kFxSlots));
+            CF_HIP(hipMemsetAsync(e->fx_bad, 0, kFxSlots * sizeof(int), e->stream));
+            e->fx_step = 0;
         }
         if (det_fx_path(e, B_step)) return CF_OK;   // the sort-based buffers are not used
     }
@@ -478,12 +501,47 @@ int ensure_batch(cf_engine* e, int B) {
     return CF_OK;
 }
 
+// speculative negative counts (StepArgs::spec_ph) can apply to a batch of B
+// pairs: pos_sort's dense item apply (every item row visited, so a phantom
+// holding rank 0 cannot hide an item from an owner rule) -- the same test as
+// apply_args' dense_items
+// Deterministic mode keeps them off: a phantom raises its item's count, so
+// an item whose only real occurrence shares it with a phantom takes the
+// summed path -- a fixed-point sum of one term, rounded to 2^-32 -- instead of
+// the gradient launch's singleton Adagrad in fp32.  Both are valid steps, but
+// the deterministic result must not depend on a performance option (round 5:
+// BPR / AMF W = 1 spec on vs off differed in the last bits, deterministically).
+bool spec_possible(const cf_engine* e, int64_t B) {
+    return e->spec_neg && !e->det && e->cfg.n_items <= 2 * B * items_per_pair(e->cfg);
+}
+
+// compact negative slot rows for order_cap pairs: phantoms leave holes in the
+// negatives' ranks, so the slots span up to twice the batch's negatives when
+// speculative counts can apply -- otherwise B * W rows (round-4 ADVICE: the
+// doubled array was ~128 MB never used at cfg2 shapes without spec_neg)
+int64_t slotN_need(const cf_engine* e, int64_t cap) {
+    return cap * e->cfg.n_neg * (spec_possible(e, cap) ? 2 : 1);
+}
+
 int ensure_order(cf_engine* e, int B) {
-    if (!psort_possible(e) || (e->srec && B <= e->order_cap)) return CF_OK;
+    if (!psort_possible(e)) return CF_OK;
+    if (e->srec && B <= e->order_cap) {
+        const int64_t need = slotN_need(e, e->order_cap);
+        if (need <= e->slotN_rows) return CF_OK;
+        // spec_neg switched on after the allocation: widen the slots only
+        CF_HIP(hipStreamSynchronize(e->stream));
+        CF_HIP(hipStreamSynchronize(e->side));
+        dfree(e->slotN);
+        e->slotN_rows = 0;
+        CF_TRY(dalloc(&e->slotN, (size_t)need * e->cfg.n_factors));
+        e->slotN_rows = need;
+        return CF_OK;
+    }
     CF_HIP(hipStreamSynchronize(e->stream));
     CF_HIP(hipStreamSynchronize(e->side));
     dfree(e->srec);
     dfree(e->slotN);
+    e->slotN_rows = 0;
     dfree(e->slotP);
     for (int q = 0; q < 2; ++q) {
         dfree(e->spec_ph_[q]);
@@ -493,10 +551,10 @@ int ensure_order(cf_engine* e, int B) {
     // one partial row per (gradient block, positive item): row block + item
     CF_TRY(dalloc(&e->slotP, ((size_t)std::max(B, e->Bcap) / kPsortPPB + 1 + (size_t)e->cfg.n_items) *
                                  e->cfg.n_factors));
-    // compact negative slots offN[j] + rank: the counts include the draw's
-    // phantoms (StepArgs::spec_ph, at most one per negative), whose ranks
-    // leave holes, so the slots span up to twice the batch's negatives
-    CF_TRY(dalloc(&e->slotN, (size_t)std::max(B, e->Bcap) * e->cfg.n_neg * 2 * e->cfg.n_factors));
+    // compact negative slots offN[j] + rank (slotN_need)
+    const int64_t nN = slotN_need(e, std::max(B, e->Bcap));
+    CF_TRY(dalloc(&e->slotN, (size_t)nN * e->cfg.n_factors));
+    e->slotN_rows = nN;
     // at most one phantom per negative (StepArgs::spec_ph)
     for (int q = 0; q < 2; ++q) {
         CF_TRY(dalloc(&e->spec_ph_[q], (size_t)std::max(B, e->Bcap) * e->cfg.n_neg));
@@ -588,7 +646,7 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         // speculative negative counts need the dense item apply of pos_sort
         // (every item row visited: a phantom holding rank 0 cannot hide an
         // item from an owner rule) -- the same test as apply_args
-        if (e->spec_neg && a.count_items && c.n_items <= 2 * (int64_t)B * items_per_pair(c)) {
+        if (a.count_items && spec_possible(e, B) && e->slotN_rows >= 2 * (int64_t)B * c.n_neg) {
             a.spec_ph = e->spec_ph_[k];
             a.spec_n = e->spec_n_[k];
         }
@@ -597,8 +655,9 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
             a.det_fx = 1;
             a.slotP64 = e->slotP64;
             a.GU64 = e->GU64;
+            a.hotU = e->hotU;
             a.GV64 = e->GV64;
-            a.fx_bad = e->fx_bad;
+            a.fx_bad = e->fx_bad + std::min(e->fx_step++, kFxSlots - 1);
         }
     }
     a.shard_u0 = e->shard_u0;
@@ -786,6 +845,8 @@ ApplyArgs apply_args(cf_engine* e, const StepArgs& a, int B, int k, double* loss
     p.det_fx = a.det_fx;
     p.slotP64 = a.slotP64;
     p.GU64 = a.GU64;
+    p.hotU = a.hotU;
+    p.hot_n = a.det_fx ? e->hot_n : nullptr;
     p.GV64 = a.GV64;
     p.fx_bad = a.fx_bad;
     p.d = c.n_factors;
@@ -920,6 +981,10 @@ int psort(cf_engine* e, const StepArgs& a) {
     q.slotN = e->slotN;
     q.cntVw = a.cntV;
     q.d = e->cfg.n_factors;
+    if (a.det_fx) {   // compact GU64 rows for the users past their slot cap
+        q.hotU = e->hotU;
+        q.hot_n = e->hot_n;
+    }
     CF_HIP(launch_psort(q, e->psort_tmp, e->psort_tmp_bytes, e->stream));
     return CF_OK;
 }
@@ -1052,13 +1117,22 @@ int run_items_dense(cf_engine* e) {
 // inf / NaN; the int64 sums would otherwise wrap silently)
 int check_fx(cf_engine* e) {
     if (!e->fx_bad) return CF_OK;
-    CF_HIP(hipMemcpyAsync(e->h_fx_bad, e->fx_bad, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    const int n = std::min(e->fx_step, kFxSlots);
+    e->fx_step = 0;
+    if (n == 0) return CF_OK;
+    CF_HIP(hipMemcpyAsync(e->h_fx_bad, e->fx_bad, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, e->stream));
     CF_HIP(hipStreamSynchronize(e->stream));
-    if (*e->h_fx_bad == 0) return CF_OK;
-    *e->h_fx_bad = 0;
-    CF_HIP(hipMemsetAsync(e->fx_bad, 0, sizeof(int), e->stream));
+    int first = -1;
+    for (int q = 0; q < n && first < 0; ++q)
+        if (e->h_fx_bad[q] != 0) first = q;
+    if (first < 0) return CF_OK;
+    CF_HIP(hipMemsetAsync(e->fx_bad, 0, (size_t)n * sizeof(int), e->stream));
+    const std::string at = first == kFxSlots - 1 ? "at or after step " + std::to_string(first)
+                                                  : "at step " + std::to_string(first);
     return fail(CF_ENUMERIC, "deterministic mode: a gradient term was not finite or outside the "
-                             "fixed-point range (|g| >= 2^20, or a row sum >= 2^30); the step is invalid");
+                             "fixed-point range (|g| >= 2^20, or a row sum >= 2^30) " + at +
+                             " of the steps since the last check (0-based); that step and every later one "
+                             "of the call are invalid");
 }
 
 int read_loss(cf_engine* e, int slot, double* out) {
@@ -1149,7 +1223,7 @@ float** table_slot(cf_engine* e, int t) {
 
 // fused fp32-MFMA scoring + streaming top-k: no score matrix in HBM
 int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclude_train,
-                     int32_t* idx_out, float* val_out) {
+                     const uint64_t* item_mask, int32_t* idx_out, float* val_out) {
     const cf_config& c = e->cfg;
     int32_t* d_users = nullptr;
     int32_t* d_idx = nullptr;
@@ -1178,6 +1252,7 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
     f.idx_out = d_idx;
     f.val_out = d_val;
     f.variant = e->fused_variant;
+    f.item_mask = item_mask;
     hipError_t he = hipMemcpyAsync(d_users, users, (size_t)n * 4, hipMemcpyHostToDevice, e->stream);
     if (he == hipSuccess) {
         ProfScope ps(e, CF_K_TOPK);
@@ -1295,7 +1370,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     e->shard_u1 = c.n_users;
     if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
-    if (hipHostMalloc((void**)&e->h_fx_bad, sizeof(int), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&e->h_fx_bad, kFxSlots * sizeof(int), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
     *e->h_fx_bad = 0;
     hipStream_t s = e->stream;
@@ -1339,6 +1414,7 @@ int cf_destroy(cf_engine* e) {
         if (e->own_tab[t]) *table_slot(e, t) = e->own_tab[t];
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pf_recs[0]); dfree(e->pf_recs[1]); dfree(e->slotP64); dfree(e->GU64); dfree(e->GV64); dfree(e->fx_bad);
+    dfree(e->hotU); dfree(e->hot_n);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
@@ -1348,7 +1424,7 @@ int cf_destroy(cf_engine* e) {
         if (e->prep_done[k]) (void)hipEventDestroy(e->prep_done[k]);
         if (e->apply_done[k]) (void)hipEventDestroy(e->apply_done[k]);
     }
-    dfree(e->loss_partial); dfree(e->loss); dfree(e->keys);
+    dfree(e->loss_partial); dfree(e->loss); dfree(e->keys); dfree(e->item_mask);
     dfree(e->slotU); dfree(e->slotV); dfree(e->slotVb); dfree(e->GVrep); dfree(e->x_own); dfree(e->coefs);
     dfree(e->bounds); dfree(e->xhist); dfree(e->xcounts);
     dfree(e->det_keys); dfree(e->det_vals); dfree(e->det_off); dfree(e->slotUc); dfree(e->slotVc);
@@ -1504,6 +1580,47 @@ int cf_get_table(cf_engine* e, int32_t t, float* dst, int64_t n) {
     return CF_OK;
 }
 
+// every table in one call, in enum cf_table order (U, V, b, AU, AV, Ab);
+// NULL = keep / skip.  All sizes are implied by the config; b and Ab exist
+// only for the bias models (GBPR, CPLR / PRIGP), passing them to another
+// model is CF_EINVAL.  Nothing is copied unless every argument is valid.
+static int params_check(cf_engine* e, const void* const* t) {
+    for (int k = 0; k < 6; ++k) {
+        if (!t[k]) continue;
+        int64_t n = 0;
+        if (!table_ptr(e, k, &n)) return fail(CF_EINVAL, "table " + std::to_string(k) + " not present in this model");
+    }
+    return CF_OK;
+}
+
+int cf_set_params(cf_engine* e, const float* U, const float* V, const float* b, const float* AU,
+                  const float* AV, const float* Ab) {
+    CF_TRY(check_engine(e));
+    const void* t[6] = {U, V, b, AU, AV, Ab};
+    CF_TRY(params_check(e, t));
+    for (int k = 0; k < 6; ++k) {
+        if (!t[k]) continue;
+        int64_t n = 0;
+        table_ptr(e, k, &n);
+        CF_TRY(cf_set_table(e, k, (const float*)t[k], n));
+    }
+    return CF_OK;
+}
+
+int cf_get_params(cf_engine* e, float* U, float* V, float* b, float* AU, float* AV, float* Ab) {
+    CF_TRY(check_engine(e));
+    float* t[6] = {U, V, b, AU, AV, Ab};
+    const void* tc[6] = {U, V, b, AU, AV, Ab};
+    CF_TRY(params_check(e, tc));
+    for (int k = 0; k < 6; ++k) {
+        if (!t[k]) continue;
+        int64_t n = 0;
+        table_ptr(e, k, &n);
+        CF_TRY(cf_get_table(e, k, t[k], n));
+    }
+    return CF_OK;
+}
+
 int cf_step(cf_engine* e, const int32_t* pairs, const int32_t* negs, const int32_t* groups,
             int32_t B, double* loss_out) {
     CF_TRY(check_engine(e));
@@ -1574,6 +1691,28 @@ int cf_train_steps(cf_engine* e, int32_t B, int32_t n_steps, double* loss_sum_ou
     return CF_OK;
 }
 
+// One training epoch of the device sampler, as one iteration of the
+// reference's loop: n_batches = int(len(pairs) / batch_size) steps
+// (bprmf.py:138-148), their mean pre-update batch loss as TraLoss
+// (aveloss = np.mean(losses), bprmf.py:150).  The steps end at an epoch
+// boundary: from a boundary (or after steps at another B) that is a whole
+// epoch; from inside an epoch, the batches it has left.
+int cf_train_epoch(cf_engine* e, int32_t B, double* mean_loss_out) {
+    CF_TRY(check_engine(e));
+    if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
+    if (!e->pairs) return fail(CF_ESTATE, "no interactions: call cf_set_interactions first");
+    if ((int64_t)B > e->nnz) return fail(CF_EINVAL, "batch size exceeds the number of interactions");
+    CF_TRY(discard_pending(e));   // the sampler position a caller sees
+    const int64_t per_epoch = e->nnz / B;
+    int64_t left = per_epoch;
+    if (e->sampler_B == B && e->batch > 0 && e->batch < per_epoch) left = per_epoch - e->batch;
+    if (left > INT32_MAX) return fail(CF_EINVAL, "epoch too long for one call");
+    double sum = 0.0;
+    CF_TRY(cf_train_steps(e, B, (int32_t)left, mean_loss_out ? &sum : nullptr));
+    if (mean_loss_out) *mean_loss_out = sum / (double)left;
+    return CF_OK;
+}
+
 int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* groups) {
     CF_TRY(check_engine(e));
     CF_TRY(discard_pending(e));
@@ -1585,6 +1724,7 @@ int cf_sample(cf_engine* e, int32_t B, int32_t* pairs, int32_t* negs, int32_t* g
     const int k = e->set;
     e->set ^= 1;
     StepArgs a = base_step_args(e, B, k);
+    if (a.det_fx && e->fx_step > 0) e->fx_step -= 1;   // a draw, not a step: no range-flag word
     CF_TRY(sampler_args(e, B, &a));
     a.count_users = 0;
     a.count_items = 0;
@@ -1823,6 +1963,10 @@ int cf_step_local_draw(cf_engine* e, int32_t B) {
 int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
                   const int32_t* groups) {
     CF_TRY(cf_step_local_grad(e, B, pairs, negs, groups));
+    // the one-call form has no caller collective between item-reduce pieces
+    // (item_pieces > 1 defers them): reduce every remaining piece here, so the
+    // apply finds the item gradient complete
+    while (e->lg_pieces_left > 0) CF_TRY(cf_step_item_reduce(e, e->item_pieces - e->lg_pieces_left));
     return cf_step_local_apply(e, 0);
 }
 
@@ -2228,14 +2372,45 @@ int cf_take_loss(cf_engine* e, double* out) {
     return read_loss(e, 0, out);
 }
 
-int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int32_t exclude_train,
+int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, const uint8_t* mask_or_NULL,
                   int32_t* idx_out, float* val_out) {
+    // NULL: the reference's filter (each user's train items); a mask: exactly
+    // the items it flags, for every user
+    return cf_score_topk_ex(e, users, n, k, mask_or_NULL ? 0 : 1, mask_or_NULL, idx_out, val_out);
+}
+
+int cf_score_topk_ex(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int32_t exclude_train,
+                     const uint8_t* item_mask, int32_t* idx_out, float* val_out) {
     CF_TRY(check_engine(e));
     const cf_config& c = e->cfg;
     if (n < 0 || !idx_out || (n > 0 && !users)) return fail(CF_EINVAL, "bad arguments");
     if (k < 1 || k > 4096) return fail(CF_EINVAL, "k must be 1..4096");
     if (exclude_train && !e->indptr) return fail(CF_ESTATE, "exclude_train needs cf_set_interactions");
     if (n == 0) return CF_OK;
+    // the caller's item mask (uint8 [n_items], host or device) as one bit per
+    // item, 64 items per word -- the fused kernel ORs one word into each
+    // 64-item tile's exclusion mask, the materialised path zeroes the keys
+    const uint64_t* d_mask = nullptr;
+    if (item_mask) {
+        const int64_t nw = (c.n_items + 63) / 64;
+        std::vector<uint8_t> hm;
+        if (is_device_ptr(item_mask)) {
+            hm.resize((size_t)c.n_items);
+            CF_HIP(hipMemcpy(hm.data(), item_mask, (size_t)c.n_items, hipMemcpyDeviceToHost));
+            item_mask = hm.data();
+        }
+        std::vector<uint64_t> bits((size_t)nw, 0ull);
+        for (int64_t j = 0; j < c.n_items; ++j)
+            if (item_mask[j]) bits[(size_t)(j >> 6)] |= 1ull << (j & 63);
+        if (e->mask_words < nw) {
+            dfree(e->item_mask);
+            CF_TRY(dalloc(&e->item_mask, (size_t)nw));
+            e->mask_words = nw;
+        }
+        CF_HIP(hipMemcpyAsync(e->item_mask, bits.data(), (size_t)nw * 8, hipMemcpyHostToDevice, e->stream));
+        CF_HIP(hipStreamSynchronize(e->stream));   // `bits` is pageable and local
+        d_mask = e->item_mask;
+    }
     std::vector<int32_t> host_users;
     if (is_device_ptr(users)) {  // device ids (torch): checked from a host copy
         host_users.resize((size_t)n);
@@ -2245,11 +2420,11 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
     for (int r = 0; r < n; ++r)
         if (users[r] < 0 || users[r] >= c.n_users) return fail(CF_EINVAL, "user id out of range");
     CF_HIP(hipStreamSynchronize(e->side));
-    const bool fused_ok = k <= kFusedMaxK && c.n_factors <= kFusedMaxD;
+    const bool fused_ok = k <= kFusedMaxWideK && c.n_factors <= kFusedMaxD;
     if (e->topk_path == 2 && !fused_ok)
-        return fail(CF_EINVAL, "fused top-k needs k <= 28 and n_factors <= 128");
+        return fail(CF_EINVAL, "fused top-k needs k <= 128 and n_factors <= 128");
     if (fused_ok && e->topk_path != 1)
-        return score_topk_fused(e, users, n, k, exclude_train, idx_out, val_out);
+        return score_topk_fused(e, users, n, k, exclude_train, d_mask, idx_out, val_out);
     const size_t row_bytes = (size_t)c.n_items * 4;
     const size_t budget = (size_t)512 << 20;
     int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)n, budget / row_bytes));
@@ -2283,6 +2458,7 @@ int cf_score_topk(cf_engine* e, const int32_t* users, int32_t n, int32_t k, int3
         s.exclude_train = exclude_train ? 1 : 0;
         s.indptr = e->indptr;
         s.indices = e->indices;
+        s.item_mask = d_mask;
         {
             ProfScope ps(e, CF_K_SCORE);
             he = launch_score(s, e->stream);
@@ -2374,6 +2550,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         CF_HIP(hipStreamSynchronize(e->stream));
         if (n == "slot_max") e->capV = (int)value; else e->capU = (int)value;
         e->slots_ready = false;   // re-sized at the next step
+        if (n == "slot_max_user") e->fx_cap = 0;   // the compact GU64 rows scale with 1 / (capU + 1)
         return CF_OK;
     }
     if (n == "hot_replicas") {

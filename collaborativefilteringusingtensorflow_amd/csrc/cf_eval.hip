@@ -70,7 +70,9 @@ __global__ __launch_bounds__(kBlock) void score_kernel(ScoreArgs a) {
             float s = acc[m][n];
             if (MODEL == CML) s = -s;
             if (MODEL == GBPR) s += a.b[ii];
-            a.keys[(int64_t)uu * a.n_items + ii] = float_key(s);
+            // key 0 = excluded: the caller's item mask here, train items by mask_train_kernel
+            const bool off = a.item_mask != nullptr && ((a.item_mask[ii >> 6] >> (ii & 63)) & 1ull);
+            a.keys[(int64_t)uu * a.n_items + ii] = off ? 0u : float_key(s);
         }
     }
 }
@@ -248,44 +250,97 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
     return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
-// one wave sorts a user's <=128 candidates descending, keeps the best `keep`
-// (<= 64) in place and returns how many it kept
+// one wave sorts a user's <= 64 R candidates descending (R registers per
+// lane: entry e = lane + 64 r), keeps the best `keep` (<= 64 R - 64) in place
+// and returns how many it kept; the k-th best becomes the row's threshold
+template <int R>
 __device__ int wave_compact(unsigned long long* __restrict__ buf, int* cnt,
                             unsigned long long* thr, int keep, int k) {
     const int lane = lane_id();
     const int n = *cnt;
-    unsigned long long x0 = lane < n ? buf[lane] : 0ull;
-    unsigned long long x1 = lane + 64 < n ? buf[lane + 64] : 0ull;
-    for (int size = 2; size <= 128; size <<= 1) {
+    if constexpr (R == 2) {   // the two-block-per-CU kernel's form (its register budget is tight)
+        unsigned long long x0 = lane < n ? buf[lane] : 0ull;
+        unsigned long long x1 = lane + 64 < n ? buf[lane + 64] : 0ull;
+        for (int size = 2; size <= 128; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                if (stride == 64) {  // partner is the lane's other register; size == 128
+                    if (x0 < x1) { const unsigned long long t = x0; x0 = x1; x1 = t; }
+                    continue;
+                }
+                const bool lower = (lane & stride) == 0;
+                {
+                    const unsigned long long y = shfl_xor_u64(x0, stride);
+                    const bool desc = (lane & size) == 0;
+                    const unsigned long long mx = x0 > y ? x0 : y, mn = x0 > y ? y : x0;
+                    x0 = (desc == lower) ? mx : mn;
+                }
+                {
+                    const unsigned long long y = shfl_xor_u64(x1, stride);
+                    const bool desc = ((lane + 64) & size) == 0;
+                    const unsigned long long mx = x1 > y ? x1 : y, mn = x1 > y ? y : x1;
+                    x1 = (desc == lower) ? mx : mn;
+                }
+            }
+        }
+        const int m = n < keep ? n : keep;
+        if (lane < m) buf[lane] = x0;            // keep <= 64
+        const unsigned long long kth = shfl_u64(x0, k - 1);
+        if (lane == 0) {
+            *cnt = m;
+            if (m >= k) *thr = kth;
+        }
+        return m;
+    }
+    unsigned long long x[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) x[r] = lane + 64 * r < n ? buf[lane + 64 * r] : 0ull;
+    for (int size = 2; size <= 64 * R; size <<= 1) {
         for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride == 64) {  // partner is the lane's other register; size == 128
-                if (x0 < x1) { const unsigned long long t = x0; x0 = x1; x1 = t; }
+            if (stride >= 64) {   // partners in the lane's own registers r, r | rs
+                const int rs = stride >> 6;
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if ((r & rs) != 0) continue;
+#pragma unroll
+                    for (int r2 = 0; r2 < R; ++r2) {
+                        if (r2 != (r | rs)) continue;
+                        const bool desc = ((lane + 64 * r) & size) == 0;
+                        const unsigned long long mx = x[r] > x[r2] ? x[r] : x[r2];
+                        const unsigned long long mn = x[r] > x[r2] ? x[r2] : x[r];
+                        x[r] = desc ? mx : mn;
+                        x[r2] = desc ? mn : mx;
+                    }
+                }
                 continue;
             }
             const bool lower = (lane & stride) == 0;
-            {
-                const unsigned long long y = shfl_xor_u64(x0, stride);
-                const bool desc = (lane & size) == 0;
-                const unsigned long long mx = x0 > y ? x0 : y, mn = x0 > y ? y : x0;
-                x0 = (desc == lower) ? mx : mn;
-            }
-            {
-                const unsigned long long y = shfl_xor_u64(x1, stride);
-                const bool desc = ((lane + 64) & size) == 0;
-                const unsigned long long mx = x1 > y ? x1 : y, mn = x1 > y ? y : x1;
-                x1 = (desc == lower) ? mx : mn;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const unsigned long long y = shfl_xor_u64(x[r], stride);
+                const bool desc = ((lane + 64 * r) & size) == 0;
+                const unsigned long long mx = x[r] > y ? x[r] : y, mn = x[r] > y ? y : x[r];
+                x[r] = (desc == lower) ? mx : mn;
             }
         }
     }
     const int m = n < keep ? n : keep;
-    if (lane < m) buf[lane] = x0;            // keep <= 64
-    const unsigned long long kth = shfl_u64(x0, k - 1);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (lane + 64 * r < m) buf[lane + 64 * r] = x[r];
+    unsigned long long xk = x[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r)
+        if (r == ((k - 1) >> 6)) xk = x[r];
+    const unsigned long long kth = shfl_u64(xk, (k - 1) & 63);
     if (lane == 0) {
         *cnt = m;
         if (m >= k) *thr = kth;
     }
     return m;
 }
+
+// sort registers per lane for a candidate list of CAP slots
+__host__ __device__ constexpr int fused_sort_regs(int cap) { return cap <= 64 ? 1 : cap <= 128 ? 2 : 4; }
 
 // V tile in LDS: 64 rows x 128 floats, no padding; the 16-B chunk q of row r
 // sits at chunk q ^ (r & 31), so the 16 lanes of a ds_read_b128 phase (rows
@@ -313,11 +368,17 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 #ifndef CF_FUSED_BPREFETCH
 #define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
-template <int MODEL>
-__global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) {
-    // ~80 KB of LDS: two blocks per CU.  The user operands live in registers.
+// CAP: candidate slots per user.  kFusedCap (92, k <= 28): ~80 KB of LDS,
+// two blocks per CU.  kFusedCapWide (192, k <= 128; round 5, GBPR's topN =
+// 100): ~130 KB, one block per CU.
+// MASK: the caller's item mask is read (a.item_mask may still be null); the
+// narrow kernel without it keeps its register budget (GBPR: 16 B less spill)
+template <int MODEL, int CAP = kFusedCap, bool MASK = false>
+__global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_kernel(FusedTopkArgs a) {
+    // The user operands live in registers.
+    constexpr int SR = fused_sort_regs(CAP);
     __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFusedMaxD];
-    __shared__ unsigned long long buf[kFusedUsers * kFusedCap];
+    __shared__ unsigned long long buf[kFusedUsers * CAP];
     __shared__ unsigned long long thr[kFusedUsers];
     __shared__ unsigned long long mask[kFusedUsers];
     __shared__ int cnt[kFusedUsers];
@@ -421,7 +482,9 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
         if (MODEL == GBPR && tid < kFusedItems)
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
         if (tid < kFusedUsers) {
-            unsigned long long m = 0ull;
+            // the caller's item exclusions (one word per 64-item tile), then
+            // the user's train items
+            unsigned long long m = (MASK && a.item_mask != nullptr) ? a.item_mask[j0 >> 6] : 0ull;
             while (nxt < j0 + kFusedItems) {   // sorted row: no load unless an item is consumed
                 m |= 1ull << (int)(nxt - j0);
                 ++cur;
@@ -533,7 +596,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                                                    (0xFFFFFFFFull - (unsigned long long)J);
                     if (key > thr[R]) {
                         const int pos = atomicAdd(&cnt[R], 1);
-                        buf[R * kFusedCap + pos] = key;
+                        buf[R * CAP + pos] = key;
                     }
                 }
             }
@@ -582,7 +645,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                                                    (0xFFFFFFFFull - (unsigned long long)J);
                     if (key > thr[R]) {
                         const int pos = atomicAdd(&cnt[R], 1);
-                        buf[R * kFusedCap + pos] = key;
+                        buf[R * CAP + pos] = key;
                     }
                 }
             }
@@ -601,7 +664,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
                                                (0xFFFFFFFFull - (unsigned long long)J);
                 if (key > thr[R]) {
                     const int pos = atomicAdd(&cnt[R], 1);
-                    buf[R * kFusedCap + pos] = key;
+                    buf[R * CAP + pos] = key;
                 }
             }
         }
@@ -618,14 +681,14 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
             constexpr int kRowsPerWave = kFusedUsers / kWavesPerBlock;
             const int Rl = wv + kWavesPerBlock * lane;
             unsigned long long need = __ballot(lane < kRowsPerWave && Rl < nu &&
-                                               cnt[lane < kRowsPerWave ? Rl : 0] > kFusedCap - kFusedItems);
+                                               cnt[lane < kRowsPerWave ? Rl : 0] > CAP - kFusedItems);
             if (need != 0ull) {
                 if (lane == 0) atomicAdd(&thr_ver, 1);
                 while (need != 0ull) {
                     const int l = __ffsll((long long)need) - 1;
                     need &= need - 1ull;
                     const int R = wv + kWavesPerBlock * l;
-                    wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+                    wave_compact<SR>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
                 }
             }
         }
@@ -633,18 +696,18 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_kernel(FusedTopkArgs a) 
     }
     // ---- final sort and output -------------------------------------------------------
     for (int R = wv; R < nu; R += kWavesPerBlock) {
-        const int n = wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        const int n = wave_compact<SR>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
         const int64_t orow = (int64_t)(u0 + R) * a.k;
-        if (lane < a.k) {
+        for (int o = lane; o < a.k; o += (CAP <= kFusedCap ? a.k : kWave)) {   // k <= 28: one pass
             int id = -1;
             float v = __int_as_float(0x7fc00000);
-            if (lane < n) {
-                const unsigned long long e = buf[R * kFusedCap + lane];
+            if (o < n) {
+                const unsigned long long e = buf[R * CAP + o];
                 id = (int)(0xFFFFFFFFull - (e & 0xFFFFFFFFull));
                 v = key_float((uint32_t)(e >> 32));
             }
-            a.idx_out[orow + lane] = id;
-            if (a.val_out) a.val_out[orow + lane] = v;
+            a.idx_out[orow + o] = id;
+            if (a.val_out) a.val_out[orow + o] = v;
         }
     }
 }
@@ -806,7 +869,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
                 const int l = __ffsll((long long)need) - 1;
                 need &= need - 1ull;
                 const int R = wv + kWavesPerBlock * l;
-                wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+                wave_compact<fused_sort_regs(kFusedCap)>(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
             }
         }
     };
@@ -822,7 +885,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
         if (MODEL == GBPR && tid < kFusedItems)
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
         if (tid < kFusedUsers) {
-            unsigned long long m = 0ull;
+            unsigned long long m = a.item_mask != nullptr ? a.item_mask[j0 >> 6] : 0ull;
             while (nxt < j0 + kFusedItems) {
                 m |= 1ull << (int)(nxt - j0);
                 ++cur;
@@ -906,7 +969,7 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
     }
     __syncthreads();
     for (int R = wv; R < nu; R += kWavesPerBlock) {
-        const int n = wave_compact(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
+        const int n = wave_compact<fused_sort_regs(kFusedCap)>(buf + R * kFusedCap, &cnt[R], &thr[R], a.k, a.k);
         const int64_t orow = (int64_t)(u0 + R) * a.k;
         if (lane < a.k) {
             int id = -1;
@@ -927,11 +990,28 @@ hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
     const dim3 grid((a.n_users + kFusedUsers - 1) / kFusedUsers), block(kBlock);
     // CML's distance transform does not fit the pipelined kernel's registers
     // at two blocks per CU (its A operands spill): it keeps the sequential one
-    if (a.variant == 1 && a.model != CML) {
+    if (a.k > kFusedMaxWideK) return hipErrorInvalidValue;   // the host checks first
+    if (a.variant == 1 && a.model != CML && a.k <= kFusedMaxK && a.item_mask == nullptr) {
         if (a.model == GBPR)
             hipLaunchKernelGGL(fused_topk_pipe_kernel<GBPR>, grid, block, 0, s, a);
         else
             hipLaunchKernelGGL(fused_topk_pipe_kernel<BPR>, grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.k > kFusedMaxK) {   // 28 < k <= 128: the wide lists, one block per CU
+        switch (a.model) {
+            case GBPR: hipLaunchKernelGGL((fused_topk_kernel<GBPR, kFusedCapWide, true>), grid, block, 0, s, a); break;
+            case CML: hipLaunchKernelGGL((fused_topk_kernel<CML, kFusedCapWide, true>), grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL((fused_topk_kernel<BPR, kFusedCapWide, true>), grid, block, 0, s, a); break;
+        }
+        return hipGetLastError();
+    }
+    if (a.item_mask != nullptr) {
+        switch (a.model) {
+            case GBPR: hipLaunchKernelGGL((fused_topk_kernel<GBPR, kFusedCap, true>), grid, block, 0, s, a); break;
+            case CML: hipLaunchKernelGGL((fused_topk_kernel<CML, kFusedCap, true>), grid, block, 0, s, a); break;
+            default: hipLaunchKernelGGL((fused_topk_kernel<BPR, kFusedCap, true>), grid, block, 0, s, a); break;
+        }
         return hipGetLastError();
     }
     switch (a.model) {

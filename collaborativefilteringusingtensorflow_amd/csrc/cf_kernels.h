@@ -87,7 +87,10 @@ struct StepArgs {
     // int64 atomics (GU64), the per-pair losses add as integers (kFxLoss)
     int det_fx;
     long long* __restrict__ slotP64;        // [B / kPsortPPB + 1 + n_items, d] (as slotP)
-    unsigned long long* __restrict__ GU64;  // [n_users, d], zero between steps
+    // users past their slot cap: compact int64 rows (round 5; was [n_users, d],
+    // 512 MB at cfg2): psort gives each such user a row hotU[u] in the batch
+    unsigned long long* __restrict__ GU64;  // [hot rows, d], zero between steps
+    const int32_t* __restrict__ hotU;       // [n_users] compact row of a user past its cap (this batch)
     unsigned long long* __restrict__ GV64;  // [n_items, d]: positive partials past capP, zero between steps
     int* __restrict__ fx_bad;               // set when a term / sum leaves the fixed-point range (to_fx)
     // speculative negative counts (round 4; pos_sort with the dense item
@@ -222,7 +225,9 @@ struct XchgArgs {
 struct ApplyArgs {
     int det_fx;                               // fixed-point sums (StepArgs::det_fx)
     const long long* __restrict__ slotP64;
-    unsigned long long* __restrict__ GU64;
+    unsigned long long* __restrict__ GU64;   // StepArgs::GU64 (compact rows via hotU)
+    const int32_t* __restrict__ hotU;
+    int* __restrict__ hot_n;                 // the compact rows handed out by psort; block 0 re-zeroes it
     unsigned long long* __restrict__ GV64;
     int* __restrict__ fx_bad;                 // StepArgs::fx_bad
     int d;
@@ -328,14 +333,19 @@ struct ScoreArgs {
     int exclude_train;
     const int64_t* __restrict__ indptr;
     const int32_t* __restrict__ indices;
+    const uint64_t* __restrict__ item_mask;   // [ceil(n_items / 64)] excluded items (bit j % 64 of word j / 64), nullable
 };
 
-// fused scoring GEMM (fp32 MFMA) + streaming per-user top-k, d <= 128, k <= 28
+// fused scoring GEMM (fp32 MFMA) + streaming per-user top-k, d <= 128, k <= 128
 constexpr int kFusedUsers = 64;
 constexpr int kFusedItems = 64;
 constexpr int kFusedMaxD = 128;
 constexpr int kFusedCap = 92;    // candidate slots per user (LDS for two blocks per CU)
 constexpr int kFusedMaxK = kFusedCap - kFusedItems;   // a compacted list + one tile's 64 fit
+// 28 < k <= 128 (round 5: GBPR's topN = 100, testgbprmf.py:23-32): 192 slots
+// per user, ~130 KB of LDS, one block per CU
+constexpr int kFusedCapWide = 192;
+constexpr int kFusedMaxWideK = kFusedCapWide - kFusedItems;
 
 struct FusedTopkArgs {
     int model;
@@ -353,6 +363,7 @@ struct FusedTopkArgs {
     int32_t* __restrict__ idx_out;       // [n_users, k]
     float* __restrict__ val_out;         // [n_users, k] (nullable)
     int variant;                         // 0: the sequential kernel, 1: software-pipelined (A/B)
+    const uint64_t* __restrict__ item_mask;   // as ScoreArgs::item_mask, nullable
 };
 
 struct TopkArgs {
@@ -423,6 +434,10 @@ struct PsortArgs {
     const int32_t* occU; const int32_t* rankU;
     const int32_t* occV; const int32_t* rankV;
     const int32_t* cntU;                 // the batch's final counts
+    // deterministic mode: a user's occurrence of rank capU (the user is past
+    // its slot cap) takes the next compact GU64 row, hotU[u] (null = off)
+    int32_t* hotU;
+    int* hot_n;
     const int32_t* cntV; const int32_t* cntP;
     int2* offPN;                         // written: [n_items + 1] exclusive scans of (cntP, cntV)
     int32_t* srec;                       // [B, psort_stride(W)]

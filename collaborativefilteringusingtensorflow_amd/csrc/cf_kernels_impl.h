@@ -1467,7 +1467,7 @@ __device__ __forceinline__ void gfinish_pre(float* __restrict__ X, float* __rest
     } else {
 #ifndef CF_EXP_NO_ATOMIC
         if (a.GU64 != nullptr && X == a.U)   // deterministic pos_sort: a user past its slot cap
-            fx_atomic<EPL>(a.GU64 + r * (int64_t)d, d, gl, g, a.fx_bad);
+            fx_atomic<EPL>(a.GU64 + (int64_t)a.hotU[r] * d, d, gl, g, a.fx_bad);
         else
             gatomic<EPL>(acc_of(G, slot, a), r, d, gl, g);
 #endif
@@ -1937,13 +1937,16 @@ __device__ __forceinline__ void grad_fast_body(const StepArgs& a, int block) {
     }
 }
 
-template <int MODEL, int EPL, int WT, int P, bool DRAW, bool SORT = false>
+// FULL (round 5): as grad_sort_kernel's, for the phased kernel without draw
+// blocks -- cfg2 at SURVEY's B = 65,536 (pos_sort off) runs this one
+template <int MODEL, int EPL, int WT, int P, bool DRAW, bool SORT = false, bool FULL = false>
 #ifdef CF_GRAD_WAVES_PER_EU
 #define CF_GRAD_ATTR __attribute__((amdgpu_waves_per_eu(CF_GRAD_WAVES_PER_EU, 8)))
 #else
 #define CF_GRAD_ATTR
 #endif
 __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs a, StepArgs nx, int ng, int np) {
+    if constexpr (FULL) __builtin_assume(a.d == kGL * EPL);
     int idx = blockIdx.x;
     if (DRAW && minor_block(blockIdx.x, ng, np, idx))
         prep_any<MODEL == GBPR ? GBPR : BPR>(nx, idx);
@@ -1961,6 +1964,9 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #endif
 #ifndef CF_ASSUME_FULL_ROWS
 #define CF_ASSUME_FULL_ROWS 1
+#endif
+#ifndef CF_ASSUME_FULL_FAST
+#define CF_ASSUME_FULL_FAST 1   // grad_fast_kernel's FULL instantiation at d = 64 (round 5)
 #endif
 // the same for apply_ps_kernel: measured even at cfg2/4/5 (round 4) -- the
 // apply hoists more loads (79 -> 92 VGPRs, one wave per SIMD less), off
@@ -2585,7 +2591,7 @@ __device__ __forceinline__ void apply_row(const ApplyArgs& a, int64_t r, bool is
                 }
         }
         if (local > cap) {
-            unsigned long long* row = a.GU64 + r * (int64_t)a.d;
+            unsigned long long* row = a.GU64 + (int64_t)a.hotU[r] * a.d;
             fx_ld_add<EPL>(reinterpret_cast<const long long*>(row), a.d, gl, t);
             long long z[EPL];
 #pragma unroll
@@ -2921,6 +2927,8 @@ __global__ __launch_bounds__(kBlock, CF_APPLY_MIN_WAVES) void apply_ps_kernel(Ap
     if constexpr (FULL) __builtin_assume(p.d == kGL * EPL);
     int b = blockIdx.x;
     if (blockIdx.x == 0 && p.loss_acc != nullptr) fold_loss<kBlock>(p);
+    // the compact GU64 rows of this batch are handed out again by the next psort
+    if (FX && blockIdx.x == 0 && threadIdx.x == 0 && p.hot_n != nullptr) *p.hot_n = 0;
     if constexpr (DRAW && !CF_APPLY_DRAW_TAIL) {
         int idx;
         if (minor_block(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)) {
@@ -3360,10 +3368,14 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
             default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, true>), grid, block, 0, s, a, n, ng, np); break;
         }
     } else {
+        const bool full = CF_ASSUME_FULL_FAST && a.d == kGL * epl_for(a.d);
         switch (epl_for(a.d)) {
             case 1: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 1, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
             case 2: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 2, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
-            case 4: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
+            case 4:
+                if (full) hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false, false, true>), grid, block, 0, s, a, n, ng, 0);
+                else hipLaunchKernelGGL((grad_fast_kernel<MODEL, 4, WT, P, false>), grid, block, 0, s, a, n, ng, 0);
+                break;
             default: hipLaunchKernelGGL((grad_fast_kernel<MODEL, 8, WT, P, false>), grid, block, 0, s, a, n, ng, 0); break;
         }
     }

@@ -152,6 +152,37 @@ class Engine(object):
                 "cf_get_table(%s)" % name)
         return out
 
+    PARAM_TABLES = ("user", "item", "bias", "acc_user", "acc_item", "acc_bias")
+
+    def set_params(self, **tables):
+        """cf_set_params: any of user, item, bias, acc_user, acc_item,
+        acc_bias in one call (the others kept)."""
+        bad = set(tables) - set(self.PARAM_TABLES)
+        if bad:
+            raise ValueError("unknown tables %s" % sorted(bad))
+        keep, ptrs = [], []
+        for name in self.PARAM_TABLES:
+            a = tables.get(name)
+            if a is None:
+                ptrs.append(None)
+                continue
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            if a.shape != self._table_shape(name):
+                raise ValueError("table %s must have shape %s" % (name, self._table_shape(name)))
+            keep.append(a)
+            ptrs.append(_ptr(a, ctypes.c_float))
+        N.check(self._L.cf_set_params(self._h, *ptrs), "cf_set_params")
+
+    def get_params(self, names=None):
+        """cf_get_params: {name: array} for ``names`` (default every table
+        the model has)."""
+        has_bias = self.model in (N.CF_GBPR, N.CF_PLR)
+        names = names or [t for t in self.PARAM_TABLES if has_bias or "bias" not in t]
+        out = {n: np.empty(self._table_shape(n), dtype=np.float32) for n in names}
+        N.check(self._L.cf_get_params(self._h, *[_ptr(out[t], ctypes.c_float) if t in out else None
+                                                 for t in self.PARAM_TABLES]), "cf_get_params")
+        return out
+
     # ---- training -------------------------------------------------------------
     def _batch(self, pairs, negs, groups):
         if _is_dev(pairs):   # torch device tensors: staged on the device (cf_step docs)
@@ -218,6 +249,14 @@ class Engine(object):
         N.check(self._L.cf_train_steps(self._h, int(batch_size), int(n_steps),
                                        ctypes.byref(loss) if return_loss else None),
                 "cf_train_steps")
+        return float(loss.value) if return_loss else None
+
+    def train_epoch(self, batch_size, return_loss=True):
+        """One iteration of the reference's train loop (cf_train_epoch): the
+        sampler's epoch to its end, returning the mean batch loss (TraLoss)."""
+        loss = ctypes.c_double(0.0)
+        N.check(self._L.cf_train_epoch(self._h, int(batch_size), ctypes.byref(loss) if return_loss else None),
+                "cf_train_epoch")
         return float(loss.value) if return_loss else None
 
     def sample(self, batch_size):
@@ -385,28 +424,57 @@ class Engine(object):
         return float(v.value)
 
     # ---- evaluation -------------------------------------------------------------
-    def score_topk(self, users, k, exclude_train=True, return_values=False):
+    def score_topk(self, users, k, exclude_train=True, return_values=False, item_mask=None):
+        """Top-k items per user (cf_score_topk_ex): exclude_train drops each
+        user's train items (the reference's __recommend filter), item_mask
+        (bool / uint8 [n_items], numpy or a torch device tensor) drops the
+        flagged items for every user on top."""
+        mp, mkeep = None, None
+        if item_mask is not None:
+            if _is_dev(item_mask):
+                import torch
+                mkeep, _ = _dev(item_mask.reshape(-1), torch.uint8, ctypes.c_uint8)
+                mp = ctypes.c_void_p(mkeep.data_ptr())
+            else:
+                mkeep = np.ascontiguousarray(item_mask, dtype=np.uint8).reshape(-1)
+                mp = ctypes.c_void_p(mkeep.ctypes.data)
+            if mkeep.shape[0] != self.n_items:
+                raise ValueError("item_mask must have n_items entries")
         if _is_dev(users):   # device ids in, device results out
             import torch
             u, up = _dev(users.reshape(-1), torch.int32, ctypes.c_int32)
             n = u.shape[0]
             idx = torch.empty((n, int(k)), dtype=torch.int32, device=u.device)
             val = torch.empty((n, int(k)), dtype=torch.float32, device=u.device) if return_values else None
-            N.check(self._L.cf_score_topk(
-                self._h, up, n, int(k), 1 if exclude_train else 0,
+            N.check(self._L.cf_score_topk_ex(
+                self._h, up, n, int(k), 1 if exclude_train else 0, mp,
                 ctypes.cast(idx.data_ptr(), ctypes.POINTER(ctypes.c_int32)),
                 ctypes.cast(val.data_ptr(), ctypes.POINTER(ctypes.c_float)) if return_values else None),
-                "cf_score_topk")
+                "cf_score_topk_ex")
             return (idx, val) if return_values else idx
         users = _i32(users).reshape(-1)
         n = users.shape[0]
         idx = np.empty((n, int(k)), dtype=np.int32)
         val = np.empty((n, int(k)), dtype=np.float32) if return_values else None
-        N.check(self._L.cf_score_topk(self._h, _ptr(users, ctypes.c_int32), n, int(k),
-                                      1 if exclude_train else 0, _ptr(idx, ctypes.c_int32),
-                                      _ptr(val, ctypes.c_float) if return_values else None),
-                "cf_score_topk")
+        N.check(self._L.cf_score_topk_ex(self._h, _ptr(users, ctypes.c_int32), n, int(k),
+                                         1 if exclude_train else 0, mp, _ptr(idx, ctypes.c_int32),
+                                         _ptr(val, ctypes.c_float) if return_values else None),
+                "cf_score_topk_ex")
         return (idx, val) if return_values else idx
+
+    def recommend(self, users, k, mask=None):
+        """cf_score_topk with SURVEY 8(b)'s mask_or_NULL: None = exclude each
+        user's train items; a uint8 [n_items] mask = exactly those items."""
+        users = _i32(users).reshape(-1)
+        n = users.shape[0]
+        idx = np.empty((n, int(k)), dtype=np.int32)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8).reshape(-1)
+        if m is not None and m.shape[0] != self.n_items:
+            raise ValueError("mask must have n_items entries")
+        N.check(self._L.cf_score_topk(self._h, _ptr(users, ctypes.c_int32), n, int(k),
+                                      None if m is None else ctypes.c_void_p(m.ctypes.data),
+                                      _ptr(idx, ctypes.c_int32), None), "cf_score_topk")
+        return idx
 
     PATH_FLAGS = {"phased": 1, "pos_sort": 2, "item_records": 4, "deterministic": 8, "dense_items": 16,
                   "lds": 32}

@@ -176,6 +176,19 @@ int cf_set_table(cf_engine* eng, int32_t table, const float* host_src,
                  int64_t n_elems);
 int cf_get_table(cf_engine* eng, int32_t table, float* host_dst,
                  int64_t n_elems);
+/*
+ * Every parameter table in one call, enum cf_table order:
+ * U [n_users,d], V [n_items,d], b [n_items], AU, AV, Ab (the model's
+ * variables and their Adagrad slots: bprmf.py:24-34 + the optimizer's
+ * accumulators; checkpoint / restore).  NULL = keep (set) or skip (get); b
+ * and Ab exist only for the bias models (GBPR, PLR) -- non-NULL for another
+ * model is CF_EINVAL, and nothing is copied unless every argument is valid.
+ * Host or device memory, as cf_set_table / cf_get_table.
+ */
+int cf_set_params(cf_engine* eng, const float* U, const float* V, const float* b,
+                  const float* AU, const float* AV, const float* Ab);
+int cf_get_params(cf_engine* eng, float* U, float* V, float* b, float* AU,
+                  float* AV, float* Ab);
 
 /* ---- training ------------------------------------------------------------ */
 /*
@@ -204,6 +217,17 @@ int cf_step(cf_engine* eng, const int32_t* host_pairs,
  */
 int cf_train_steps(cf_engine* eng, int32_t B, int32_t n_steps,
                    double* loss_sum_out);
+
+/*
+ * One iteration of the reference's train loop on the device sampler:
+ * n_batches = int(len(tra_tuple) / batch_size) steps (bprmf.py:138-148),
+ * ending at an epoch boundary -- a whole epoch from a boundary (or after
+ * steps at another B), the batches the sampler's epoch has left otherwise --
+ * and mean_loss_out (may be NULL: asynchronous) = the mean of their
+ * pre-update batch losses, the reference's TraLoss (aveloss = np.mean(losses),
+ * bprmf.py:150; gbprmf.py:168, cml.py:192, amf.py:229).
+ */
+int cf_train_epoch(cf_engine* eng, int32_t B, double* mean_loss_out);
 
 /*
  * Draw the next batch of the device sampler without training (advances the
@@ -392,19 +416,30 @@ int cf_step_plr(cf_engine* eng, const int32_t* host_tuples, int32_t width, const
 /*
  * For each of n users: scores over all items (U.V^T [+ b for GBPR],
  * -|u-v|^2 for CML: bprmf.py:77-81, gbprmf.py:95-99, cml.py:111-117,
- * amf.py:144-148), drop the user's train items (exclude_train=1) and return
- * the top k item ids sorted by score descending, ties to the lower id
- * (TopKV2) -- i.e. the reference's __recommend (bprmf.py:90-103).
+ * amf.py:144-148), drop the excluded items and return the top k item ids
+ * sorted by score descending, ties to the lower id (TopKV2) -- the
+ * reference's __recommend (bprmf.py:90-103; its top_k over max|train|+topN
+ * then the python filter loop equals filtering before the selection).
+ * mask_or_NULL: NULL = exclude each user's train items (the
+ * reference's filter); else uint8 [n_items], exactly the items with
+ * mask[j] != 0 are excluded for every user (an all-zero mask: the raw top-k).
  * idx_out [n,k] int32 (-1 pads when fewer than k items remain), val_out
- * [n,k] float (may be NULL).
+ * [n,k] float (may be NULL).  k <= 128 and d <= 128 stream through the fused
+ * MFMA + top-k kernel (no score matrix in HBM); larger k materialise scores
+ * per user chunk.
  */
 int cf_score_topk(cf_engine* eng, const int32_t* host_users, int32_t n,
-                  int32_t k, int32_t exclude_train, int32_t* host_idx_out,
+                  int32_t k, const uint8_t* mask_or_NULL, int32_t* host_idx_out,
                   float* host_val_out);
+/* The same with both exclusions: exclude_train != 0 drops each user's train
+ * items, item_mask (NULL = none) the flagged items on top. */
+int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
+                     int32_t k, int32_t exclude_train, const uint8_t* item_mask,
+                     int32_t* host_idx_out, float* host_val_out);
 
 /*
  * Engine options (name, value):
- *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 28 and d <= 128, else
+ *   "topk_path"  0 = auto (fused MFMA+top-k when k <= 128 and d <= 128, else
  *                materialised scores + radix select), 1 = materialised,
  *                2 = fused (CF_EINVAL when k/d exceed its limits)
  *   "fused_variant" the fused scoring + top-k kernel: 0 = sequential (MFMAs,

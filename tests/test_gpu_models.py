@@ -212,6 +212,42 @@ def test_cfg2_bench_batch_pos_sort_matches_oracle(cfg2_graph):
     e.close()
 
 
+def _dev_used():
+    from collaborativefilteringusingtensorflow_amd import _native as N   # noqa: F401 (one HIP runtime)
+    import torch
+    torch.cuda.synchronize()
+    free, total = torch.cuda.mem_get_info(0)
+    return total - free
+
+
+def test_cfg2_deterministic_memory(cfg2_graph):
+    """Deterministic mode at the benched cfg2 instantiation (B = 2^19,
+    pos_sort, fixed point) allocates its users-past-their-cap rows compactly
+    (one int64 row per hot user of the batch, at most B / (capU + 1), found
+    by psort) instead of a dense [n_users, d] int64 array (512 MB at cfg2;
+    round-4 verdict item 8).  Device memory of a deterministic engine after
+    two steps, less that of the fast engine, measured with hipMemGetInfo:
+    was ~630 MB (GU64 512 + GV64 51 + slotP64 68), now under 250 MB."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d, B = 1_000_000, 100_000, 64, 1 << 19
+    ip, ix = cfg2_graph
+    used = {}
+    for det in (0, 1):
+        base = _dev_used()
+        e = Engine("bpr", nu, ni, d, n_neg=1, reg=0.02, seed=78)
+        e.set_option("deterministic", det)
+        e.set_interactions(ip, ix)
+        e.init_params(0.0, 0.1, truncated=True, seed=1)
+        loss = e.train_steps(B, 2)
+        assert np.isfinite(loss)
+        used[det] = _dev_used() - base
+        assert e.step_path(B)[1]["deterministic"] == bool(det)
+        e.close()
+    extra = (used[1] - used[0]) / 2 ** 20
+    print("deterministic extra device memory at cfg2: %.1f MiB (fast %.1f MiB)" % (extra, used[0] / 2 ** 20))
+    assert extra < 250, extra
+
+
 def test_driver_worker_end_to_end(fold1, tmp_path):
     """The testbprmf-structured driver: text folds -> loadSparseR ->
     matBinarize -> device Sampler -> BPRMF.train -> scores (testbprmf.py:32-52)."""

@@ -281,32 +281,88 @@ def test_pos_sort_auto_by_batch_size():
     e.close()
 
 
-@pytest.mark.parametrize("W", [1, 5])
-def test_spec_neg_equals_plain_draw(fold1, W):
+SPEC_MODELS = {"bpr": dict(reg=0.05), "amf": dict(reg=0.05, reg_adv=1.0),
+               "cml": dict(margin=1.0, reg_cov=1.0, clip_norm=1.0)}
+
+
+def _spec_engine(fold1, model, W, spec, det):
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    e = Engine(model, 943, 1682, 32, n_neg=W, seed=41, **SPEC_MODELS[model])
+    e.set_option("item_slots", 0)
+    e.set_option("pos_sort", 1)
+    e.set_option("spec_neg", spec)
+    e.set_option("deterministic", det)
+    e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    e.init_params(0.0, 0.1, truncated=(model != "cml"), seed=2)
+    return e
+
+
+@pytest.mark.parametrize("model,W", [("bpr", 1), ("bpr", 5), ("amf", 1), ("amf", 5), ("cml", 1)])
+def test_spec_neg_steps_match_oracle(fold1, model, W):
     """Speculative negative counts (cf_set_option "spec_neg", StepArgs::spec_ph):
     on ml-100k a heavy user's row holds up to ~40 % of the 1,682 items, so many
     first candidates are rejected and leave phantom occurrences (zeroed slot
-    rows, phantom-only items' counts reset).  The draw is the same stream, so
-    spec on and off train the same model up to fp32 summation order -- also
-    across a discarded drawn-ahead batch (the batch size changes mid-run)."""
-    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    rows, phantom-only items' counts reset).  Each device-drawn step with
+    phantoms is checked against one float64 oracle step on the same batch
+    from the engine's own tables, within the a-priori fp32 bound
+    (conftest.LocalStepCheck) -- BPR, AMF across its switch to the
+    adversarial phase, and CML, whose apply clips every row it updates (an
+    item touched only by phantoms must get no update and no clip)."""
+    e = _spec_engine(fold1, model, W, 1, 0)
+    kw = SPEC_MODELS[model]
+    if model == "cml":
+        chk = LocalStepCheck(model="cml", use_rank_weight=True, **kw)
+    else:
+        chk = LocalStepCheck(kw["reg"], adversarial=None if model == "bpr" else False,
+                             reg_adv=kw.get("reg_adv", 1.0))
+    e.profile(True)
+    for s in range(10):
+        if model == "amf" and s == 5:
+            e.begin_phase(1)
+            chk.T, chk.adversarial = None, True
+        st = e.sampler_state()
+        pairs, negs, _ = e.sample(2048)     # the batch the next step draws
+        e.set_sampler_state(*st)
+        chk.before(e)
+        loss = e.train_steps(2048, 1)       # drawn on the device, with phantoms
+        chk.after(e, pairs, negs, loss, "step %d" % s)
+    e.profile(False)
+    assert e.profile_read("psort")[1] == 10
+    e.close()
+
+
+@pytest.mark.parametrize("det", [0, 1], ids=["fast", "det"])
+@pytest.mark.parametrize("model,W", [("bpr", 1), ("bpr", 5), ("amf", 1), ("amf", 5)])
+def test_spec_neg_equals_plain_draw(fold1, model, W, det):
+    """The same training with spec_neg on and off -- the draw is the same
+    stream -- also across a discarded drawn-ahead batch (the batch size
+    changes mid-run) and AMF's phase switch.  Fast path: equal up to fp32
+    summation order.  Deterministic mode: bitwise equal -- it keeps the
+    speculative counts off (a phantom would move an item whose only real
+    occurrence shares its count onto the fixed-point summed path, changing
+    its last bits; the deterministic result must not depend on a
+    performance option)."""
     out = []
     for spec in (0, 1):
-        e = Engine("bpr", 943, 1682, 32, n_neg=W, reg=0.05, seed=41)
-        e.set_option("item_slots", 0)
-        e.set_option("pos_sort", 1)
-        e.set_option("spec_neg", spec)
-        e.set_interactions(fold1["train_indptr"], fold1["train_indices"])
-        e.init_params(0.0, 0.1, truncated=True, seed=2)
+        e = _spec_engine(fold1, model, W, spec, det)
         e.profile(True)
         loss = e.train_steps(2048, 12)
+        if model == "amf":
+            e.begin_phase(1)                # the adversarial phase (amf.py:216-244)
         loss += e.train_steps(1024, 6)     # the pending 2048-pair draw is discarded
         loss += e.train_steps(2048, 6)
         e.profile(False)
         assert e.profile_read("psort")[1] == 24
+        flags = e.step_path(2048)[1]
+        assert flags["pos_sort"] and flags["deterministic"] == bool(det)
         out.append((loss, {t: e.get_table(t) for t in ("user", "item", "acc_user", "acc_item")}))
         e.close()
     (l0, T0), (l1, T1) = out
+    if det:
+        assert l1 == l0
+        for t in T0:
+            assert np.array_equal(T1[t], T0[t]), t
+        return
     assert abs(l1 - l0) <= 1e-5 * abs(l0)
     for t in T0:
         assert_close(T1[t], T0[t], t)

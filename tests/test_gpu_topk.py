@@ -127,3 +127,93 @@ def test_exclusion_and_padding(fold1, path):
     assert list(idx[0][2:]) == [-1, -1, -1]
     assert 3 not in idx[1] and len(set(idx[1].tolist())) == 5
     e.close()
+
+
+def _excl_csr(fold1, n_users, item_mask, with_train):
+    """Per-user excluded items as a CSR (oracle.recommend's train argument):
+    the flagged items, plus the user's train items when with_train."""
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    flagged = np.nonzero(item_mask)[0]
+    rows = []
+    for u in range(n_users):
+        s = set(flagged.tolist())
+        if with_train:
+            s |= set(ix[ip[u]:ip[u + 1]].tolist())
+        rows.append(np.array(sorted(s), np.int32))
+    indptr = np.zeros(n_users + 1, np.int64)
+    indptr[1:] = np.cumsum([len(r) for r in rows])
+    return indptr, np.concatenate(rows)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("model,d", [("bpr", 32), ("gbpr", 64), ("cml", 50)])
+def test_topk_item_mask_matches_oracle(fold1, model, d, path):
+    """cf_score_topk's mask_or_NULL (SURVEY 8(b)) and cf_score_topk_ex's
+    item mask: flagged items are dropped for every user -- on top of the
+    train items (exclude_train) or alone (cf_score_topk with a mask) -- on the
+    fused kernels (k <= 28 and the wide lists) and the materialised path."""
+    e, U, V, b = setup(model, fold1, d, 23, bias=(model == "gbpr"), truncated=(model != "cml"))
+    e.set_option("topk_path", path)
+    rng = np.random.RandomState(5)
+    mask = (rng.rand(int(fold1["n_items"])) < 0.2).astype(np.uint8)
+    mask[:70] = 1                       # whole 64-item tiles flagged too
+    users = np.arange(0, 943, 5, dtype=np.int32)
+    S = O.predict(model, U.astype(np.float64), V.astype(np.float64),
+                  None if b is None else b.astype(np.float64), users)
+    both = _excl_csr(fold1, 943, mask, True)
+    alone = _excl_csr(fold1, 943, mask, False)
+    for k in (10, 100):
+        idx = e.score_topk(users, k, exclude_train=True, item_mask=mask)
+        check_lists(idx, S, O.recommend(S, both[0], both[1], users, k), atol=1e-5)
+        idx = e.recommend(users, k, mask=mask)
+        check_lists(idx, S, O.recommend(S, alone[0], alone[1], users, k), atol=1e-5)
+        idx = e.recommend(users, k)     # NULL: the reference's train filter
+        check_lists(idx, S, O.recommend(S, fold1["train_indptr"], fold1["train_indices"], users, k),
+                    atol=1e-5)
+    e.close()
+
+
+def test_wide_k_takes_fused_path(fold1):
+    """GBPR's topN = 100 (testgbprmf.py:23-32) streams through the fused
+    kernel's wide lists (no score matrix written: no score launch)."""
+    e, U, V, b = setup("gbpr", fold1, 64, 24, bias=True)
+    users = np.arange(943, dtype=np.int32)
+    e.profile_reset()
+    e.profile(True)
+    e.score_topk(users, 100)
+    e.profile(False)
+    assert e.profile_read("score")[1] == 0
+    assert e.profile_read("topk")[1] == 1
+    e.close()
+
+
+@pytest.mark.parametrize("k", [100, 128])
+def test_wide_k_gbpr_million_items(k):
+    """k = 100 / 128 with GBPR's +b at d = 64 over 1M items (cfg4's item
+    count, where the materialised path would write [chunk, 1M] score rows):
+    128 users against the float64 oracle under the near-tie rule."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni, d = 512, 1_000_000, 64
+    rng = np.random.RandomState(31)
+    deg = rng.randint(1, 60, nu)
+    ip = np.zeros(nu + 1, np.int64)
+    ip[1:] = np.cumsum(deg)
+    ix = np.concatenate([np.sort(rng.choice(ni, g, replace=False)) for g in deg]).astype(np.int32)
+    e = Engine("gbpr", nu, ni, d, n_neg=1, gsize=1, seed=3)
+    e.set_option("fused_variant", _FV[0])
+    e.set_interactions(ip, ix)
+    U = O.init_table(rng, (nu, d))
+    V = O.init_table(rng, (ni, d))
+    bb = O.init_table(rng, (ni,))
+    e.set_table("user", U)
+    e.set_table("item", V)
+    e.set_table("bias", bb)
+    users = np.arange(0, nu, 4, dtype=np.int32)
+    e.profile_reset()
+    e.profile(True)
+    idx = e.score_topk(users, k)
+    e.profile(False)
+    assert e.profile_read("score")[1] == 0
+    S = O.predict("gbpr", U.astype(np.float64), V.astype(np.float64), bb.astype(np.float64), users)
+    check_lists(idx, S, O.recommend(S, ip, ix, users, k), atol=2e-5)
+    e.close()
