@@ -137,7 +137,8 @@ struct cf_engine {
     bool slots_ready = false;
     // cf_set_option("pipeline") for cf_train_steps: 0 = three launches per
     // step (prep, grad, apply); 1 = apply(s) + prep(s+1) fused (two launches);
-    // 2 = grad(s) + prep(s+1) fused, apply(s) alone
+    // 2 = grad(s) + prep(s+1) fused, apply(s) alone; 3 = as 2 on the pos_sort
+    // path (grad_sort_kernel carries the draw), else as 1
     int pipeline = 1;
 
     // batch: two buffer sets, so that the sampler of step s+1 runs on the side
@@ -994,6 +995,19 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
     CF_TRY(det_ranks(e, a));
     CF_TRY(psort(e, a));
     ApplyArgs p = apply_args(e, a, B, k, loss_acc);
+    if (next && e->pipeline == 3 && a.srec != nullptr) {
+        // pipeline 3 (pos_sort steps): the draw + count of step s+1 rides in
+        // the positive-sorted gradient launch of step s, the apply runs alone;
+        // psort of s+1 follows the apply, so offPN / srec / slotN stay single
+        {
+            ProfScope ps(e, CF_K_GRAD_PREP);
+            CF_HIP(launch_grad(a, e->stream, next));
+        }
+        ProfScope ps(e, CF_K_APPLY);
+        CF_HIP(launch_apply(p, e->stream));
+        if (e->prep_side) CF_HIP(hipEventRecord(e->apply_done[k], e->stream));
+        return pending_clips(e);
+    }
     if (next && e->pipeline == 2) {
         p.n_partial = grad_blocks(a, true);   // the launch with draw blocks keeps 256-lane groups
         // the draw + count of step s+1 rides in the gradient launch of step s
@@ -2494,7 +2508,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "fused_variant") {
-        if (value < 0 || value > 1) return fail(CF_EINVAL, "fused_variant must be 0 or 1");
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "fused_variant must be 0, 1 or 2");
         e->fused_variant = (int)value;
         return CF_OK;
     }
@@ -2539,7 +2553,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "pipeline") {
-        if (value < 0 || value > 2) return fail(CF_EINVAL, "pipeline must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(CF_EINVAL, "pipeline must be 0, 1, 2 or 3");
         CF_TRY(discard_pending(e));
         e->pipeline = (int)value;
         return CF_OK;

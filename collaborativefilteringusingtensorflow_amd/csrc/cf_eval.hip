@@ -368,6 +368,13 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 #ifndef CF_FUSED_BPREFETCH
 #define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
+#ifndef CF_FUSED_SETPRIO
+// 1 (round 5 experiment): a wave raises its issue priority for its MFMA
+// stream (s_setprio 3) and drops it for the candidate phase, so the SIMD's
+// other wave -- of the other block -- fills the gaps instead of both waves'
+// MFMA streams and candidate phases lining up
+#define CF_FUSED_SETPRIO 0
+#endif
 // CAP: candidate slots per user.  kFusedCap (92, k <= 28): ~80 KB of LDS,
 // two blocks per CU.  kFusedCapWide (192, k <= 128; round 5, GBPR's topN =
 // 100): ~130 KB, one block per CU.
@@ -500,6 +507,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
 #endif
         if (more) load_tile(j0 + kFusedItems);
         // ---- 32 x 32 tile per wave on the matrix cores --------------------------
+        if (CF_FUSED_SETPRIO) __builtin_amdgcn_s_setprio(3);
         floatx16 acc;
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[q] = 0.f;
@@ -554,6 +562,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
                 if (t0 < Dh) mfma4(t0);   // block-uniform
         }
 #endif
+        if (CF_FUSED_SETPRIO) __builtin_amdgcn_s_setprio(0);
         float vnorm = 0.f;
         if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
         // ---- candidates above each user's threshold -------------------------------
@@ -985,12 +994,278 @@ __global__ __launch_bounds__(kBlock, 2) void fused_topk_pipe_kernel(FusedTopkArg
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same pass with specialised waves (fused_variant 2; round 5, verdict item
+// 5).  In fused_topk_kernel every wave computes its MFMA tile, then tests its
+// own scores; counter passes showed the matrix cores busy 54 % of the time,
+// the waves of a SIMD lining their MFMA streams and candidate phases up.
+// Here a block of 512 threads (64 users) splits the work:
+//  * waves 0-3 ("MFMA waves") only compute: tile t's 2 x 2 arrangement of
+//    32 x 32 score tiles from the V tile in LDS, the model transform (GBPR
+//    bias, CML distance), and the scores into an LDS score tile Sc[t & 1];
+//    they run at raised issue priority;
+//  * waves 4-7 ("candidate waves"), in the same step: stage V tile t+1 (its
+//    bias and its train-mask words) into the other LDS buffers, issue the
+//    loads of tile t+2, and test tile t-1's scores against their rows'
+//    thresholds -- lane (w, l) owns row 16 (w - 4) + (l & 15) and 16 of its
+//    64 columns -- appending keys to the row's list and compacting the lists
+//    of the rows this wave owns.
+// One barrier per step.  Per SIMD one wave of each kind, so the candidate
+// phase runs beside the MFMA stream instead of after it.  ~150 KB of LDS:
+// one block per CU.  Same keys, same lists, same output as fused_topk_kernel
+// (k <= 28).
+// ---------------------------------------------------------------------------
+constexpr int kWsThreads = 512;
+constexpr int kWsSP = kFusedItems + 4;   // score-tile row stride (floats): 16-B rows, staggered banks
+
+template <int MODEL>
+__global__ __launch_bounds__(kWsThreads, 1) void fused_topk_ws_kernel(FusedTopkArgs a) {
+    constexpr int CAP = kFusedCap;
+    __shared__ __attribute__((aligned(16))) float Vs[2][kFusedItems * kFusedMaxD];
+    __shared__ __attribute__((aligned(16))) float Sc[2][kFusedUsers * kWsSP];
+    __shared__ unsigned long long buf[kFusedUsers * CAP];
+    __shared__ unsigned long long thr[kFusedUsers];
+    __shared__ unsigned long long maskb[3][kFusedUsers];
+    __shared__ int cnt[kFusedUsers];
+    __shared__ float unorm[kFusedUsers];
+    __shared__ float bt[2][kFusedItems];
+
+    const int tid = threadIdx.x;
+    const int lane = lane_id();
+    const int wv = tid >> 6;
+    const bool mw = wv < 4;                  // MFMA wave
+    const int d = a.d, Dp = a.Dp, Dh = a.Dh;
+    const int u0 = blockIdx.x * kFusedUsers;
+    const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
+    const int64_t ntile = (a.n_items + kFusedItems - 1) / kFusedItems;
+    constexpr int kAH = kFusedMaxD / 2;
+
+    // ---- MFMA waves: their A operands (U rows) in registers -----------------
+    const int wr = (wv & 3) >> 1, wc = wv & 1;
+    const int h = lane >> 5, c = lane & 31;
+    float ua[kAH];
+    if (mw) {
+        const int r = wr * 32 + c;
+        const float* urow = a.U + (int64_t)a.users[u0 + (r < nu ? r : 0)] * d;
+#pragma unroll
+        for (int t = 0; t < kAH; ++t) {
+            const int kk = h * Dh + t;
+            ua[t] = (r < nu && t < Dh && kk < d) ? urow[kk] : 0.f;
+        }
+        if (MODEL == CML) {
+            float sq = 0.f;
+#pragma unroll
+            for (int t = 0; t < kAH; ++t) sq = fmaf(ua[t], ua[t], sq);
+            sq += __shfl_xor(sq, 32, 64);
+            if (wc == 0 && h == 0) unorm[r] = sq;
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_s_setprio(2);
+    }
+
+    // ---- candidate waves: tile staging, train cursors, candidate rows -------
+    const int ct = tid - 4 * kWave;          // 0..255 on candidate waves
+    int64_t cur = 0, end = 0, nxt = INT64_MAX;   // train cursor of user ct (ct < 64)
+    if (!mw && ct < kFusedUsers) {
+        thr[ct] = 0ull;
+        cnt[ct] = 0;
+        if (a.exclude_train && ct < nu) {
+            const int u = a.users[u0 + ct];
+            cur = a.indptr[u];
+            end = a.indptr[u + 1];
+            if (cur < end) nxt = a.indices[cur];
+        }
+    }
+    const bool vec = (d & 3) == 0;
+    const int q4 = Dp >> 2;
+    constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + 255) / 256;
+    float4 pre[kPre];
+    auto load_tile = [&](int64_t jt) {
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) {
+            const int t = ct + q * 256;
+            const int r = t / q4, kk = (t - r * q4) * 4;
+            const int64_t j = jt + r;
+            pre[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t < kFusedItems * q4 && j < a.n_items && kk < d)
+                pre[q] = *reinterpret_cast<const float4*>(a.V + j * d + kk);
+        }
+    };
+    // stage tile ti (items j0 .. j0 + 63) into buffer ti & 1: V rows (from
+    // the prefetch registers when vec), bias, and the train / caller mask
+    // words into maskb[ti % 3]
+    auto stage_tile = [&](int64_t ti) {
+        const int64_t j0 = ti * kFusedItems;
+        float* V_ = Vs[ti & 1];
+        if (vec) {
+#pragma unroll
+            for (int q = 0; q < kPre; ++q) {
+                const int t = ct + q * 256;
+                const int r = t / q4, kk = (t - r * q4) * 4;
+                if (t < kFusedItems * q4) *reinterpret_cast<float4*>(V_ + vs_off(r, kk)) = pre[q];
+            }
+        } else {
+            for (int t = ct; t < kFusedItems * Dp; t += 256) {
+                const int r = t / Dp, kk = t - r * Dp;
+                const int64_t j = j0 + r;
+                V_[vs_off(r, kk)] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
+            }
+        }
+        if (ct < kFusedItems) {
+            if (MODEL == GBPR) bt[ti & 1][ct] = (j0 + ct < a.n_items) ? a.b[j0 + ct] : 0.f;
+            unsigned long long m = a.item_mask != nullptr ? a.item_mask[j0 >> 6] : 0ull;
+            while (nxt < j0 + kFusedItems) {
+                m |= 1ull << (int)(nxt - j0);
+                ++cur;
+                nxt = cur < end ? (int64_t)a.indices[cur] : INT64_MAX;
+            }
+            maskb[ti % 3][ct] = m;
+        }
+    };
+    const int Rc = ((wv - 4) & 3) * 16 + (lane & 15);   // candidate row of this lane
+    const int ch = lane >> 4;                           // its 16-column chunk
+    if (!mw) {
+        if (vec) load_tile(0);
+        stage_tile(0);
+        if (vec && ntile > 1) load_tile(kFusedItems);
+    }
+    __syncthreads();
+
+    for (int64_t t = 0; t <= ntile; ++t) {
+        if (mw) {
+            if (t < ntile) {
+                const float* V_ = Vs[t & 1];
+                // one MFMA wave per SIMD: two independent accumulator chains
+                // (alternate groups of four k-steps), so a dependent MFMA
+                // never waits on the previous one's result; summed at the end
+                floatx16 acc, acc2;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    acc[q] = 0.f;
+                    acc2[q] = 0.f;
+                }
+                float vsq = 0.f;
+                const int br = wc * 32 + c;
+                auto mfma4 = [&](floatx16& A, int t0) {
+                    const float4 b4 = *reinterpret_cast<const float4*>(V_ + vs_off(br, h * Dh + t0));
+                    A = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 0], b4.x, A, 0, 0, 0);
+                    A = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 1], b4.y, A, 0, 0, 0);
+                    A = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 2], b4.z, A, 0, 0, 0);
+                    A = __builtin_amdgcn_mfma_f32_32x32x2f32(ua[t0 + 3], b4.w, A, 0, 0, 0);
+                    if (MODEL == CML) vsq += b4.x * b4.x + b4.y * b4.y + b4.z * b4.z + b4.w * b4.w;
+                };
+                if (Dh == kAH) {
+#pragma unroll
+                    for (int t0 = 0; t0 < kAH; t0 += 8) {
+                        mfma4(acc, t0);
+                        mfma4(acc2, t0 + 4);
+                    }
+                } else {
+#pragma unroll
+                    for (int t0 = 0; t0 < kAH; t0 += 8) {
+                        if (t0 < Dh) mfma4(acc, t0);          // block-uniform
+                        if (t0 + 4 < Dh) mfma4(acc2, t0 + 4);
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc[q] += acc2[q];
+                const int jl = wc * 32 + c;
+                float vnorm = 0.f;
+                if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
+                const float bj = (MODEL == GBPR) ? bt[t & 1][jl] : 0.f;
+                float* S_ = Sc[t & 1];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                    float sv = acc[q];
+                    if (MODEL == GBPR) sv += bj;
+                    if (MODEL == CML) sv = 2.f * sv - vnorm - unorm[R];   // -|u - v|^2
+                    S_[R * kWsSP + jl] = sv;
+                }
+            }
+        } else {
+#ifndef CF_WS_EXP_NOSTAGE   // attribution only (stale tiles, wrong results)
+            if (t + 1 < ntile) stage_tile(t + 1);
+            if (vec && t + 2 < ntile) load_tile((t + 2) * kFusedItems);
+#endif
+#ifdef CF_WS_EXP_NOCAND   // attribution only (no candidates)
+            if (false) {
+#else
+            if (t >= 1 && Rc < nu) {
+#endif
+                // tile t-1's scores of this lane's row, columns ch*16 .. +16
+                const int64_t jb = (t - 1) * kFusedItems + ch * 16;
+                const float* S_ = Sc[(t - 1) & 1] + Rc * kWsSP + ch * 16;
+                float sv[16];
+#pragma unroll
+                for (int e = 0; e < 16; e += 4) {
+                    const float4 v4 = *reinterpret_cast<const float4*>(S_ + e);
+                    sv[e] = v4.x; sv[e + 1] = v4.y; sv[e + 2] = v4.z; sv[e + 3] = v4.w;
+                }
+                const uint32_t mb = (uint32_t)(maskb[(t - 1) % 3][Rc] >> (ch * 16)) & 0xFFFFu;
+                const unsigned long long th = thr[Rc];
+                const float thf = key_float((uint32_t)(th >> 32));
+                // key > th implies s >= key_float(th word); NaN passes the prefilter
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int64_t J = jb + e;
+                    if (!(sv[e] < thf) && J < a.n_items && !((mb >> e) & 1u)) {
+                        const unsigned long long key = ((unsigned long long)float_key(sv[e]) << 32) |
+                                                       (0xFFFFFFFFull - (unsigned long long)J);
+                        if (key > th) {
+                            const int pos = atomicAdd(&cnt[Rc], 1);
+                            buf[Rc * CAP + pos] = key;
+                        }
+                    }
+                }
+            }
+            // this wave's 16 rows: shrink the lists that could overflow at
+            // the next step (only this wave touches them)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            const int Rl = ((wv - 4) & 3) * 16 + (lane & 15);
+            unsigned long long need = __ballot(lane < 16 && Rl < nu && cnt[Rl] > CAP - kFusedItems);
+            while (need != 0ull) {
+                const int l = __ffsll((long long)need) - 1;
+                need &= need - 1ull;
+                const int R = ((wv - 4) & 3) * 16 + l;
+                wave_compact<fused_sort_regs(CAP)>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- final sort and output (all eight waves) --------------------------------
+    for (int R = wv; R < nu; R += kWsThreads / kWave) {
+        const int n = wave_compact<fused_sort_regs(CAP)>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
+        const int64_t orow = (int64_t)(u0 + R) * a.k;
+        if (lane < a.k) {
+            int id = -1;
+            float v = __int_as_float(0x7fc00000);
+            if (lane < n) {
+                const unsigned long long e = buf[R * CAP + lane];
+                id = (int)(0xFFFFFFFFull - (e & 0xFFFFFFFFull));
+                v = key_float((uint32_t)(e >> 32));
+            }
+            a.idx_out[orow + lane] = id;
+            if (a.val_out) a.val_out[orow + lane] = v;
+        }
+    }
+}
+
 hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
     if (a.n_users <= 0) return hipSuccess;
     const dim3 grid((a.n_users + kFusedUsers - 1) / kFusedUsers), block(kBlock);
     // CML's distance transform does not fit the pipelined kernel's registers
     // at two blocks per CU (its A operands spill): it keeps the sequential one
     if (a.k > kFusedMaxWideK) return hipErrorInvalidValue;   // the host checks first
+    if (a.variant == 2 && a.k <= kFusedMaxK) {   // specialised waves
+        const dim3 wgrid(grid.x), wblock(kWsThreads);
+        switch (a.model) {
+            case GBPR: hipLaunchKernelGGL(fused_topk_ws_kernel<GBPR>, wgrid, wblock, 0, s, a); break;
+            case CML: hipLaunchKernelGGL(fused_topk_ws_kernel<CML>, wgrid, wblock, 0, s, a); break;
+            default: hipLaunchKernelGGL(fused_topk_ws_kernel<BPR>, wgrid, wblock, 0, s, a); break;
+        }
+        return hipGetLastError();
+    }
     if (a.variant == 1 && a.model != CML && a.k <= kFusedMaxK && a.item_mask == nullptr) {
         if (a.model == GBPR)
             hipLaunchKernelGGL(fused_topk_pipe_kernel<GBPR>, grid, block, 0, s, a);

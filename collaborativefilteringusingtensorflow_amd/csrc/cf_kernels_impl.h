@@ -1977,14 +1977,26 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #ifndef CF_SORT_TILES
 #define CF_SORT_TILES 1
 #endif
-template <int MODEL, int EPL, int WT, bool FX = false, bool FULL = false>
-__global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a) {
+// DRAW (round 5, pipeline 3): the launch also carries the draw + count blocks
+// of step s+1 (other buffer set), interleaved with the gradient blocks -- the
+// draw is latency-bound, the gradient launch waits on memory 59 % of its
+// wave cycles -- and the apply of step s then runs alone
+template <int MODEL, int EPL, int WT, bool FX = false, bool FULL = false, bool DRAW = false>
+__global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(StepArgs a, StepArgs nx, int ng,
+                                                                             int np) {
     // FULL: the launcher takes this instantiation only for full rows (d ==
     // 16 EPL), so every per-element `e < d` guard folds away -- each guarded
     // load / store was an exec-mask save, a branch and a restore: 1,907 ->
     // 1,285 instructions at cfg2 (round 4)
     if constexpr (FULL) __builtin_assume(a.d == kGL * EPL);
-    grad_fast_body<MODEL, EPL, WT, CF_SORT_TILES, kGroupsPerBlock, true, FX>(a, blockIdx.x);
+    int idx = blockIdx.x;
+    if constexpr (DRAW) {
+        if (minor_block(blockIdx.x, ng, np, idx)) {
+            prep_any<BPR>(nx, idx);
+            return;
+        }
+    }
+    grad_fast_body<MODEL, EPL, WT, CF_SORT_TILES, kGroupsPerBlock, true, FX>(a, idx);
 }
 
 // the same gradient blocks at one wave per workgroup (no draw blocks): a
@@ -3309,6 +3321,27 @@ static hipError_t launch_grad_w(const StepArgs& a, const StepArgs* nx, hipStream
                   : launch_grad_w_d<MODEL, WT, false>(a, n, ng, 0, s);
 }
 
+// grad_sort_kernel by row width; FX: the deterministic fixed-point form;
+// DRAW: with the next step's draw blocks (pipeline 3)
+template <int MODEL, int WT, bool FX, bool DRAW>
+static hipError_t launch_sort_e(const StepArgs& a, const StepArgs& n, int ng, int np, dim3 grid, bool full,
+                                hipStream_t s) {
+    const dim3 block(kBlock);
+    switch (epl_for(a.d)) {
+        case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT, FX, false, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT, FX, false, DRAW>), grid, block, 0, s, a, n, ng, np); break;
+        case 4:
+            if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, FX, true, DRAW>), grid, block, 0, s, a, n, ng, np);
+            else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, FX, false, DRAW>), grid, block, 0, s, a, n, ng, np);
+            break;
+        default:
+            if (full && !FX) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, FX, true, DRAW>), grid, block, 0, s, a, n, ng, np);
+            else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, FX, false, DRAW>), grid, block, 0, s, a, n, ng, np);
+            break;
+    }
+    return hipGetLastError();
+}
+
 template <int MODEL, int WT, int P>
 static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     if (CF_GRAD_WAVE_BLOCKS && prep_blocks(nx) == 0) {
@@ -3328,35 +3361,15 @@ static hipError_t launch_grad_fast(const StepArgs& a, const StepArgs* nx, hipStr
     const StepArgs n = nx ? *nx : a;
     const dim3 grid(ng + np), block(kBlock);
     if constexpr (MODEL != GBPR && P == 1) {
-        if (a.srec != nullptr) {   // pos_sort (the engine never pairs it with a draw)
-            if (np > 0) return hipErrorInvalidValue;
-            const dim3 sgrid((a.B + CF_SORT_TILES * kPsortPPB - 1) / (CF_SORT_TILES * kPsortPPB));
+        if (a.srec != nullptr) {   // pos_sort; with nx (pipeline 3) the next draw rides along
+            const int sg = (a.B + CF_SORT_TILES * kPsortPPB - 1) / (CF_SORT_TILES * kPsortPPB);
+            const dim3 sgrid(sg + np);
             const bool full = CF_ASSUME_FULL_ROWS && a.d == kGL * epl_for(a.d);
-            if (a.det_fx) {   // deterministic: fixed-point partials and loss
-                switch (epl_for(a.d)) {
-                    case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT, true>), sgrid, block, 0, s, a); break;
-                    case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT, true>), sgrid, block, 0, s, a); break;
-                    case 4:
-                        if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true, true>), sgrid, block, 0, s, a);
-                        else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, true>), sgrid, block, 0, s, a);
-                        break;
-                    default: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, true>), sgrid, block, 0, s, a); break;
-                }
-                return hipGetLastError();
-            }
-            switch (epl_for(a.d)) {
-                case 1: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 1, WT>), sgrid, block, 0, s, a); break;
-                case 2: hipLaunchKernelGGL((grad_sort_kernel<MODEL, 2, WT>), sgrid, block, 0, s, a); break;
-                case 4:
-                    if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT, false, true>), sgrid, block, 0, s, a);
-                    else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 4, WT>), sgrid, block, 0, s, a);
-                    break;
-                default:
-                    if (full) hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT, false, true>), sgrid, block, 0, s, a);
-                    else hipLaunchKernelGGL((grad_sort_kernel<MODEL, 8, WT>), sgrid, block, 0, s, a);
-                    break;
-            }
-            return hipGetLastError();
+            if (np > 0)
+                return a.det_fx ? launch_sort_e<MODEL, WT, true, true>(a, n, sg, np, sgrid, full, s)
+                                : launch_sort_e<MODEL, WT, false, true>(a, n, sg, np, sgrid, full, s);
+            return a.det_fx ? launch_sort_e<MODEL, WT, true, false>(a, n, sg, 0, sgrid, full, s)
+                            : launch_sort_e<MODEL, WT, false, false>(a, n, sg, 0, sgrid, full, s);
         }
     }
     if (a.srec != nullptr) return hipErrorInvalidValue;

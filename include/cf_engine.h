@@ -471,8 +471,10 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                1 = the duplicate apply of step s with the draw + count of
  *                step s+1, two launches per step (default); 2 = the draw +
  *                count of step s+1 inside step s's gradient launch, the apply
- *                alone (measured 4.7 us/step slower at cfg2); 0 = one step at
- *                a time, three launches.
+ *                alone (measured 4.7 us/step slower at cfg2); 3 = as 2 for
+ *                positive-sorted steps (the draw rides in grad_sort_kernel,
+ *                psort of s+1 follows the apply), else as 1; 0 = one step
+ *                at a time, three launches.
  *   "neg_check"  how the device draw rejects a negative candidate in Pos(u):
  *                1 = probe an open-addressed set of the (u, i) pairs (16 B
  *                per interaction, built when selected; ~1 sector per
