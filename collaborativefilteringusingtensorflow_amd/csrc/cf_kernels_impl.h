@@ -64,9 +64,21 @@ namespace cfk {
 #ifndef CF_VEC_ROWS
 #define CF_VEC_ROWS 0
 #endif
+// Round 5: rows of d > 64 (EPL >= 8: cfg3 / cfg5's d = 128) take the vector
+// layout by default -- the apply's 512-B slot and table rows move as two
+// float4 per lane: cfg5 apply + draw 96.2 -> 88.8 us, 0.2013 -> 0.1940
+// ms/step; the d = 64 kernels keep the scalar one (cfg2 gradient 164.5 ->
+// 194.5 us with it, cfg4 apply 77.4 -> 86.0; profiles/r05/ab/r05h_*).  The
+// mapping is per kernel (memory rows are always natural order), so kernels
+// with different layouts exchange rows freely
+#ifndef CF_VEC_ROWS_WIDE
+#define CF_VEC_ROWS_WIDE 1
+#endif
+template <int EPL>
+__host__ __device__ constexpr bool vec_rows() { return CF_VEC_ROWS || (CF_VEC_ROWS_WIDE && EPL >= 8); }
 template <int EPL>
 struct Lay {
-    static constexpr int VW = CF_VEC_ROWS ? (EPL >= 4 ? 4 : EPL) : 1;
+    static constexpr int VW = vec_rows<EPL>() ? (EPL >= 4 ? 4 : EPL) : 1;
     static constexpr int NQ = EPL / VW;  // stripes per row
 };
 
@@ -81,7 +93,7 @@ template <int EPL>
 __device__ __forceinline__ void row_ld(const float* __restrict__ row, int d, int gl, float fill,
                                        float (&x)[EPL]) {
     constexpr int VW = Lay<EPL>::VW;
-    if (CF_VEC_ROWS && d == kGL * EPL) {
+    if (vec_rows<EPL>() && d == kGL * EPL) {
 #pragma unroll
         for (int q = 0; q < Lay<EPL>::NQ; ++q) {
             const float* p = row + q * (kGL * VW) + gl * VW;
@@ -107,7 +119,7 @@ __device__ __forceinline__ void row_ld(const float* __restrict__ row, int d, int
 template <int EPL>
 __device__ __forceinline__ void row_st(float* __restrict__ row, int d, int gl, const float (&x)[EPL]) {
     constexpr int VW = Lay<EPL>::VW;
-    if (CF_VEC_ROWS && d == kGL * EPL) {
+    if (vec_rows<EPL>() && d == kGL * EPL) {
 #pragma unroll
         for (int q = 0; q < Lay<EPL>::NQ; ++q) {
             float* p = row + q * (kGL * VW) + gl * VW;
@@ -195,7 +207,7 @@ template <int EPL>
 __device__ __forceinline__ void gatomic(float* __restrict__ G, int64_t r, int d, int gl,
                                         const float (&g)[EPL]) {
     float* row = G + r * (int64_t)d;
-    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+    const bool full = vec_rows<EPL>() && d == kGL * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         const int e = elem_of<EPL>(s, gl, full);
@@ -228,7 +240,7 @@ __device__ __forceinline__ float from_fx(long long v, int* __restrict__ bad) {
 
 template <int EPL>
 __device__ __forceinline__ void fx_ld_add(const long long* __restrict__ row, int d, int gl, long long (&t)[EPL]) {
-    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+    const bool full = vec_rows<EPL>() && d == kGL * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         const int e = elem_of<EPL>(s, gl, full);
@@ -238,7 +250,7 @@ __device__ __forceinline__ void fx_ld_add(const long long* __restrict__ row, int
 
 template <int EPL>
 __device__ __forceinline__ void fx_st(long long* __restrict__ row, int d, int gl, const long long (&t)[EPL]) {
-    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+    const bool full = vec_rows<EPL>() && d == kGL * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         const int e = elem_of<EPL>(s, gl, full);
@@ -249,7 +261,7 @@ __device__ __forceinline__ void fx_st(long long* __restrict__ row, int d, int gl
 template <int EPL>
 __device__ __forceinline__ void fx_atomic(unsigned long long* __restrict__ row, int d, int gl, const float (&g)[EPL],
                                           int* __restrict__ bad) {
-    const bool full = CF_VEC_ROWS && d == kGL * EPL;
+    const bool full = vec_rows<EPL>() && d == kGL * EPL;
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         const int e = elem_of<EPL>(s, gl, full);
@@ -1804,7 +1816,7 @@ __device__ __forceinline__ void psort_head(const StepArgs& a, const PairRows<MOD
             fx_st<EPL>(a.slotP64 + ((int64_t)block + r.i) * a.d, a.d, gl, t);
         } else {   // past capP: int64 atomics, exact in any order
             unsigned long long* row = a.GV64 + (int64_t)r.i * a.d;
-            const bool full = CF_VEC_ROWS && a.d == kGL * EPL;
+            const bool full = vec_rows<EPL>() && a.d == kGL * EPL;
 #pragma unroll
             for (int s = 0; s < EPL; ++s) {
                 const int e = elem_of<EPL>(s, gl, full);
@@ -1977,6 +1989,9 @@ __global__ __launch_bounds__(kBlock) CF_GRAD_ATTR void grad_fast_kernel(StepArgs
 #ifndef CF_SORT_TILES
 #define CF_SORT_TILES 1
 #endif
+#ifndef CF_SORT_XCD
+#define CF_SORT_XCD 1   // round 5: XCD-contiguous sorted tiles (cfg2 gradient 170 -> 163 us, profiles/r05/ab)
+#endif
 // DRAW (round 5, pipeline 3): the launch also carries the draw + count blocks
 // of step s+1 (other buffer set), interleaved with the gradient blocks -- the
 // draw is latency-bound, the gradient launch waits on memory 59 % of its
@@ -1996,6 +2011,16 @@ __global__ __launch_bounds__(kBlock, CF_SORT_MIN_WAVES) void grad_sort_kernel(St
             return;
         }
     }
+#if CF_SORT_XCD
+    // XCD-contiguous tiles: workgroups are dealt round-robin over the 8 XCDs
+    // (b and b + 8 share one), so XCD x takes the contiguous run of sorted
+    // tiles [x * full + min(x, rem), ...) -- a Zipf-head positive item whose
+    // run spans many tiles is then gathered through one XCD's L2
+    if constexpr (!DRAW) {
+        const int nb = (int)gridDim.x, full = nb >> 3, rem = nb & 7, x = idx & 7;
+        idx = x * full + (x < rem ? x : rem) + (idx >> 3);
+    }
+#endif
     grad_fast_body<MODEL, EPL, WT, CF_SORT_TILES, kGroupsPerBlock, true, FX>(a, idx);
 }
 
@@ -2733,7 +2758,7 @@ __device__ __forceinline__ void apply_item_ps(const ApplyArgs& a, int64_t r, int
         // hundreds: one at a time they were a serial chain of load latencies)
         const long long* P64 = a.slotP64 + ((int64_t)(o / kPsortPPB) + r) * a.d;
         constexpr int NF2 = NF / 2 > 0 ? NF / 2 : 1;
-        const bool full = CF_VEC_ROWS && a.d == kGL * EPL;
+        const bool full = vec_rows<EPL>() && a.d == kGL * EPL;
         for (int t0 = 0; t0 < npp; t0 += NF2) {
             long long h[NF2][EPL];
 #pragma unroll
