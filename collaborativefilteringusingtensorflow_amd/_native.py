@@ -18,7 +18,7 @@ MODEL_IDS = {"bpr": CF_BPR, "bprmf": CF_BPR, "gbpr": CF_GBPR, "gbprmf": CF_GBPR,
 TABLES = {"user": 0, "item": 1, "bias": 2, "acc_user": 3, "acc_item": 4, "acc_bias": 5}
 KERNELS = {"sample": 0, "step": 1, "apply": 2, "apply_dense": 3, "clip": 4, "score": 5,
            "topk": 6, "slot": 7, "apply_prep": 8, "grad_prep": 9, "apply_slot": 10,
-           "item_reduce": 11, "psort": 12, "step_remote": 13}
+           "item_reduce": 11, "psort": 12, "step_remote": 13, "epoch_order": 14}
 STATUS = {0: "CF_OK", -1: "CF_EINVAL", -2: "CF_EHIP", -3: "CF_ESTATE", -4: "CF_ENOMEM", -5: "CF_EAGAIN",
           -6: "CF_ENUMERIC"}
 CF_EAGAIN = -5

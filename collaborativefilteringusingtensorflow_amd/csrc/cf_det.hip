@@ -257,7 +257,45 @@ __global__ __launch_bounds__(kScanThreads) void psort_tile_scan_kernel(const int
 // n_items + 1 entries: the last one holds the totals
 int psort_tiles(int64_t n_items) { return (int)((n_items + 1 + kScanTile - 1) / kScanTile); }
 
+// sorted batches (cf_set_option "sorted_batches"): every pair q gets the
+// batch its epoch slot falls in, perm_inverse(q) / B (pairs past the last
+// whole batch: bin n_batches), with q as the value -- q ascending, so the
+// stable radix sort by batch leaves each batch's pairs in pair (CSR) order
+__global__ void epoch_keys_kernel(PermKey p, PermInv v, int64_t nnz, int64_t n_used, int B, int32_t nb,
+                                  int32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = t0; q < nnz; q += nt) {
+        const uint64_t slot = perm_inverse((uint64_t)q, p, v);
+        keys[q] = slot < (uint64_t)n_used ? (int32_t)(slot / (uint64_t)B) : nb;
+        vals[q] = (int32_t)q;
+    }
+}
+
 }  // namespace
+
+size_t epoch_order_scratch(int64_t nnz, int32_t n_batches) {
+    size_t bytes = 0;
+    hipcub::DoubleBuffer<int32_t> k(nullptr, nullptr), v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k, v, (int)nnz, 0, key_bits((int64_t)n_batches + 1));
+    return bytes;
+}
+
+hipError_t launch_epoch_order(const PermKey& p, int64_t nnz, int B, int32_t* keys, int32_t* vals, void* tmp,
+                              size_t tmp_bytes, const int32_t** order_out, hipStream_t s) {
+    if (nnz <= 0 || nnz > INT32_MAX || B <= 0) return hipErrorInvalidValue;
+    const int32_t nb = (int32_t)(nnz / B);
+    PermInv v{};
+    for (int r = 0; r < 3; ++r) v.mi[r] = perm_mul_inverse(p.m[r]);
+    hipLaunchKernelGGL(epoch_keys_kernel, dim3(grid_of(nnz)), dim3(256), 0, s, p, v, nnz, (int64_t)nb * B, B, nb,
+                       keys, vals);
+    hipcub::DoubleBuffer<int32_t> dk(keys, keys + nnz), dv(vals, vals + nnz);
+    size_t bytes = tmp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, dk, dv, (int)nnz, 0, key_bits((int64_t)nb + 1), s);
+    if (e != hipSuccess) return e;
+    *order_out = dv.Current();
+    return hipGetLastError();
+}
 
 size_t psort_scratch(int64_t n_items) { return (size_t)psort_tiles(n_items) * sizeof(int2); }
 

@@ -40,6 +40,36 @@ __host__ __device__ __forceinline__ uint64_t permute(uint64_t x, const PermKey& 
     return x;
 }
 
+// Inverse of perm_rounds; mi[r] = the inverse of p.m[r] modulo 2^64
+// (perm_mul_inverse), which is also its inverse modulo 2^bits.  A round's
+// xorshift x ^= x >> s is undone by y ^ (y >> s) ^ (y >> 2s) ^ ..
+struct PermInv {
+    uint64_t mi[3];
+};
+__host__ __device__ __forceinline__ uint64_t perm_mul_inverse(uint64_t m) {
+    uint64_t inv = m;   // m * m == 1 mod 8 for odd m: 3 correct bits, doubled per step
+#pragma unroll
+    for (int i = 0; i < 6; ++i) inv *= 2ull - m * inv;
+    return inv;
+}
+__host__ __device__ __forceinline__ uint64_t perm_rounds_inv(uint64_t x, const PermKey& p, const PermInv& v) {
+#pragma unroll
+    for (int r = 2; r >= 0; --r) {
+        uint64_t z = x;
+        for (uint32_t t = p.shift; t < 64; t += p.shift) z ^= x >> t;
+        x = (z * v.mi[r]) & p.mask;
+        x = (x ^ p.k[r]) & p.mask;
+    }
+    return x;
+}
+// the slot a pair index comes from: permute(perm_inverse(q)) == q
+__host__ __device__ __forceinline__ uint64_t perm_inverse(uint64_t q, const PermKey& p, const PermInv& v) {
+    do {
+        q = perm_rounds_inv(q, p, v);
+    } while (q >= p.n);
+    return q;
+}
+
 // butterfly sum: every lane ends with the bitwise-identical total
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -13,6 +13,8 @@
 
 #include "../../include/cf_engine.h"
 #include "cf_kernels.h"
+#include "cf_device.h"
+#include <thread>
 
 using namespace cfk;
 
@@ -93,6 +95,27 @@ struct cf_engine {
     int64_t* indptr_t = nullptr;
     int32_t* indices_t = nullptr;
     std::vector<int64_t> h_indptr;
+    // sorted batches (round 5, cf_set_option "sorted_batches", default 1):
+    // each batch's pairs in pair (CSR) order, so the draw reads its records
+    // in ascending order, its users are nearly consecutive (their count
+    // atomics share lines) and its row scans stay local.  The batch SET is
+    // the epoch bijection's, unchanged.  Two slots: the current epoch's order
+    // and the next one's, computed ahead on eo_stream (StepArgs::order)
+    int sorted_batches = 2;   // 0 off, 1 on, 2 auto (kSortedAutoBatches batches per epoch and up)
+    struct EpochOrder {
+        int32_t* keys = nullptr;     // [2 nnz]
+        int32_t* vals = nullptr;     // [2 nnz]
+        void* tmp = nullptr;
+        size_t tmp_bytes = 0;
+        int64_t cap = 0;
+        int64_t epoch = -1;
+        int B = 0;
+        const int32_t* order = nullptr;
+        hipEvent_t ready = nullptr;
+        bool async = false;          // computed on eo_stream: the engine stream waits on `ready`
+    } eo[2];
+    hipStream_t eo_stream = nullptr;
+    hipEvent_t eo_mark = nullptr;
 
     // tables
     float *U = nullptr, *V = nullptr, *b = nullptr;
@@ -674,6 +697,87 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     return a;
 }
 
+// sorted batches, auto: the epoch's order costs ~2 ms per 50M pairs (the
+// inverse-bijection keys + a radix sort), once per epoch; it pays where an
+// epoch has many batches -- cfg2 at B = 65,536 (762 per epoch): -3.2 us of a
+// 74 us step for ~0.8 us of order; at B = 2^19 (95 per epoch) the charge eats
+// the gain
+constexpr int64_t kSortedAutoBatches = 256;
+bool sorted_batches_on(const cf_engine* e, int B) {
+    if (e->sorted_batches == 0 || e->nnz > INT32_MAX || B < 1) return false;
+    return e->sorted_batches == 1 || e->nnz / B >= kSortedAutoBatches;
+}
+
+// the order of (epoch, B) in slot k, enqueued on stream st
+int compute_epoch_order(cf_engine* e, int k, int64_t epoch, int B, hipStream_t st) {
+    cf_engine::EpochOrder& o = e->eo[k];
+    const int64_t nnz = e->nnz;
+    if (o.cap < nnz) {
+        CF_HIP(hipDeviceSynchronize());
+        dfree(o.keys);
+        dfree(o.vals);
+        if (o.tmp) (void)hipFree(o.tmp);
+        o.tmp = nullptr;
+        o.cap = 0;
+        CF_TRY(dalloc(&o.keys, (size_t)(2 * nnz)));
+        CF_TRY(dalloc(&o.vals, (size_t)(2 * nnz)));
+        o.cap = nnz;
+        o.tmp_bytes = 0;
+    }
+    const size_t need = epoch_order_scratch(nnz, (int32_t)(nnz / B));
+    if (need > o.tmp_bytes) {
+        CF_HIP(hipDeviceSynchronize());
+        if (o.tmp) (void)hipFree(o.tmp);
+        o.tmp = nullptr;
+        hipError_t he = hipMalloc(&o.tmp, need);
+        if (he != hipSuccess) return fail(CF_ENOMEM, std::string("hipMalloc (epoch order scratch): ") + hipGetErrorString(he));
+        o.tmp_bytes = need;
+    }
+    const PermKey pk = make_perm_key((uint64_t)nnz, e->cfg.seed, (uint64_t)epoch);
+    {
+        ProfScope ps(e, CF_K_EPOCH_ORDER, st);
+        CF_HIP(launch_epoch_order(pk, nnz, B, o.keys, o.vals, o.tmp, o.tmp_bytes, &o.order, st));
+    }
+    o.epoch = epoch;
+    o.B = B;
+    o.async = st != e->stream;
+    if (o.async) CF_HIP(hipEventRecord(o.ready, st));
+    return CF_OK;
+}
+
+// the order of the sampler's epoch at batch size B, ready on the engine
+// stream; the next epoch's is started on eo_stream
+int epoch_order(cf_engine* e, int B, const int32_t** out) {
+    if (!e->eo_stream) {
+        int lo = 0, hi = 0;
+        CF_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CF_HIP(hipStreamCreateWithPriority(&e->eo_stream, hipStreamNonBlocking, lo));   // lowest priority
+        CF_HIP(hipEventCreateWithFlags(&e->eo_mark, hipEventDisableTiming));
+        for (auto& o : e->eo) CF_HIP(hipEventCreateWithFlags(&o.ready, hipEventDisableTiming));
+    }
+    const int64_t ep = e->epoch;
+    int k = (e->eo[0].epoch == ep && e->eo[0].B == B) ? 0 : (e->eo[1].epoch == ep && e->eo[1].B == B) ? 1 : -1;
+    if (k < 0) {
+        // not computed ahead (first epoch, a jump, another B): in order on the engine stream
+        k = (e->eo[0].epoch == ep + 1 && e->eo[0].B == B) ? 1 : 0;
+        if (e->eo[k].async) CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
+        CF_TRY(compute_epoch_order(e, k, ep, B, e->stream));
+    } else if (e->eo[k].async) {
+        CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
+        e->eo[k].async = false;
+    }
+    *out = e->eo[k].order;
+    cf_engine::EpochOrder& nx = e->eo[k ^ 1];
+    if (!(nx.epoch == ep + 1 && nx.B == B) && e->nnz / B >= 2) {
+        // the next epoch's order, behind everything the engine stream holds
+        // so far (the kernels that still read this slot's previous epoch)
+        CF_HIP(hipEventRecord(e->eo_mark, e->stream));
+        CF_HIP(hipStreamWaitEvent(e->eo_stream, e->eo_mark, 0));
+        CF_TRY(compute_epoch_order(e, k ^ 1, ep + 1, B, e->eo_stream));
+    }
+    return CF_OK;
+}
+
 // position the device sampler for the next batch of B pairs
 int sampler_args(cf_engine* e, int B, StepArgs* a) {
     if (!e->pairs) return fail(CF_ESTATE, "no interactions: call cf_set_interactions first");
@@ -698,6 +802,11 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
     a->perm = make_perm_key((uint64_t)e->nnz, e->cfg.seed, (uint64_t)e->epoch);
     a->rng_key = mix64_host(e->cfg.seed ^ mix64_host((uint64_t)e->epoch * 0x9E3779B97F4A7C15ull +
                                                      0x2545F4914F6CDD1Dull));
+    if (sorted_batches_on(e, B)) {
+        const int32_t* ord = nullptr;
+        CF_TRY(epoch_order(e, B, &ord));
+        a->order = ord;   // batch b's pairs at [bB, bB + B), CSR order
+    }
     e->batch += 1;
     return CF_OK;
 }
@@ -1069,8 +1178,9 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
     CF_TRY(begin_step(e, B, nullptr, nullptr, nullptr, k, e->stream, &a));
     // the positive-sorted gradient launch of step s fetches step s+1's pair
     // records (StepArgs::pf_out); the draw of s+1 then reads them coalesced
+    // (sorted batches read their records coalesced already: no prefetch)
     const bool pf = e->pair_prefetch && a.srec != nullptr && e->pipeline == 1 && !e->prep_side &&
-                    a.pos_set == nullptr;
+                    a.pos_set == nullptr && a.order == nullptr;
     if (pf && e->pf_cap < B) {
         CF_HIP(hipStreamSynchronize(e->stream));
         for (int q = 0; q < 2; ++q) {
@@ -1429,6 +1539,14 @@ int cf_destroy(cf_engine* e) {
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pf_recs[0]); dfree(e->pf_recs[1]); dfree(e->slotP64); dfree(e->GU64); dfree(e->GV64); dfree(e->fx_bad);
     dfree(e->hotU); dfree(e->hot_n);
+    for (auto& o : e->eo) {
+        dfree(o.keys);
+        dfree(o.vals);
+        if (o.tmp) (void)hipFree(o.tmp);
+        if (o.ready) (void)hipEventDestroy(o.ready);
+    }
+    if (e->eo_mark) (void)hipEventDestroy(e->eo_mark);
+    if (e->eo_stream) (void)hipStreamDestroy(e->eo_stream);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
     dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
@@ -1478,6 +1596,7 @@ int cf_synchronize(cf_engine* e) {
     CF_TRY(check_engine(e));
     CF_HIP(hipStreamSynchronize(e->side));
     CF_HIP(hipStreamSynchronize(e->stream));
+    if (e->eo_stream) CF_HIP(hipStreamSynchronize(e->eo_stream));
     return CF_OK;
 }
 
@@ -2523,6 +2642,12 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         e->item_pieces = (int)value;
         return CF_OK;
     }
+    if (n == "sorted_batches") {   // each batch's pairs in CSR order (StepArgs::order)
+        if (value < 0 || value > 2) return fail(CF_EINVAL, "sorted_batches must be 0, 1 or 2");
+        CF_TRY(discard_pending(e));
+        e->sorted_batches = (int)value;
+        return CF_OK;
+    }
     if (n == "spec_neg") {   // speculative negative counts in the pos_sort draw (StepArgs::spec_ph)
         if (value < 0 || value > 1) return fail(CF_EINVAL, "spec_neg must be 0 or 1");
         CF_TRY(discard_pending(e));   // a drawn-ahead batch was counted under the old setting
@@ -2690,6 +2815,7 @@ int cf_profile_read(cf_engine* e, int32_t kid, double* total_ms, int64_t* launch
     double t = 0.0;
     for (auto& pr : e->ev[kid]) {
         float ms = 0.f;
+        CF_HIP(hipEventSynchronize(pr.second));   // events of the epoch-order stream too
         CF_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
         t += ms;
     }

@@ -79,6 +79,12 @@ struct StepArgs {
     PermKey pf_perm;
     int pf_B;
     const int4* __restrict__ pre_pairs;     // the draw's record of pair p at [p] (null: pairs[permute(..)])
+    // sorted batches (round 5, cf_set_option "sorted_batches"): the epoch's
+    // pair indices batch by batch, each batch in pair (CSR) order -- the draw
+    // takes pairs[order[slot]] instead of pairs[permute(slot)]: the same
+    // batch set, its records read in ascending order, its users nearly
+    // consecutive; null = off
+    const int32_t* __restrict__ order;
     // deterministic mode on the positive-sorted path (round 3):
     // every sum of gradient rows is taken in 64-bit fixed point (kFxOne
     // units), which is associative, so the result does not depend on the
@@ -452,6 +458,11 @@ struct PsortArgs {
     int d;
 };
 hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s);
+// sorted batches: keys / vals hold 2 * nnz int32 each; *order_out = the
+// epoch's pair indices sorted by (batch, pair) -- batch b at [b B, (b+1) B)
+size_t epoch_order_scratch(int64_t nnz, int32_t n_batches);
+hipError_t launch_epoch_order(const PermKey& p, int64_t nnz, int B, int32_t* keys, int32_t* vals, void* tmp,
+                              size_t tmp_bytes, const int32_t** order_out, hipStream_t s);
 // a discarded draw's phantoms (StepArgs::spec_ph): uncount them, re-zero spec_n
 hipError_t launch_uncount_spec(const int2* ph, int* n, int32_t* cnt, hipStream_t s);
 // grad_sort_kernel carries the pair-record prefetch (StepArgs::pf_out)

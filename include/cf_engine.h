@@ -99,7 +99,9 @@ enum cf_kernel_id {
                             the pairs into positive-item order               */
     CF_K_STEP_REMOTE = 13,/* split exchange step: the gradient of the pairs with
                             a remote group member (cf_xchg_grad_part 2)      */
-    CF_K_COUNT = 14
+    CF_K_EPOCH_ORDER = 14,/* sorted batches: an epoch's pair order (inverse
+                            bijection keys + radix sort by batch), once per epoch */
+    CF_K_COUNT = 15
 };
 
 /*
@@ -475,6 +477,13 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                positive-sorted steps (the draw rides in grad_sort_kernel,
  *                psort of s+1 follows the apply), else as 1; 0 = one step
  *                at a time, three launches.
+ *   "sorted_batches" the device sampler's batches read in pair (CSR) order:
+ *                the same batch sets as the epoch bijection, each batch's
+ *                pairs ascending, so the draw's records, user count atomics
+ *                and row scans stay local.  The order of each epoch (inverse
+ *                bijection keys + a radix sort by batch) is computed ahead
+ *                on a low-priority stream.  0 off, 1 on, 2 auto (default:
+ *                on when an epoch has >= 256 batches)
  *   "neg_check"  how the device draw rejects a negative candidate in Pos(u):
  *                1 = probe an open-addressed set of the (u, i) pairs (16 B
  *                per interaction, built when selected; ~1 sector per

@@ -69,6 +69,33 @@ def test_epoch_is_a_permutation(fold1):
     s.close()
 
 
+@pytest.mark.parametrize("B", [100, 997, 4096])
+def test_sorted_batches_same_sets_in_csr_order(fold1, B):
+    """Sorted batches (cf_set_option "sorted_batches", the default since
+    round 5): batch b of an epoch is the SAME set of pairs as the epoch
+    bijection's slots [bB, bB + B) -- the draw only reads them in pair (CSR)
+    order, i.e. ascending (u, i) -- over two epochs, with the order of the
+    next epoch computed ahead on the engine's low-priority stream."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    per_epoch = len(ix) // B
+    out = []
+    for sb in (0, 1):
+        e = Engine("bpr", nu, ni, 8, n_neg=1, seed=33)
+        e.set_option("sorted_batches", sb)
+        e.set_interactions(ip, ix)
+        out.append([e.sample(B)[0] for _ in range(2 * per_epoch)])
+        e.close()
+    for b, (plain, srt) in enumerate(zip(*out)):
+        kp = np.sort(plain[:, 0].astype(np.int64) * ni + plain[:, 1])
+        ks = srt[:, 0].astype(np.int64) * ni + srt[:, 1]
+        assert np.array_equal(np.sort(ks), kp), b          # the same batch set
+        assert (np.diff(ks) > 0).all(), b                   # in CSR order
+        ok = [(ix[ip[u]:ip[u + 1]] == i).any() for u, i in srt[:: max(1, B // 50)]]
+        assert all(ok), b
+
+
 def test_negatives_uniform_over_complement(fold1):
     from collaborativefilteringusingtensorflow_amd.engine import Engine
     nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
