@@ -372,6 +372,9 @@ def main():
                     help="cf_set_option pair_prefetch (the gradient launch fetches the next draw's pair records)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="cf_set_option deterministic (sort-based ranks, no float atomics)")
+    ap.add_argument("--amf-mode", default="reference", choices=["reference", "apr"],
+                    help="AMF configs: cf_config.amf_mode (apr: Δ from the normalised embedding-loss "
+                         "gradient, DESIGN 3.13; not the reference's computation)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the process group, check it, print a line; no GPU work (tests)")
     args = ap.parse_args()
@@ -467,6 +470,11 @@ def main():
     for k in ("margin", "reg_cov", "clip_norm", "reg_adv", "rho"):
         if k in cfg:
             kw[k] = cfg[k]
+    if args.amf_mode != "reference":
+        if cfg["model"] != "amf":
+            raise SystemExit("--amf-mode applies to AMF configs (cfg5)")
+        kw["amf_mode"] = args.amf_mode
+        cfg["desc"] += " [amf_mode %s, epsilon 0.5]" % args.amf_mode
     eng = Engine(cfg["model"], u1 - u0, ni, d, n_neg=W, gsize=cfg["G"], device=local_rank,
                  dense_item_apply=sharded, seed=1000 + rank, **kw)
     eng.set_option("grad_path", args.grad_path)

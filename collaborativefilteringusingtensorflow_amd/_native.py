@@ -13,6 +13,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "cf_engine.h")
 
 CF_BPR, CF_GBPR, CF_CML, CF_AMF, CF_PLR = 0, 1, 2, 3, 4
 CF_PLR_PRIGP, CF_PLR_CPLR = 0, 1
+CF_AMF_REFERENCE, CF_AMF_APR = 0, 1
+AMF_MODES = {"reference": CF_AMF_REFERENCE, "apr": CF_AMF_APR}
 MODEL_IDS = {"bpr": CF_BPR, "bprmf": CF_BPR, "gbpr": CF_GBPR, "gbprmf": CF_GBPR,
              "cml": CF_CML, "amf": CF_AMF, "plr": CF_PLR, "prigp": CF_PLR, "cplr": CF_PLR}
 TABLES = {"user": 0, "item": 1, "bias": 2, "acc_user": 3, "acc_item": 4, "acc_bias": 5}
@@ -53,7 +55,7 @@ class CfConfig(ctypes.Structure):
         ("alpha", ctypes.c_float),
         ("beta", ctypes.c_float),
         ("gamma", ctypes.c_float),
-        ("reserved1", ctypes.c_int32),
+        ("amf_mode", ctypes.c_int32),
     ]
 
 

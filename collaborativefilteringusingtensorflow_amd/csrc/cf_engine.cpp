@@ -122,6 +122,10 @@ struct cf_engine {
     float *AU = nullptr, *AV = nullptr, *Ab = nullptr;
     float *GU = nullptr, *GV = nullptr, *Gb = nullptr;
     float *GV_own = nullptr, *Gb_own = nullptr;
+    // amf_mode CF_AMF_APR: the batch's summed embedding-loss gradient of every
+    // duplicated row (apr_embed_kernel), zero between steps; Δ = epsilon *
+    // l2_normalize(row).  Rows seen once take Δ from their own pair.
+    float *GadvU = nullptr, *GadvV = nullptr;
     int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
     int32_t* cntV_[2] = {nullptr, nullptr};
     // store-and-sum of duplicated rows: row r of a table owns the fixed slot
@@ -345,7 +349,7 @@ constexpr int kPsortAutoB = 1 << 18;
 // allocated only then)
 bool psort_possible(const cf_engine* e) {
     const cf_config& c = e->cfg;
-    if (!e->pos_sort || e->item_recs) return false;
+    if (!e->pos_sort || e->item_recs || c.amf_mode == CF_AMF_APR) return false;   // apr: generic kernel
     if (c.dense_item_apply && e->item_reduce != 1) return false;   // the multi-rank item reduce: slot rows only
     if (c.model != CF_BPR && c.model != CF_AMF && c.model != CF_CML) return false;
     if ((int64_t)c.n_users * e->capU > INT32_MAX) return false;   // user slot rows ride in int32 records
@@ -606,6 +610,12 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     a.margin = c.margin;
     a.reg_cov = c.reg_cov;
     a.reg_adv = c.reg_adv;
+    if (a.adversarial && c.amf_mode == CF_AMF_APR) {
+        a.apr = 1;
+        a.epsilon = c.epsilon;
+        a.GadvU = e->GadvU;
+        a.GadvV = e->GadvV;
+    }
     a.use_rank_weight = c.use_rank_weight;
     a.n_items_f = (float)c.n_items;
     a.n_items = c.n_items;
@@ -1446,6 +1456,13 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     if (!(c.lr > 0.f) || !(c.acc_init > 0.f)) return fail(CF_EINVAL, "lr and acc_init must be > 0");
     if (c.model == CF_CML && !(c.clip_norm > 0.f)) return fail(CF_EINVAL, "clip_norm must be > 0");
     if (c.model == CF_CML && c.n_neg > 16) return fail(CF_EINVAL, "CML supports n_neg <= 16");
+    if (c.amf_mode != CF_AMF_REFERENCE && c.amf_mode != CF_AMF_APR)
+        return fail(CF_EINVAL, "amf_mode must be CF_AMF_REFERENCE (0) or CF_AMF_APR (1)");
+    if (c.amf_mode == CF_AMF_APR && c.model != CF_AMF) return fail(CF_EINVAL, "amf_mode apr is an AMF mode");
+    if (c.amf_mode == CF_AMF_APR && c.dense_item_apply)
+        return fail(CF_EINVAL, "amf_mode apr is single-rank: the item Δ needs the cross-rank gradient sum "
+                               "(not built; DESIGN 3.13)");
+    if (c.amf_mode == CF_AMF_APR && !(c.epsilon >= 0.f)) return fail(CF_EINVAL, "epsilon must be >= 0");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
         return fail(CF_EHIP, "no HIP device visible (the engine has no CPU fallback)");
@@ -1458,7 +1475,7 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     // rows -> records) cfg3 0.256 -> 0.230, cfg5 0.258 -> 0.227 (d 128, W 5);
     // cfg2 0.497 -> 0.519, cfg4 0.241 -> 0.254 (d 64: the apply's record ->
     // stash gather chain costs more than the smaller slot stores save)
-    e->item_recs = c.n_factors >= 128 ? 1 : 0;
+    e->item_recs = (c.n_factors >= 128 && c.amf_mode != CF_AMF_APR) ? 1 : 0;   // apr: gradient rows only
     int r = CF_OK;
     auto bail = [&](int code) {
         cf_destroy(e);
@@ -1492,6 +1509,12 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     e->GV = e->GV_own;
     e->Gb = e->Gb_own;
     e->shard_u1 = c.n_users;
+    if (c.amf_mode == CF_AMF_APR) {
+        if ((r = dalloc(&e->GadvU, ud)) || (r = dalloc(&e->GadvV, id))) return bail(r);
+        if (hipMemsetAsync(e->GadvU, 0, ud * 4, e->stream) != hipSuccess ||
+            hipMemsetAsync(e->GadvV, 0, id * 4, e->stream) != hipSuccess)
+            return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
+    }
     if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
     if (hipHostMalloc((void**)&e->h_fx_bad, kFxSlots * sizeof(int), hipHostMallocDefault) != hipSuccess)
@@ -1549,7 +1572,7 @@ int cf_destroy(cf_engine* e) {
     if (e->eo_stream) (void)hipStreamDestroy(e->eo_stream);
     dfree(e->pos_set);
     dfree(e->U); dfree(e->V); dfree(e->b); dfree(e->AU); dfree(e->AV); dfree(e->Ab);
-    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own);
+    dfree(e->GU); dfree(e->GV_own); dfree(e->Gb_own); dfree(e->GadvU); dfree(e->GadvV);
     for (int k = 0; k < 2; ++k) {
         dfree(e->cntU_[k]); dfree(e->cntV_[k]); dfree(e->occU_[k]); dfree(e->occV_[k]);
         dfree(e->rankU_[k]); dfree(e->rankV_[k]);
@@ -2731,6 +2754,8 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     }
     if (n == "item_slots") {   // 0: gradient rows, 1: (pair, alpha, beta) records + user-row stash
         if (value < 0 || value > 1) return fail(CF_EINVAL, "item_slots must be 0 or 1");
+        if (value == 1 && e->cfg.amf_mode == CF_AMF_APR)
+            return fail(CF_EINVAL, "item_slots 1 (records alpha * X + beta * V) cannot carry apr's perturbed rows");
         if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
@@ -2748,6 +2773,8 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
     }
     if (n == "deterministic") {
         if (value < 0 || value > 1) return fail(CF_EINVAL, "deterministic must be 0 or 1");
+        if (value == 1 && e->cfg.amf_mode == CF_AMF_APR)
+            return fail(CF_EINVAL, "deterministic mode does not cover amf_mode apr (its Δ sums are float atomics)");
         if (e->lg_stage != 0 || e->x_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));

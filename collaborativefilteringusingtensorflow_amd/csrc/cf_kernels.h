@@ -44,6 +44,13 @@ struct StepArgs {
     int adversarial; // AMF phase flag
     int grad_path;   // 0 auto, 1 generic grad_kernel, 2 phased grad_fast_kernel when eligible
     float reg, rho, margin, reg_cov, reg_adv;
+    // AMF apr (cf_config.amf_mode 1, adversarial phase): Δ_X = epsilon *
+    // l2_normalize(dL_embed/dX); GadvU / GadvV hold the batch's summed
+    // embedding-loss gradient of duplicated rows (zero between steps)
+    int apr;
+    float epsilon;
+    float* GadvU;
+    float* GadvV;
     int use_rank_weight;
     float n_items_f;
     int64_t n_items;

@@ -1093,6 +1093,103 @@ struct NegRows {
     }
 };
 
+// AMF apr (cf_config.amf_mode 1): Δ of row r = epsilon * l2_normalize(the
+// batch's summed embedding-loss gradient of r), tf.nn.l2_normalize(x, 1) =
+// x * rsqrt(max(sum x^2, 1e-12)) (amf.py:131-137).  A row seen once takes the
+// gradient of its own pair, g1, from registers; a duplicated row the sum that
+// apr_embed_kernel left in Gadv.  dx may alias g1.
+template <int EPL>
+__device__ __forceinline__ void apr_delta(const float* __restrict__ Gadv, int64_t r, int count, int d, int gl,
+                                          float eps, const float (&g1)[EPL], float (&dx)[EPL]) {
+    if (count >= 2) {
+        gload<EPL>(Gadv, r, d, gl, dx);
+    } else {
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) dx[s] = g1[s];
+    }
+    const float sc = eps * rsqrtf(fmaxf(gdot<EPL>(dx, dx), 1e-12f));
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) dx[s] *= sc;
+}
+
+// One AMF apr pair of the adversarial phase (amf.py:92-116, 139-162 with the
+// assigns of __update_adv__ run): loss softplus(-x) + reg_adv *
+// softplus(-clip(x', -80, 1e8)) + reg * L2, x = <u,i> - <u,j>,
+// x' = <u+Δu, i+Δi> - <u, j+Δj> (the user is not perturbed in uj,
+// amf.py:110); Δ is a constant (stop_gradient, amf.py:131-132).  Pass 1 forms
+// the pair's own embedding-loss gradients of u and i (the rows seen once take
+// Δ from them), pass 2 the loss and the gradient rows.
+template <int EPL, int WT>
+__device__ __forceinline__ void apr_pair(const StepArgs& a, int p, int gl, int u, int i, int cu, int ci,
+                                         int64_t su, int64_t si, const float (&uu)[EPL], const float (&vi)[EPL],
+                                         NegRows<EPL, WT>& J, float& loss_g, float& sq) {
+    const int d = a.d;
+    const int W = WT > 0 ? WT : a.W;
+    const float ui = gdot<EPL>(uu, vi);
+    float g1[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) g1[s] = 0.f;
+    float sc = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const int sl = J.get(a, p, w, gl);
+        const float c = -rcp_1p(expf(ui - gdot<EPL>(uu, J.v[sl])));
+        sc += c;
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) g1[s] = fmaf(c, vi[s] - J.v[sl][s], g1[s]);
+    }
+    float up[EPL], ip[EPL];
+    apr_delta<EPL>(a.GadvU, u, cu, d, gl, a.epsilon, g1, up);
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) g1[s] = sc * uu[s];
+    apr_delta<EPL>(a.GadvV, i, ci, d, gl, a.epsilon, g1, ip);
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        up[s] += uu[s];
+        ip[s] += vi[s];
+    }
+    const float uiP = gdot<EPL>(up, ip);
+    float gu[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) gu[s] = a.reg * uu[s];
+    float scP = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const int sl = J.get(a, p, w, gl);
+        const float x = ui - gdot<EPL>(uu, J.v[sl]);
+        const float c = -rcp_1p(expf(x));
+        loss_g += softplus(-x);
+        float jp[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) jp[s] = -c * uu[s];
+        apr_delta<EPL>(a.GadvV, J.j[sl], J.c[sl], d, gl, a.epsilon, jp, jp);
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) jp[s] += J.v[sl][s];
+        const float xP = uiP - gdot<EPL>(uu, jp);
+        loss_g += a.reg_adv * softplus(-fmaxf(fminf(xP, 1e8f), -80.f));
+        const float cP = (xP >= -80.f && xP <= 1e8f) ? a.reg_adv * -rcp_1p(expf(xP)) : 0.f;
+        scP += cP;
+        float gj[EPL];
+#pragma unroll
+        for (int s = 0; s < EPL; ++s) {
+            gu[s] = fmaf(c, vi[s] - J.v[sl][s], gu[s]);
+            gu[s] = fmaf(cP, ip[s] - jp[s], gu[s]);
+            gj[s] = -(c + cP) * uu[s] + a.reg * J.v[sl][s];
+            sq = fmaf(J.v[sl][s], J.v[sl][s], sq);
+        }
+        ifinish<EPL>(a, J.j[sl], J.c[sl], J.sl[sl], p, -(c + cP), a.reg, 0, gl, J.v[sl], gj);
+    }
+    float gi[EPL];
+#pragma unroll
+    for (int s = 0; s < EPL; ++s) {
+        gi[s] = fmaf(sc, uu[s], fmaf(scP, up[s], a.reg * vi[s]));
+        sq = fmaf(uu[s], uu[s], sq);
+        sq = fmaf(vi[s], vi[s], sq);
+    }
+    gfinish<EPL>(a.U, a.AU, a.GU, a.slotU, a.cntU, u, cu, su, d, gl, uu, gu, a);
+    ifinish<EPL>(a, i, ci, si, p, sc, a.reg, 0, gl, vi, gi);
+}
+
 template <int MODEL, int EPL, int WT>
 __device__ __forceinline__ void grad_body(const StepArgs& a, int block) {
     __shared__ double s_loss[kGroupsPerBlock];
@@ -3297,6 +3394,7 @@ static int epl_for(int d) {
 // it applies -- BPR / AMF / CML at d = 128, GBPR (G = 1) at d = 64; one pair
 // per 16-lane group, 16 per block
 static bool lds_path(const StepArgs& a) {
+    if (a.apr) return false;   // AMF apr: the generic kernel (apr_pair)
     const bool want = a.grad_path == 3 || (a.grad_path == 0 && CF_GRAD_LDS);
     if (!want || a.W != 5 || a.srec != nullptr) return false;
     if (a.model == BPR || a.model == AMF || a.model == CML) return a.d == 128;
@@ -3307,6 +3405,7 @@ static bool lds_path(const StepArgs& a) {
 // which grad kernel a step takes (see launch_grad_m): 1 = W=1 fast, 5 = W=5
 // fast (or the LDS-staged kernel), 0 = generic
 static int fast_w(const StepArgs& a) {
+    if (a.apr) return 0;   // AMF apr: the generic kernel (apr_pair)
     if (lds_path(a)) return 5;
     // CML at W = 5 keeps five distance rows and the clip live per pair: the
     // generic kernel measured faster than the phased one there (cfg3: 160 vs

@@ -50,7 +50,7 @@ class Engine(object):
                  reg=0.02, rho=0.5, margin=1.5, reg_cov=1.0, clip_norm=1.0, reg_adv=1.0,
                  epsilon=0.5, acc_init=0.1, use_rank_weight=True, device=0,
                  dense_item_apply=False, seed=20261015, plr_kind=None, alpha=1.0, beta=1.0,
-                 gamma=1.0):
+                 gamma=1.0, amf_mode="reference"):
         L = N.lib()
         if isinstance(model, str):
             name = model.lower()
@@ -82,6 +82,9 @@ class Engine(object):
         cfg.dense_item_apply = 1 if dense_item_apply else 0
         cfg.plr_kind = int(plr_kind or 0)
         cfg.alpha, cfg.beta, cfg.gamma = float(alpha), float(beta), float(gamma)
+        # AMF: "reference" (Δ = 0, what amf.py computes) or "apr" (Δ from the
+        # normalised embedding-loss gradient, include/cf_engine.h amf_mode)
+        cfg.amf_mode = N.AMF_MODES[amf_mode] if isinstance(amf_mode, str) else int(amf_mode)
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         self.cfg = cfg
         self.model = int(model)

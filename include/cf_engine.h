@@ -139,8 +139,19 @@ typedef struct cf_config {
     int32_t plr_kind;         /* enum cf_plr_kind (CF_PLR)                      */
     uint64_t seed;            /* device sampler / init seed                     */
     float alpha, beta, gamma; /* PLR term weights (prigp.py:128, cplr_u.py:136) */
-    int32_t reserved1;
+    int32_t amf_mode;         /* AMF adversarial phase: CF_AMF_REFERENCE (0, the
+                                 default) is what amf.py:139-162 computes -- Δ = 0,
+                                 because the tf.assign ops of __update_adv__
+                                 (amf.py:117-137) never run; CF_AMF_APR (1) runs
+                                 them as written for adv_method "grad":
+                                 Δ_X = epsilon * l2_normalize(dL_embed/dX, axis 1)
+                                 from the step's pre-update rows (stop-gradient),
+                                 perturbing U_u, V_i, V_j in ui and V_j in uj
+                                 (amf.py:96-116).  Single-rank, not deterministic,
+                                 slot rows (item_slots 0); see DESIGN 3.13      */
 } cf_config;
+
+enum cf_amf_mode { CF_AMF_REFERENCE = 0, CF_AMF_APR = 1 };
 
 /* ---- lifecycle ---------------------------------------------------------- */
 const char* cf_version(void);

@@ -158,6 +158,56 @@ def amf_step(U, V, AU, AV, pairs, negs, reg, adversarial, reg_adv=1.0, lr=0.1):
     return float(loss)
 
 
+def _l2_normalize_rows(G):
+    """``tf.nn.l2_normalize(x, 1)`` = x * rsqrt(max(sum(x^2, 1), 1e-12))."""
+    n2 = np.sum(G * G, axis=1, keepdims=True)
+    return G / np.sqrt(np.maximum(n2, G.dtype.type(1e-12)))
+
+
+def amf_apr_step(U, V, AU, AV, pairs, negs, reg, epsilon, reg_adv=1.0, lr=0.1):
+    """One adversarial-phase AMF step with ``__update_adv__``'s assigns RUN
+    (engine ``amf_mode`` "apr"; not what the reference computes).
+
+    amf.py:128-137 (adv_method "grad"): G_X = dL_embed/dX densified
+    (stop_gradient on IndexedSlices = the per-row sum), Δ_X = epsilon *
+    l2_normalize(G_X, 1) from the pre-update rows.
+    amf.py:96-116: x' = <U_u + Δ_u, V_i + Δ_i> - <U_u, V_j + Δ_j> (the user
+    is NOT perturbed in uj, amf.py:110); loss = softplus(-x) + reg*L2 +
+    reg_adv * softplus(-clip(x', -80, 1e8)); Δ is a constant.  The gradient
+    of the clip passes where -80 <= x' <= 1e8.  Returns the pre-update loss.
+    """
+    pairs = np.asarray(pairs)
+    negs = np.asarray(negs).reshape(pairs.shape[0], -1)
+    dt = U.dtype.type
+    u_idx, i_idx = pairs[:, 0], pairs[:, 1]
+    Uu, Vi, Vj = U[u_idx], V[i_idx], V[negs]
+    x = np.sum(Uu * Vi, axis=1)[:, None] - np.sum(Uu[:, None, :] * Vj, axis=-1)
+    c = _c_bpr(x).astype(U.dtype)                                   # [B,W]
+    # dense embedding-loss gradients (amf.py:130-132)
+    GU = np.zeros_like(U)
+    GV = np.zeros_like(V)
+    np.add.at(GU, u_idx, (c[:, :, None] * (Vi[:, None, :] - Vj)).sum(axis=1))
+    np.add.at(GV, i_idx, c.sum(axis=1)[:, None] * Uu)
+    np.add.at(GV, negs.reshape(-1), (-c[:, :, None] * Uu[:, None, :]).reshape(-1, U.shape[1]))
+    DU = dt(epsilon) * _l2_normalize_rows(GU)
+    DV = dt(epsilon) * _l2_normalize_rows(GV)
+    uP, iP, jP = Uu + DU[u_idx], Vi + DV[i_idx], Vj + DV[negs]
+    xP = np.sum(uP * iP, axis=1)[:, None] - np.sum(Uu[:, None, :] * jP, axis=-1)
+    inside = ((xP >= dt(-80.0)) & (xP <= dt(1e8))).astype(U.dtype)
+    cP = dt(reg_adv) * _c_bpr(xP).astype(U.dtype) * inside
+    reg_ = dt(reg)
+    gU = ((c[:, :, None] * (Vi[:, None, :] - Vj)).sum(axis=1)
+          + (cP[:, :, None] * (iP[:, None, :] - jP)).sum(axis=1) + reg_ * Uu)
+    gVi = c.sum(axis=1)[:, None] * Uu + cP.sum(axis=1)[:, None] * uP + reg_ * Vi
+    gVj = -(c + cP)[:, :, None] * Uu[:, None, :] + reg_ * Vj
+    loss = (np.sum(_softplus(-x)) + reg_ * (_l2(Uu) + _l2(Vi) + _l2(Vj))
+            + dt(reg_adv) * np.sum(_softplus(-np.clip(xP, -80.0, 1e8))))
+    dedup_adagrad(U, AU, u_idx, gU, lr)
+    dedup_adagrad(V, AV, np.concatenate([i_idx, negs.reshape(-1)]),
+                  np.concatenate([gVi, gVj.reshape(-1, V.shape[1])]), lr)
+    return float(loss)
+
+
 def amf_switch_epoch(max_iter):
     """First adversarial epoch (0-based): amf.py:243-244 flips the flag at the
     end of the first epoch ``iter`` with ``iter > 3*max_iter/5``."""

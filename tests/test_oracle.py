@@ -130,6 +130,72 @@ def test_oracle_matches_literal_autograd(streams, model, stream, hp):
             assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
 
 
+def literal_apr_loss(U, V, pairs, negs, hp):
+    """amf.py:73-137 with __update_adv__'s assigns run (adv_method "grad"):
+    Δ = epsilon * tf.nn.l2_normalize(stop_gradient(d embed_loss / dX), 1)."""
+    p = torch.as_tensor(pairs, dtype=torch.long)
+    n = torch.as_tensor(negs, dtype=torch.long)
+    sp = torch.nn.functional.softplus
+    u, i, js = U[p[:, 0]], V[p[:, 1]], V[n]
+    x = (u * i).sum(1)[:, None] - (u[:, None, :] * js).sum(-1)
+    embed = sp(-x).sum()                                                  # amf.py:81-88
+    gU, gV = torch.autograd.grad(embed, [U, V], retain_graph=True)        # amf.py:130
+    norm = lambda g: g / torch.sqrt(torch.clamp((g * g).sum(1, keepdim=True), min=1e-12))
+    dU, dV = (hp["epsilon"] * norm(gU)).detach(), (hp["epsilon"] * norm(gV)).detach()
+    l2 = lambda t: 0.5 * (t * t).sum()
+    reg = hp["reg"] * (l2(u) + l2(i) + l2(js))                            # amf.py:66-71
+    uiP = ((u + dU[p[:, 0]]) * (i + dV[p[:, 1]])).sum(1)                  # amf.py:96-111
+    ujP = (u[:, None, :] * (js + dV[n])).sum(-1)
+    adv = sp(-torch.clamp(uiP[:, None] - ujP, -80.0, 1e8)).sum()
+    return embed + reg + hp["reg_adv"] * adv
+
+
+@pytest.mark.parametrize("eps", [0.5, 1.0])
+def test_oracle_amf_apr_matches_literal_autograd(streams, eps):
+    """The apr restatement (oracle.amf_apr_step) against torch autograd over
+    the literal graph with Δ from autograd's own dense gradients."""
+    st = get_stream(streams, "rank_b100_w5")
+    hp = dict(reg=0.05, reg_adv=1.0, epsilon=eps)
+    tabs = init(11)
+    ora = {k: v.copy() for k, v in tabs.items()}
+    oacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    tacc = {k: np.full_like(v, 0.1) for k, v in tabs.items()}
+    for s in range(5):
+        pairs, negs = st["pairs"][s], st["negs"][s]
+        T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in tabs.items()}
+        loss = literal_apr_loss(T["U"], T["V"], pairs, negs, hp)
+        loss.backward()
+        for k, t in T.items():
+            g = t.grad.numpy()
+            tacc[k] = tacc[k] + g * g
+            tabs[k] = t.detach().numpy() - 0.1 * g / np.sqrt(tacc[k])
+        lo = O.amf_apr_step(ora["U"], ora["V"], oacc["U"], oacc["V"], pairs, negs, hp["reg"], eps,
+                            reg_adv=hp["reg_adv"])
+        lt = float(loss.detach())
+        assert abs(lo - lt) <= TOL * abs(lt), (s, lo, lt)
+        for k in tabs:
+            assert rel(ora[k], tabs[k]) <= 1e-10, (s, k, rel(ora[k], tabs[k]))
+            assert rel(oacc[k], tacc[k]) <= 1e-10, (s, k)
+
+
+def test_amf_apr_differs_from_reference_mode(streams):
+    """A real Δ changes the step: apr at epsilon > 0 is not the reference
+    mode's Δ = 0 step, and at epsilon = 0 it is."""
+    st = get_stream(streams, "rank_b100_w5")
+    pairs, negs = st["pairs"][0], st["negs"][0]
+    base = init(12)
+    out = {}
+    for name, fn in [("ref", lambda t, a: O.amf_step(t["U"], t["V"], a["U"], a["V"], pairs, negs, 0.05, True)),
+                     ("apr0", lambda t, a: O.amf_apr_step(t["U"], t["V"], a["U"], a["V"], pairs, negs, 0.05, 0.0)),
+                     ("apr", lambda t, a: O.amf_apr_step(t["U"], t["V"], a["U"], a["V"], pairs, negs, 0.05, 0.5))]:
+        t = {k: v.copy() for k, v in base.items()}
+        a = {k: np.full_like(v, 0.1) for k, v in base.items()}
+        out[name] = (fn(t, a), t)
+    assert abs(out["ref"][0] - out["apr0"][0]) <= 1e-12 * abs(out["ref"][0])
+    assert rel(out["apr0"][1]["U"], out["ref"][1]["U"]) <= 1e-12
+    assert rel(out["apr"][1]["U"], out["ref"][1]["U"]) > 1e-4
+
+
 def test_cml_min_ties_share_gradient():
     """reduce_min's gradient is split equally between tied negatives."""
     tabs = init(5, nu=3, ni=6, d=4)
