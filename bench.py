@@ -560,7 +560,10 @@ def main():
     # the split GBPR exchange step runs its gradient in two launches (pairs
     # with local group members, then the rest): both are timed, summed per step
     split_grad = sharded and cfg["model"] == "gbpr"
-    eng.set_option("profile_mask", (1 << KERNELS[dom]) | ((1 << KERNELS["step_remote"]) if split_grad else 0))
+    # + the sorted batches' epoch orders computed inside the region (always
+    # timed, so their count is exact; see the charge below)
+    eng.set_option("profile_mask", (1 << KERNELS[dom]) | ((1 << KERNELS["step_remote"]) if split_grad else 0)
+                   | (1 << KERNELS["epoch_order"]))
     # every PROFILE_EVERY-th launch is timed: an event pair on every launch
     # costs the loop ~6 us/step (cfg2), sampled launches ~1/PROFILE_EVERY of it
     eng.set_option("profile_every", PROFILE_EVERY)
@@ -577,6 +580,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     step_ms, step_n = eng.profile_read(dom)
+    _, eo_in = eng.profile_read("epoch_order")
     if split_grad:
         rem_ms, _ = eng.profile_read("step_remote")
         step_ms += rem_ms
@@ -602,34 +606,51 @@ def main():
 
     # sorted batches: each epoch's pair order -- inverse
     # bijection keys + a radix sort by batch -- is computed once per epoch,
-    # ahead, on a low-priority stream, so a 20-step timed region may not meet
-    # one.  Its standalone time is measured here (a forced, uncached epoch)
-    # and charged to every timed step as ms / batches per epoch: `value` and
-    # `ms_per_step` below include it (conservative: run beside the steps it
-    # costs them less than standalone)
-    eo_ms = 0.0
+    # ahead, on a low-priority stream.  The orders computed inside the timed
+    # region (eo_in) are already on its clock; a region shorter than an epoch
+    # may meet fewer than its share (steps / batches per epoch).  The missing
+    # share is charged at the order's standalone time (measured here on a
+    # forced, uncached epoch): `value` and `ms_per_step` below include it
+    def epoch_order_ms(b):
+        """Standalone time of one epoch's order at batch b (0 when sorted
+        batches are off there): a forced, uncached epoch, then the sampler
+        state is restored."""
+        ms_ = 0.0
+        try:
+            st0 = eng.sampler_state()
+            eng.profile_reset()
+            eng.set_option("profile_mask", 1 << KERNELS["epoch_order"])
+            eng.profile(True)
+            eng.set_sampler_state(st0[0] + 7, 0)
+            run(1, b)
+            sync()
+            eng.profile(False)
+            ms, n = eng.profile_read("epoch_order")
+            ms_ = ms / n if n else 0.0
+            eng.set_sampler_state(*st0)
+            eng.take_loss()
+        except Exception as ex:  # diagnostics only
+            log("epoch order timing failed: %r" % (ex,))
+        if world > 1:
+            t = torch.tensor([ms_], dtype=torch.float64, device="cuda:%d" % local_rank)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms_ = float(t.item())
+        return ms_
+
+    def order_charge(ms_, n_in, steps, per_ep):
+        """Orders (of the region's steps / per_ep share) not on the clock."""
+        miss = max(0.0, steps / per_ep - n_in) if ms_ > 0 else 0.0
+        if world > 1:
+            t = torch.tensor([miss], dtype=torch.float64, device="cuda:%d" % local_rank)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            miss = float(t.item())
+        return miss
+
     per_epoch = max(1, len(indices) // B)
-    try:
-        st0 = eng.sampler_state()
-        eng.profile_reset()
-        eng.set_option("profile_mask", 1 << KERNELS["epoch_order"])
-        eng.profile(True)
-        eng.set_sampler_state(st0[0] + 7, 0)
-        run(1)
-        sync()
-        eng.profile(False)
-        ms, n = eng.profile_read("epoch_order")
-        eo_ms = ms / n if n else 0.0
-        eng.set_sampler_state(*st0)
-        eng.take_loss()
-    except Exception as ex:  # diagnostics only
-        log("epoch order timing failed: %r" % (ex,))
-    if world > 1:
-        t = torch.tensor([eo_ms], dtype=torch.float64, device="cuda:%d" % local_rank)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        eo_ms = float(t.item())
+    eo_ms = epoch_order_ms(B)
     elapsed_timed = elapsed
-    elapsed = elapsed + 1e-3 * eo_ms * args.steps / per_epoch
+    eo_missing = order_charge(eo_ms, eo_in, args.steps, per_epoch)
+    elapsed = elapsed + 1e-3 * eo_ms * eo_missing
 
     # SURVEY 8(d)'s batch (65,536 pairs per GPU) on the same engine and graph
     secondary = None
@@ -637,17 +658,28 @@ def main():
     if B2 and B2 != B and B2 <= len(indices):
         run(max(2, args.warmup // 2), B2)
         sync()
+        eng.profile_reset()
+        eng.set_option("profile_mask", 1 << KERNELS["epoch_order"])
+        eng.profile(True)
         t0 = time.perf_counter()
         run(args.steps, B2)
         sync()
-        el2 = time.perf_counter() - t0 + 1e-3 * eo_ms * args.steps / max(1, len(indices) // B2)
+        el2 = time.perf_counter() - t0
+        eng.profile(False)
+        _, eo2_in = eng.profile_read("epoch_order")
+        per_epoch2 = max(1, len(indices) // B2)
+        eo2_ms = epoch_order_ms(B2)
+        eo2_missing = order_charge(eo2_ms, eo2_in, args.steps, per_epoch2)
+        el2 += 1e-3 * eo2_ms * eo2_missing
         if world > 1:
             t = torch.tensor([el2], dtype=torch.float64, device="cuda:%d" % local_rank)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el2 = float(t.item())
         secondary = {"batch_pairs_per_gpu": B2, "steps": args.steps,
                      "value": B2 * W * args.steps * world / el2, "unit": "triplets/s",
-                     "ms_per_step": 1e3 * el2 / args.steps}
+                     "ms_per_step": 1e3 * el2 / args.steps,
+                     "epoch_order": {"ms_per_epoch": eo2_ms, "batches_per_epoch": per_epoch2,
+                                     "in_timed_region": eo2_in, "charged": eo2_missing}}
     # one drawn batch's row multiplicities -> the apply + draw launch's and a
     # dedup-aware step's algorithmic bytes (batch_stats)
     st = None
@@ -726,9 +758,12 @@ def main():
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
         "ms_per_step_timed": 1e3 * elapsed_timed / args.steps,
         "epoch_order": {"ms_per_epoch": eo_ms, "batches_per_epoch": per_epoch,
-                        "charged_ms_per_step": eo_ms / per_epoch,
+                        "in_timed_region": eo_in, "charged": eo_missing,
+                        "charged_ms_per_step": eo_ms * eo_missing / args.steps,
                         "def": "sorted batches: one epoch's pair order (inverse-bijection keys + radix sort "
-                               "by batch), standalone time charged to every step (DESIGN 3.1)"},
+                               "by batch) is computed per epoch; those inside the timed region are on its "
+                               "clock, the rest of the region's share (steps / batches_per_epoch) is charged "
+                               "at the standalone time (DESIGN 3.1)"},
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f32", "data": "synthetic (seeded, generated in-repo), random-init tables",
         "config": {"workload": cfg["desc"], "model": cfg["model"], "n_users": nu_all,

@@ -319,7 +319,9 @@ struct ProfScope {
     }
     ProfScope(cf_engine* e_, int k_, hipStream_t s_ = nullptr) : e(e_), k(k_), s(s_) {
         if (!e->prof || !((e->prof_mask >> k) & 1)) return;
-        if (e->prof_seen[k]++ % e->prof_every != 0) return;   // sampled launches only
+        // sampled launches only; the once-per-epoch order is always timed, so
+        // a count of its launches is exact (bench.py charges the rest)
+        if (e->prof_seen[k]++ % e->prof_every != 0 && k != CF_K_EPOCH_ORDER) return;
         if (!s) s = e->stream;
         a = get(e);
         z = get(e);
@@ -707,12 +709,13 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
     return a;
 }
 
-// sorted batches, auto: the epoch's order costs ~2 ms per 50M pairs (the
-// inverse-bijection keys + a radix sort), once per epoch; it pays where an
-// epoch has many batches -- cfg2 at B = 65,536 (762 per epoch): -3.2 us of a
-// 74 us step for ~0.8 us of order; at B = 2^19 (95 per epoch) the charge eats
-// the gain
-constexpr int64_t kSortedAutoBatches = 256;
+// sorted batches, auto: the epoch's order costs ~1 ms per 50M pairs (the
+// inverse-bijection keys + a radix sort), once per epoch, on a low-priority
+// stream beside the steps; same-box A/Bs with the orders on the clock
+// (profiles/r05/ab/r05s_*): cfg2 B = 2^19 (95 batches per epoch) 0.3588 ->
+// 0.3544 ms/step, B = 65,536 0.0740 -> 0.0724.  Below 16
+// batches per epoch the order is mostly the synchronous first one
+constexpr int64_t kSortedAutoBatches = 16;
 bool sorted_batches_on(const cf_engine* e, int B) {
     if (e->sorted_batches == 0 || e->nnz > INT32_MAX || B < 1) return false;
     return e->sorted_batches == 1 || e->nnz / B >= kSortedAutoBatches;

@@ -494,7 +494,7 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                and row scans stay local.  The order of each epoch (inverse
  *                bijection keys + a radix sort by batch) is computed ahead
  *                on a low-priority stream.  0 off, 1 on, 2 auto (default:
- *                on when an epoch has >= 256 batches)
+ *                on when an epoch has >= 16 batches)
  *   "neg_check"  how the device draw rejects a negative candidate in Pos(u):
  *                1 = probe an open-addressed set of the (u, i) pairs (16 B
  *                per interaction, built when selected; ~1 sector per
