@@ -2653,7 +2653,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "fused_variant") {
-        if (value < 0 || value > 2) return fail(CF_EINVAL, "fused_variant must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(CF_EINVAL, "fused_variant must be 0, 1, 2 or 3");
         e->fused_variant = (int)value;
         return CF_OK;
     }

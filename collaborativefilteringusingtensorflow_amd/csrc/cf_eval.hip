@@ -380,16 +380,19 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 // 100): ~130 KB, one block per CU.
 // MASK: the caller's item mask is read (a.item_mask may still be null); the
 // narrow kernel without it keeps its register budget (GBPR: 16 B less spill)
-template <int MODEL, int CAP = kFusedCap, bool MASK = false>
-__global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_kernel(FusedTopkArgs a) {
+template <int MODEL, int CAP = kFusedCap, bool MASK = false, int NU = kFusedUsers>
+__global__ __launch_bounds__(4 * NU, (CAP <= kFusedCap && NU == kFusedUsers) ? 2 : 1)
+void fused_topk_kernel(FusedTopkArgs a) {
     // The user operands live in registers.
     constexpr int SR = fused_sort_regs(CAP);
+    constexpr int NT = 4 * NU;        // threads: one wave per 32 x 32 score tile
+    constexpr int NW = NT / kWave;
     __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFusedMaxD];
-    __shared__ unsigned long long buf[kFusedUsers * CAP];
-    __shared__ unsigned long long thr[kFusedUsers];
-    __shared__ unsigned long long mask[kFusedUsers];
-    __shared__ int cnt[kFusedUsers];
-    __shared__ float unorm[kFusedUsers];
+    __shared__ unsigned long long buf[NU * CAP];
+    __shared__ unsigned long long thr[NU];
+    __shared__ unsigned long long mask[NU];
+    __shared__ int cnt[NU];
+    __shared__ float unorm[NU];
     __shared__ float bt[kFusedItems];
     __shared__ int thr_ver;                  // bumped whenever a compaction raised thresholds
 
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     const int wr = wv >> 1, wc = wv & 1;     // 32-row user block, 32-col item block
     const int h = lane >> 5, c = lane & 31;
     const int d = a.d, Dp = a.Dp, Dh = a.Dh;
-    const int u0 = blockIdx.x * kFusedUsers;
+    const int u0 = blockIdx.x * NU;
     if (tid == 0) thr_ver = 0;
     // the score words of the thresholds of this lane's 16 output rows, kept in
     // registers: a score whose key word is below its row's cannot enter the
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     uint32_t thi[16];
 #endif
     int thi_ver = -1;
-    const int nu = (a.n_users - u0) < kFusedUsers ? (a.n_users - u0) : kFusedUsers;
+    const int nu = (a.n_users - u0) < NU ? (a.n_users - u0) : NU;
 
     // A operand of lane (c, h): U[row wr*32 + c][h*Dh, (h+1)*Dh), zero-padded
     constexpr int kAH = kFusedMaxD / 2;
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     }
     int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
     int64_t nxt = INT64_MAX;                 // the train item at the cursor, kept in a register
-    if (tid < kFusedUsers) {
+    if (tid < NU) {
         thr[tid] = 0ull;
         cnt[tid] = 0;
         if (a.exclude_train && tid < nu) {
@@ -451,12 +454,12 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     // candidate phases and written to LDS after them (d % 4 == 0)
     const bool vec = (d & 3) == 0;
     const int q4 = Dp >> 2;
-    constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + kBlock - 1) / kBlock;
+    constexpr int kPre = (kFusedItems * (kFusedMaxD / 4) + NT - 1) / NT;
     float4 pre[kPre];
     auto load_tile = [&](int64_t jt) {   // 16-B loads; rows are 16-B aligned when d % 4 == 0
 #pragma unroll
         for (int q = 0; q < kPre; ++q) {
-            const int t = tid + q * kBlock;
+            const int t = tid + q * NT;
             const int r = t / q4, kk = (t - r * q4) * 4;
             const int64_t j = jt + r;
             pre[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     auto store_tile = [&]() {
 #pragma unroll
         for (int q = 0; q < kPre; ++q) {
-            const int t = tid + q * kBlock;
+            const int t = tid + q * NT;
             const int r = t / q4, kk = (t - r * q4) * 4;
             if (t < kFusedItems * q4) *reinterpret_cast<float4*>(Vs + vs_off(r, kk)) = pre[q];
         }
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
     for (int64_t j0 = 0; j0 < a.n_items; j0 += kFusedItems) {
         // ---- stage the item tile (unless prefetched), its bias, the train mask --
         if (!vec) {
-            for (int t = tid; t < kFusedItems * Dp; t += kBlock) {
+            for (int t = tid; t < kFusedItems * Dp; t += NT) {
                 const int r = t / Dp, kk = t - r * Dp;
                 const int64_t j = j0 + r;
                 Vs[vs_off(r, kk)] = (j < a.n_items && kk < d) ? a.V[j * d + kk] : 0.f;
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
         }
         if (MODEL == GBPR && tid < kFusedItems)
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
-        if (tid < kFusedUsers) {
+        if (tid < NU) {
             // the caller's item exclusions (one word per 64-item tile), then
             // the user's train items
             unsigned long long m = (MASK && a.item_mask != nullptr) ? a.item_mask[j0 >> 6] : 0ull;
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
             thi_ver = thr_ver;
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;   // < kFusedUsers
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;   // < NU
                 const float t = key_float((uint32_t)(thr[R] >> 32));
                 thf[q] = R < nu ? t : INFINITY;
             }
@@ -687,8 +690,8 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
         // the wave's 16 rows (wv, wv + 4, ..) are checked with one LDS read and
         // a ballot, not 16 dependent reads
         {
-            constexpr int kRowsPerWave = kFusedUsers / kWavesPerBlock;
-            const int Rl = wv + kWavesPerBlock * lane;
+            constexpr int kRowsPerWave = NU / NW;
+            const int Rl = wv + NW * lane;
             unsigned long long need = __ballot(lane < kRowsPerWave && Rl < nu &&
                                                cnt[lane < kRowsPerWave ? Rl : 0] > CAP - kFusedItems);
             if (need != 0ull) {
@@ -696,7 +699,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
                 while (need != 0ull) {
                     const int l = __ffsll((long long)need) - 1;
                     need &= need - 1ull;
-                    const int R = wv + kWavesPerBlock * l;
+                    const int R = wv + NW * l;
                     wave_compact<SR>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
                 }
             }
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(kBlock, CAP <= kFusedCap ? 2 : 1) void fused_topk_k
         __syncthreads();
     }
     // ---- final sort and output -------------------------------------------------------
-    for (int R = wv; R < nu; R += kWavesPerBlock) {
+    for (int R = wv; R < nu; R += NW) {
         const int n = wave_compact<SR>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);
         const int64_t orow = (int64_t)(u0 + R) * a.k;
         for (int o = lane; o < a.k; o += (CAP <= kFusedCap ? a.k : kWave)) {   // k <= 28: one pass
@@ -1271,6 +1274,25 @@ hipError_t launch_fused_topk(const FusedTopkArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(fused_topk_pipe_kernel<GBPR>, grid, block, 0, s, a);
         else
             hipLaunchKernelGGL(fused_topk_pipe_kernel<BPR>, grid, block, 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.variant == 3 && a.k <= kFusedMaxK) {   // 128 users per block, one block per CU
+        const dim3 g2((a.n_users + 2 * kFusedUsers - 1) / (2 * kFusedUsers)), b2(8 * kFusedUsers);
+        const bool m = a.item_mask != nullptr;
+        switch (a.model) {
+            case GBPR:
+                if (m) hipLaunchKernelGGL((fused_topk_kernel<GBPR, kFusedCap, true, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                else hipLaunchKernelGGL((fused_topk_kernel<GBPR, kFusedCap, false, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                break;
+            case CML:
+                if (m) hipLaunchKernelGGL((fused_topk_kernel<CML, kFusedCap, true, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                else hipLaunchKernelGGL((fused_topk_kernel<CML, kFusedCap, false, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                break;
+            default:
+                if (m) hipLaunchKernelGGL((fused_topk_kernel<BPR, kFusedCap, true, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                else hipLaunchKernelGGL((fused_topk_kernel<BPR, kFusedCap, false, 2 * kFusedUsers>), g2, b2, 0, s, a);
+                break;
+        }
         return hipGetLastError();
     }
     if (a.k > kFusedMaxK) {   // 28 < k <= 128: the wide lists, one block per CU

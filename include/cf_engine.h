@@ -458,7 +458,10 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "fused_variant" the fused scoring + top-k kernel: 0 = sequential (MFMAs,
  *                then the candidate test; default), 1 = software-pipelined
  *                (tile t's candidate test beside tile t+1's MFMAs; measured
- *                slower, kept for A/B; CML always takes 0).  Same output.
+ *                slower, kept for A/B; CML always takes 0), 2 = specialised
+ *                waves (measured slower), 3 = 128 users per block at one
+ *                block per CU (half the V-tile staging per FLOP; k <= 28).
+ *                Same output.
  *   "grad_path"  0 = auto (BPR / AMF / CML at W = 5, 64 < d <= 128, d % 4 == 0
  *                without pos_sort: the kernel with LDS-staged negative rows;
  *                else the phased gradient kernel for W in {1,5}, d <= 128,

@@ -191,7 +191,7 @@ def _check_lists(gpu_idx, scores, ref_lists, atol):
                 assert abs(scores[r][a] - scores[r][b]) <= atol, (r, a, b, scores[r][a], scores[r][b])
 
 
-@pytest.mark.parametrize("fused_variant", [0, 1], ids=["sequential", "pipelined"])
+@pytest.mark.parametrize("fused_variant", [0, 1, 3], ids=["sequential", "pipelined", "users128"])
 def test_fused_topk_d128_cfg5_slice(fused_variant):
     """The fused fp32-MFMA scoring + streaming top-10 (the cfg5 scoring
     kernel, amf.py:144-148 + bprmf.py:90-103) at d=128 on 4,096 users of the

@@ -2,7 +2,8 @@
 train-item exclusion and top-k order (descending, ties to the lower id, TF
 TopKV2) against the oracle's literal restatement.  Every test runs on both
 fused kernels (cf_set_option fused_variant: the sequential one and the
-software-pipelined one and, round 5, the specialised-wave one)."""
+software-pipelined one and, round 5, the specialised-wave one and the
+128-users-per-block one)."""
 import numpy as np
 import pytest
 
@@ -13,7 +14,7 @@ pytestmark = pytest.mark.gpu
 _FV = [0]
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2], ids=["fused-seq", "fused-pipe", "fused-ws"])
+@pytest.fixture(autouse=True, params=[0, 1, 2, 3], ids=["fused-seq", "fused-pipe", "fused-ws", "fused-u128"])
 def fused_variant(request):
     _FV[0] = request.param
     yield request.param
