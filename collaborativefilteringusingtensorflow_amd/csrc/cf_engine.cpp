@@ -76,7 +76,10 @@ struct cf_engine {
     // speculative negative counts (StepArgs::spec_ph), per buffer set
     int2* spec_ph_[2] = {nullptr, nullptr};
     int* spec_n_[2] = {nullptr, nullptr};
-    int spec_neg = 1;   // cf_set_option "spec_neg"
+    // cf_set_option "spec_neg": off by default since sorted batches (cfg2
+    // 0.3541 -> 0.3511 ms/step off, three runs each, profiles/r05/ab/r05w_*:
+    // psort's phantom zeroing costs 3 us, the fused draw no longer gains)
+    int spec_neg = 0;
     // deterministic mode on the pos_sort path: fixed-point partials and the
     // users' int64 overflow accumulators (StepArgs::det_fx)
     long long* slotP64 = nullptr;

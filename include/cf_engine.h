@@ -533,13 +533,14 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                is exact in any order, so no sort runs.
  *   "item_pieces" P = 1 (default) .. 64: the multi-rank item reduce in P
  *                pieces of item rows (cf_step_item_reduce).
- *   "spec_neg"   1 (default) = where pos_sort is active with its dense item
+ *   "spec_neg"   1 = where pos_sort is active with its dense item
  *                apply (n_items <= 2 B (1 + W)), the draw issues each
  *                negative's count atomic for its FIRST candidate before the
  *                row scan that accepts or rejects it (its latency overlaps
  *                the scan); a rejected first candidate leaves a phantom
  *                occurrence whose slot row psort zeroes.  Same batches, same
- *                sums up to fp32 order; 0 = count after the scan.
+ *                sums up to fp32 order; 0 (default since round 5's sorted
+ *                batches: 3 us faster at cfg2) = count after the scan.
  *   "pair_prefetch" 1 = the pos_sort gradient launch also fetches the next
  *                step's shuffled pair records for its draw (cf_train_steps);
  *                measured slower at cfg2 (its registers cost the gradient
