@@ -372,6 +372,8 @@ def main():
                     help="cf_set_option pair_prefetch (the gradient launch fetches the next draw's pair records)")
     ap.add_argument("--deterministic", type=int, default=0,
                     help="cf_set_option deterministic (sort-based ranks, no float atomics)")
+    ap.add_argument("--set-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra cf_set_option calls (A/B experiments), applied after the flags above")
     ap.add_argument("--amf-mode", default="reference", choices=["reference", "apr"],
                     help="AMF configs: cf_config.amf_mode (apr: Δ from the normalised embedding-loss "
                          "gradient, DESIGN 3.13; not the reference's computation)")
@@ -506,6 +508,10 @@ def main():
         eng.set_option("deterministic", 1)
     if args.slot_max:
         eng.set_option("slot_max", args.slot_max)
+    for kv in args.set_option:
+        name, val = kv.split("=", 1)
+        eng.set_option(name, int(val))
+        cfg["desc"] += " [%s=%s]" % (name, val)
     eng.set_interactions(indptr, indices)
     eng.init_params(0.0, 0.1, truncated=cfg["truncated"], seed=1)  # same V on every rank
     if cfg["model"] == "amf":
