@@ -158,3 +158,30 @@ def test_amf_class_apr_trains(fold1):
         sampler.close()
         assert out[mode][0] > 0.05, (mode, out[mode])
     assert out["reference"] != out["apr"]
+
+
+@pytest.mark.parametrize("B", [1, 17, 93])
+def test_apr_ragged_batches(fold1, streams, B):
+    """Batches that fill no block or wave evenly (the grid tails of the three
+    apr launches), including a single pair whose rows are all seen once."""
+    st = get_stream(streams, "rank_b100_w5")
+    e = _engine(fold1, 72, 5)
+    e.begin_phase(1)
+    for s in range(4):
+        _local_step(e, st["pairs"][s][:B], st["negs"][s][:B], 0.5)
+    e.close()
+
+
+def test_apr_hot_rows_in_one_batch(fold1):
+    """One user and one positive in every pair of a batch, negatives drawn
+    from a handful of items: every row is duplicated, user and positive
+    past their slot caps (float atomics), Δ from the summed Gadv rows."""
+    rng = np.random.RandomState(5)
+    B, W = 96, 5
+    pairs = np.stack([np.full(B, 7), np.full(B, 11)], 1).astype(np.int32)
+    negs = rng.randint(100, 106, size=(B, W)).astype(np.int32)
+    e = _engine(fold1, 40, W)
+    e.begin_phase(1)
+    for _ in range(3):
+        _local_step(e, pairs, negs, 0.5)
+    e.close()
