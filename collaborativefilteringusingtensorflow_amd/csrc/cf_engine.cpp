@@ -138,6 +138,9 @@ struct cf_engine {
     float* slotV = nullptr;   // [n_items * capV, d]
     float* slotVb = nullptr;  // [n_items * capV] item-bias gradient beside each slot row (GBPR / PLR)
     int capU = 2, capV = 32;
+    // user cap chosen at the first step from the batch's expected occurrences
+    // per user (ensure_batch) until cf_set_option("slot_max_user") sets it
+    bool capU_auto = true;
     // item records instead of item slot rows (cf_set_option "item_slots" 1):
     // 16 B per duplicated item occurrence + each pair's pre-update user row
     // (GBPR: its group blend row) stashed once (StepArgs::recV)
@@ -509,6 +512,22 @@ int ensure_stash(cf_engine* e, int B) {
 int ensure_order(cf_engine* e, int B);
 
 int ensure_batch(cf_engine* e, int B) {
+    if (e->capU_auto && e->Bcap == 0) {
+        // a user occurs Poisson(lam) times in a batch; its occurrences past
+        // capU take float atomics and, in deterministic mode, a compact GU64
+        // row handed out by ONE counter in psort (one address: ~88 grants per
+        // us).  cfg2 at B = 2^19 (lam 0.52): capU 2 -> 16K hot users a step,
+        // det psort 29 -> 101 us; capU 4 -> ~200 (det 0.480 -> 0.393 ms/step,
+        // fast 0.3542 -> 0.3526, profiles/r05/ab/r05ad_*) for 512 MB more
+        // slot rows.  Sparse batches (cfg4, B = 65,536) keep 2.
+        const double lam = (double)B * users_per_pair(e->cfg) / (double)e->cfg.n_users;
+        const int want = lam >= 0.25 ? 4 : 2;
+        if (want != e->capU) {
+            e->capU = want;
+            e->slots_ready = false;
+            e->fx_cap = 0;   // the compact GU64 rows scale with 1 / (capU + 1)
+        }
+    }
     CF_TRY(ensure_slots(e));
     CF_TRY(ensure_order(e, B));
     if (e->det) CF_TRY(ensure_det(e, std::max(B, e->Bcap), B));
@@ -2716,7 +2735,12 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         if (value < 1 || value > 256) return fail(CF_EINVAL, n + " must be in [1, 256]");
         CF_TRY(discard_pending(e));
         CF_HIP(hipStreamSynchronize(e->stream));
-        if (n == "slot_max") e->capV = (int)value; else e->capU = (int)value;
+        if (n == "slot_max") {
+            e->capV = (int)value;
+        } else {
+            e->capU = (int)value;
+            e->capU_auto = false;
+        }
         e->slots_ready = false;   // re-sized at the next step
         if (n == "slot_max_user") e->fx_cap = 0;   // the compact GU64 rows scale with 1 / (capU + 1)
         return CF_OK;

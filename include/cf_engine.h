@@ -478,7 +478,9 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *                add into a float accumulator with atomics; the apply sums
  *                both (default 32).  Same arithmetic up to fp32 summation
  *                order.
- *   "slot_max_user" the same for user rows (default 2).
+ *   "slot_max_user" the same for user rows (default: chosen at the first
+ *                step, 4 when a batch holds >= 0.25 occurrences per user on
+ *                average, else 2).
  *   "hot_replicas" the atomic part of a hot item row is spread over this many
  *                accumulator copies by occurrence rank (1, 2, 4, 8, 16;
  *                default 1: at cfg2 the copies' extra apply reads cost more
