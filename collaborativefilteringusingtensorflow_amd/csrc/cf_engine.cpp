@@ -796,6 +796,9 @@ int epoch_order(cf_engine* e, int B, const int32_t** out) {
         // not computed ahead (first epoch, a jump, another B): in order on the engine stream
         k = (e->eo[0].epoch == ep + 1 && e->eo[0].B == B) ? 1 : 0;
         if (e->eo[k].async) CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
+        // a draw on the side stream (prep_stream 1) may still read the slot
+        CF_HIP(hipEventRecord(e->eo_mark, e->side));
+        CF_HIP(hipStreamWaitEvent(e->stream, e->eo_mark, 0));
         CF_TRY(compute_epoch_order(e, k, ep, B, e->stream));
     } else if (e->eo[k].async) {
         CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
@@ -806,7 +809,11 @@ int epoch_order(cf_engine* e, int B, const int32_t** out) {
     if (!(nx.epoch == ep + 1 && nx.B == B) && e->nnz / B >= 2) {
         // the next epoch's order, behind everything the engine stream holds
         // so far (the kernels that still read this slot's previous epoch)
+        // (and the side stream's draws, prep_stream 1: a wait takes the
+        // event's latest record, so one event serves both)
         CF_HIP(hipEventRecord(e->eo_mark, e->stream));
+        CF_HIP(hipStreamWaitEvent(e->eo_stream, e->eo_mark, 0));
+        CF_HIP(hipEventRecord(e->eo_mark, e->side));
         CF_HIP(hipStreamWaitEvent(e->eo_stream, e->eo_mark, 0));
         CF_TRY(compute_epoch_order(e, k ^ 1, ep + 1, B, e->eo_stream));
     }

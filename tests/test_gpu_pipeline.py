@@ -72,3 +72,29 @@ def test_train_steps_equals_host_fed_stream(fold1, model, d, W, G, B, opts):
         assert_close(dev.get_table(t), host.get_table(t), t)
     host.close()
     dev.close()
+
+
+@pytest.mark.parametrize("opts", [{}, {"prep_stream": 1, "pipeline": 0}, {"pipeline": 2}],
+                         ids=["pipelined", "side-stream", "draw-in-grad"])
+def test_sorted_batches_across_epochs(fold1, opts):
+    """Sorted batches over several epoch boundaries (B = 2,000: 22 batches an
+    epoch on ml-100k, so auto sorts them): the next epoch's order is computed
+    on its own low-priority stream into the slot the epoch before last used,
+    behind every draw that may still read it -- on the engine stream and, with
+    prep_stream 1, on the side stream.  The pipelined device loop must train
+    what the host-fed sample + step stream trains."""
+    K, B = 50, 2000
+    host = make("bpr", fold1, 32, 1, 1)
+    dev = make("bpr", fold1, 32, 1, 1, **opts)
+    loss_h = 0.0
+    for _ in range(K):
+        pairs, negs, groups = host.sample(B)
+        assert np.all(np.diff(pairs[:, 0]) >= 0)   # CSR order inside the batch
+        loss_h += host.step(pairs, negs, groups)
+    loss_d = dev.train_steps(B, K)
+    assert abs(loss_d - loss_h) <= RTOL * abs(loss_h), (loss_d, loss_h)
+    assert host.sampler_state() == dev.sampler_state()
+    for t in TABLES["bpr"]:
+        assert_close(dev.get_table(t), host.get_table(t), t)
+    host.close()
+    dev.close()
