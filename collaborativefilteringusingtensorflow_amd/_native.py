@@ -101,6 +101,8 @@ SIGNATURES = {
     "cf_step_items_range": (ctypes.c_int, [_P, _I64, _I64, _P, _P]),
     "cf_bind_table": (ctypes.c_int, [_P, _I32, _P, _I64]),
     "cf_step_local_grad": (ctypes.c_int, [_P, _I32, _PI32, _PI32, _PI32]),
+    "cf_bind_apr_item_grad": (ctypes.c_int, [_P, _P, _I64]),
+    "cf_step_local_apr_embed": (ctypes.c_int, [_P, _I32, _PI32, _PI32]),
     "cf_step_local_apply": (ctypes.c_int, [_P, _I32]),
     "cf_step_item_reduce": (ctypes.c_int, [_P, _I32]),
     "cf_item_piece_rows": (ctypes.c_int, [_P, _I32, _I32, _PI64, _PI64]),

@@ -129,6 +129,10 @@ struct cf_engine {
     // duplicated row (apr_embed_kernel), zero between steps; Δ = epsilon *
     // l2_normalize(row).  Rows seen once take Δ from their own pair.
     float *GadvU = nullptr, *GadvV = nullptr;
+    // multi-rank (dense_item_apply): GadvV is the caller's buffer
+    // (cf_bind_apr_item_grad), all-reduced between cf_step_local_apr_embed and
+    // cf_step_local_grad so every item row's Δ comes from the global batch
+    float* GadvV_bound = nullptr;
     int32_t* cntU_[2] = {nullptr, nullptr};  // per-row occurrence counts (0 between steps)
     int32_t* cntV_[2] = {nullptr, nullptr};
     // store-and-sum of duplicated rows: row r of a table owns the fixed slot
@@ -638,7 +642,8 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
         a.apr = 1;
         a.epsilon = c.epsilon;
         a.GadvU = e->GadvU;
-        a.GadvV = e->GadvV;
+        a.GadvV = c.dense_item_apply ? e->GadvV_bound : e->GadvV;
+        a.apr_global = c.dense_item_apply ? 1 : 0;
     }
     a.use_rank_weight = c.use_rank_weight;
     a.n_items_f = (float)c.n_items;
@@ -1194,6 +1199,9 @@ int finish_step(cf_engine* e, const StepArgs& a, int B, int k, double* loss_acc,
 // overlap the previous step's kernels.
 int run_step(cf_engine* e, int B, const int32_t* pairs, const int32_t* negs,
              const int32_t* groups, double* loss_acc) {
+    if (e->cfg.amf_mode == CF_AMF_APR && e->phase == 1 && e->cfg.dense_item_apply && !e->GadvV_bound)
+        return fail(CF_ESTATE, "amf_mode apr with dense_item_apply: bind the apr item buffer first "
+                               "(cf_bind_apr_item_grad)");
     CF_TRY(ensure_batch(e, B));
     const int k = e->set;
     e->set ^= 1;
@@ -1491,9 +1499,6 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     if (c.amf_mode != CF_AMF_REFERENCE && c.amf_mode != CF_AMF_APR)
         return fail(CF_EINVAL, "amf_mode must be CF_AMF_REFERENCE (0) or CF_AMF_APR (1)");
     if (c.amf_mode == CF_AMF_APR && c.model != CF_AMF) return fail(CF_EINVAL, "amf_mode apr is an AMF mode");
-    if (c.amf_mode == CF_AMF_APR && c.dense_item_apply)
-        return fail(CF_EINVAL, "amf_mode apr is single-rank: the item Δ needs the cross-rank gradient sum "
-                               "(not built; DESIGN 3.13)");
     if (c.amf_mode == CF_AMF_APR && !(c.epsilon >= 0.f)) return fail(CF_EINVAL, "epsilon must be >= 0");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -1542,10 +1547,14 @@ int cf_create(const cf_config* cfg, cf_engine** out) {
     e->Gb = e->Gb_own;
     e->shard_u1 = c.n_users;
     if (c.amf_mode == CF_AMF_APR) {
-        if ((r = dalloc(&e->GadvU, ud)) || (r = dalloc(&e->GadvV, id))) return bail(r);
-        if (hipMemsetAsync(e->GadvU, 0, ud * 4, e->stream) != hipSuccess ||
-            hipMemsetAsync(e->GadvV, 0, id * 4, e->stream) != hipSuccess)
+        if ((r = dalloc(&e->GadvU, ud))) return bail(r);
+        if (hipMemsetAsync(e->GadvU, 0, ud * 4, e->stream) != hipSuccess)
             return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
+        if (!c.dense_item_apply) {   // multi-rank: the caller binds the item buffer
+            if ((r = dalloc(&e->GadvV, id))) return bail(r);
+            if (hipMemsetAsync(e->GadvV, 0, id * 4, e->stream) != hipSuccess)
+                return bail(fail(CF_EHIP, "hipMemsetAsync failed"));
+        }
     }
     if (hipHostMalloc((void**)&e->h_loss, sizeof(double), hipHostMallocDefault) != hipSuccess)
         return bail(fail(CF_ENOMEM, "pinned allocation failed"));
@@ -1999,25 +2008,87 @@ int cf_bind_item_grad(cf_engine* e, void* ptr, int64_t n) {
     return CF_OK;
 }
 
+int cf_bind_apr_item_grad(cf_engine* e, void* ptr, int64_t n) {
+    CF_TRY(check_engine(e));
+    const cf_config& c = e->cfg;
+    if (c.amf_mode != CF_AMF_APR || !c.dense_item_apply)
+        return fail(CF_ESTATE, "cf_bind_apr_item_grad needs amf_mode apr and dense_item_apply=1");
+    if (e->lg_stage != 0) return fail(CF_ESTATE, "a split step is in progress");
+    const int64_t id = c.n_items * (int64_t)c.n_factors;
+    if (n != id) return fail(CF_EINVAL, "apr item buffer must hold " + std::to_string(id) + " floats");
+    if (!ptr) {
+        e->GadvV_bound = nullptr;
+        return CF_OK;
+    }
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess || attr.type != hipMemoryTypeDevice)
+        return fail(CF_EINVAL, "apr item buffer is not device memory");
+    CF_HIP(hipMemsetAsync(ptr, 0, (size_t)n * 4, e->stream));
+    e->GadvV_bound = (float*)ptr;
+    return CF_OK;
+}
+
+// the split step's batch: drawn + counted by the previous apply launch, or
+// drawn / packed now
+static int local_batch(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
+                       const int32_t* groups, StepArgs* a, int* k) {
+    if (e->pend && (pairs || e->pend_B != B)) CF_TRY(discard_pending(e));
+    CF_TRY(ensure_batch(e, B));
+    if (e->pend) {
+        *a = e->pend_args;
+        *k = e->pend_set;
+        e->pend = false;
+    } else {
+        *k = e->set;
+        e->set ^= 1;
+        CF_TRY(begin_step(e, B, pairs, negs, groups, *k, e->stream, a));
+    }
+    return CF_OK;
+}
+
+int cf_step_local_apr_embed(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs) {
+    CF_TRY(check_engine(e));
+    if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "the split step needs dense_item_apply=1");
+    if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
+    if (e->lg_stage != 0) return fail(CF_ESTATE, "cf_step_local_apply of the previous step is missing");
+    if (e->cfg.amf_mode != CF_AMF_APR || e->phase != 1)
+        return fail(CF_ESTATE, "cf_step_local_apr_embed: amf_mode apr in the adversarial phase only");
+    if (!e->GadvV_bound) return fail(CF_ESTATE, "bind the apr item buffer first (cf_bind_apr_item_grad)");
+    StepArgs a;
+    int k;
+    CF_TRY(local_batch(e, B, pairs, negs, nullptr, &a, &k));
+    {
+        ProfScope ps(e, CF_K_STEP);
+        CF_HIP(launch_apr_embed(a, e->stream));
+    }
+    e->lg_args = a;
+    e->lg_set = k;
+    e->lg_B = B;
+    e->lg_stage = 3;   // the caller all-reduces the bound buffer, then cf_step_local_grad
+    return CF_OK;
+}
+
 int cf_step_local_grad(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
                        const int32_t* groups) {
     CF_TRY(check_engine(e));
     if (!e->cfg.dense_item_apply) return fail(CF_ESTATE, "the split step needs dense_item_apply=1");
     CF_TRY(check_not_xchg(e));
     if (B < 1) return fail(CF_EINVAL, "B must be >= 1");
-    if (e->lg_stage != 0) return fail(CF_ESTATE, "cf_step_local_apply of the previous step is missing");
-    if (e->pend && (pairs || e->pend_B != B)) CF_TRY(discard_pending(e));
-    CF_TRY(ensure_batch(e, B));
     StepArgs a;
     int k;
-    if (e->pend) {  // drawn + counted by the previous apply launch
-        a = e->pend_args;
-        k = e->pend_set;
-        e->pend = false;
+    if (e->lg_stage == 3) {   // after cf_step_local_apr_embed + the caller's all-reduce
+        if (pairs || negs || groups || B != e->lg_B)
+            return fail(CF_EINVAL, "after cf_step_local_apr_embed pass the same B and no batch");
+        a = e->lg_args;
+        k = e->lg_set;
+        a.apr_embed_done = 1;
+        e->lg_stage = 0;
     } else {
-        k = e->set;
-        e->set ^= 1;
-        CF_TRY(begin_step(e, B, pairs, negs, groups, k, e->stream, &a));
+        if (e->lg_stage != 0) return fail(CF_ESTATE, "cf_step_local_apply of the previous step is missing");
+        if (e->cfg.amf_mode == CF_AMF_APR && e->phase == 1)
+            return fail(CF_ESTATE, "amf_mode apr: cf_step_local_apr_embed and the all-reduce of the bound "
+                                   "buffer come first");
+        CF_TRY(local_batch(e, B, pairs, negs, groups, &a, &k));
     }
     CF_TRY(det_ranks(e, a));
     CF_TRY(psort(e, a));
@@ -2150,7 +2221,15 @@ int cf_step_local_draw(cf_engine* e, int32_t B) {
 
 int cf_step_local(cf_engine* e, int32_t B, const int32_t* pairs, const int32_t* negs,
                   const int32_t* groups) {
-    CF_TRY(cf_step_local_grad(e, B, pairs, negs, groups));
+    CF_TRY(check_engine(e));
+    if (e->cfg.amf_mode == CF_AMF_APR && e->phase == 1 && e->cfg.dense_item_apply) {
+        // apr with no caller collective: this rank's sum is taken as the
+        // global one (exact at world size 1)
+        CF_TRY(cf_step_local_apr_embed(e, B, pairs, negs));
+        CF_TRY(cf_step_local_grad(e, B, nullptr, nullptr, nullptr));
+    } else {
+        CF_TRY(cf_step_local_grad(e, B, pairs, negs, groups));
+    }
     // the one-call form has no caller collective between item-reduce pieces
     // (item_pieces > 1 defers them): reduce every remaining piece here, so the
     // apply finds the item gradient complete

@@ -51,8 +51,10 @@ __global__ __launch_bounds__(kBlock) void apr_embed_kernel(StepArgs a) {
         const int i = a.occV[p];
         const int cu = a.cntU[u];
         const int ci = a.cntV[i];
-        bool dup = cu >= 2 || ci >= 2;
-        for (int w = 0; w < W; ++w) dup |= a.cntV[a.occV[a.B + p * W + w]] >= 2;
+        // multi-rank (apr_global): every item occurrence adds, a row seen once
+        // here may be seen on another rank
+        bool dup = cu >= 2 || ci >= 2 || a.apr_global;
+        for (int w = 0; w < W && !dup; ++w) dup |= a.cntV[a.occV[a.B + p * W + w]] >= 2;
         if (!dup) continue;
         float uu[EPL], vi[EPL], gu[EPL];
         il_load<EPL>(a.U, u, d, gl, uu);
@@ -69,14 +71,14 @@ __global__ __launch_bounds__(kBlock) void apr_embed_kernel(StepArgs a) {
             sc += c;
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = fmaf(c, vi[s] - vj[s], gu[s]);
-            if (a.cntV[j] >= 2) {
+            if (a.apr_global || a.cntV[j] >= 2) {
 #pragma unroll
                 for (int s = 0; s < EPL; ++s) vj[s] = -c * uu[s];
                 il_atomic<EPL>(a.GadvV, j, d, gl, vj);
             }
         }
         if (cu >= 2) il_atomic<EPL>(a.GadvU, u, d, gl, gu);
-        if (ci >= 2) {
+        if (a.apr_global || ci >= 2) {
 #pragma unroll
             for (int s = 0; s < EPL; ++s) gu[s] = sc * uu[s];
             il_atomic<EPL>(a.GadvV, i, d, gl, gu);
@@ -93,6 +95,7 @@ __global__ __launch_bounds__(kBlock) void apr_zero_kernel(StepArgs a, int64_t nU
     const int64_t q = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 4;
     if (q >= n) return;
     const bool user = q < nU;
+    if (!user && a.apr_global) return;   // the item buffer is cleared whole (launch_grad_amf)
     const int64_t o = user ? q : q - nU;
     const int r = user ? a.occU[o] : a.occV[o];
     const int rank = user ? a.rankU[o] : a.rankV[o];
@@ -193,20 +196,29 @@ static hipError_t launch_apr_zero(const StepArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_apr_embed(const StepArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    if (!a.apr || a.GadvU == nullptr || a.GadvV == nullptr || !a.count_users) return hipErrorInvalidValue;
+    return a.W == 1 ? launch_apr_embed_w<1>(a, s) : a.W == 5 ? launch_apr_embed_w<5>(a, s) : launch_apr_embed_w<0>(a, s);
+}
+
 hipError_t launch_grad_amf(const StepArgs& a, const StepArgs* nx, hipStream_t s) {
     if (!a.apr || a.B <= 0) return launch_grad_m<AMF>(a, nx, s);
-    // apr runs on slot rows with counted users and items: no pos_sort, item
-    // records, deterministic compact slots or multi-rank item reduce
-    if (a.srec != nullptr || a.recV != nullptr || a.det_fx || a.offU != nullptr || a.items_grad_only ||
-        !a.count_users || !a.count_items || a.GadvU == nullptr || a.GadvV == nullptr)
+    // apr runs on slot rows with counted users: no pos_sort, item records or
+    // deterministic compact slots; items counted too unless every item row
+    // reads the all-reduced buffer (apr_global, the multi-rank item reduce)
+    if (a.srec != nullptr || a.recV != nullptr || a.det_fx || a.offU != nullptr || !a.count_users ||
+        (!a.apr_global && (a.items_grad_only || !a.count_items)) || a.GadvU == nullptr || a.GadvV == nullptr)
         return hipErrorInvalidValue;
-    hipError_t err = a.W == 1 ? launch_apr_embed_w<1>(a, s)
-                   : a.W == 5 ? launch_apr_embed_w<5>(a, s) : launch_apr_embed_w<0>(a, s);
-    if (err != hipSuccess) return err;
+    hipError_t err = hipSuccess;
+    if (!a.apr_embed_done && (err = launch_apr_embed(a, s)) != hipSuccess) return err;
     err = a.W == 1 ? launch_apr_grad<1>(a, nx, s)
         : (a.W == 5 && epl_for(a.d) <= 8) ? launch_apr_grad<5>(a, nx, s) : launch_apr_grad<0>(a, nx, s);
     if (err != hipSuccess) return err;
-    return launch_apr_zero(a, s);
+    if ((err = launch_apr_zero(a, s)) != hipSuccess) return err;
+    if (a.apr_global)   // rows of every rank's batch are set after the all-reduce
+        return hipMemsetAsync(a.GadvV, 0, (size_t)a.n_items * a.d * sizeof(float), s);
+    return hipSuccess;
 }
 
 }  // namespace cfk

@@ -51,6 +51,8 @@ struct StepArgs {
     float epsilon;
     float* GadvU;
     float* GadvV;
+    int apr_global;       // multi-rank: GadvV holds every item row's sum over all ranks
+    int apr_embed_done;   // cf_step_local_apr_embed ran (and the caller all-reduced GadvV)
     int use_rank_weight;
     float n_items_f;
     int64_t n_items;
@@ -392,6 +394,10 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + cou
 // gather, loss, grads, singleton apply; with `next`, the same launch also
 // draws and counts the next step's batch (other buffer set)
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
+// AMF apr: the embedding-loss pass alone (cf_step_local_apr_embed)
+hipError_t launch_apr_embed(const StepArgs& a, hipStream_t s);
+// AMF apr: the embedding-loss pass alone (cf_step_local_apr_embed)
+hipError_t launch_apr_embed(const StepArgs& a, hipStream_t s);
 // the phased gradient kernel's compile-time W (1 or 5) a step takes, 0 = generic
 int grad_fast_w(const StepArgs& a);
 // the step takes grad_lds_kernel (LDS-staged negatives)

@@ -1142,7 +1142,8 @@ __device__ __forceinline__ void apr_pair(const StepArgs& a, int p, int gl, int u
     apr_delta<EPL>(a.GadvU, u, cu, d, gl, a.epsilon, g1, up);
 #pragma unroll
     for (int s = 0; s < EPL; ++s) g1[s] = sc * uu[s];
-    apr_delta<EPL>(a.GadvV, i, ci, d, gl, a.epsilon, g1, ip);
+    // multi-rank (apr_global): every item row's Δ from the all-reduced sum
+    apr_delta<EPL>(a.GadvV, i, a.apr_global ? 2 : ci, d, gl, a.epsilon, g1, ip);
 #pragma unroll
     for (int s = 0; s < EPL; ++s) {
         up[s] += uu[s];
@@ -1162,7 +1163,7 @@ __device__ __forceinline__ void apr_pair(const StepArgs& a, int p, int gl, int u
         float jp[EPL];
 #pragma unroll
         for (int s = 0; s < EPL; ++s) jp[s] = -c * uu[s];
-        apr_delta<EPL>(a.GadvV, J.j[sl], J.c[sl], d, gl, a.epsilon, jp, jp);
+        apr_delta<EPL>(a.GadvV, J.j[sl], a.apr_global ? 2 : J.c[sl], d, gl, a.epsilon, jp, jp);
 #pragma unroll
         for (int s = 0; s < EPL; ++s) jp[s] += J.v[sl][s];
         const float xP = uiP - gdot<EPL>(uu, jp);

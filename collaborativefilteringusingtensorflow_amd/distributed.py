@@ -206,13 +206,17 @@ class ShardedStep(object):
     is complete and runs beside the user update and the draw of the next
     batch; the item update waits for it."""
 
-    def __init__(self, backend, items, process_group=None, draw_ahead=True):
+    def __init__(self, backend, items, process_group=None, draw_ahead=True, apr_buf=None):
         import torch.distributed as dist
         self.backend = backend
         self.items = _items(items, process_group)
         self.item_grad = self.items.grad
         self.group = process_group
         self.draw_ahead = draw_ahead
+        # AMF apr (include/cf_engine.h cf_step_local_apr_embed): the bound
+        # [n_items * d] buffer of the embedding-loss sums, all-reduced before
+        # the gradient launch in the adversarial phase (SURVEY 8(e))
+        self.apr_buf = apr_buf
         self._dist = dist
 
     def __call__(self, batch_size=None, pairs=None, negs=None, groups=None):
@@ -226,7 +230,13 @@ class ShardedStep(object):
             x.apply(be)
             x.gather(dist, False)
             return
-        if pairs is None:
+        if self.apr_buf is not None and be.apr_active():
+            # every item row's Δ from the global batch: this rank's sums, the
+            # all-reduce, then the gradient launch on the summed buffer
+            B = be.step_local_apr_embed(batch_size, pairs, negs)
+            dist.all_reduce(self.apr_buf, group=self.group)
+            be.step_local_grad(B)
+        elif pairs is None:
             be.step_local_grad(batch_size)
         else:
             be.step_local_grad(pairs=pairs, negs=negs, groups=groups)
@@ -316,7 +326,11 @@ def make_gpu_sharded(engine, n_items, d, with_bias, device, exchange="allreduce"
         items = AllReduceItems(grad, process_group, pieces=pieces, row_width=d, n_rows=n_items)
     else:
         raise ValueError("exchange must be 'allreduce' or 'rs_ag'")
-    return ShardedStep(engine, items, process_group), items
+    apr_buf = None
+    if getattr(engine, "cfg", None) is not None and engine.cfg.amf_mode == 1:   # CF_AMF_APR
+        apr_buf = torch.zeros(n_items * d, dtype=torch.float32, device=device)
+        engine.bind_apr_item_grad(apr_buf.data_ptr(), apr_buf.numel())
+    return ShardedStep(engine, items, process_group, apr_buf=apr_buf), items
 
 
 def item_users(indptr, indices, n_items):

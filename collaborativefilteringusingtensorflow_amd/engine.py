@@ -285,6 +285,12 @@ class Engine(object):
 
     def begin_phase(self, phase):
         N.check(self._L.cf_begin_phase(self._h, int(phase)), "cf_begin_phase")
+        self._phase = int(phase)
+
+    def apr_active(self):
+        """AMF apr in its adversarial phase: a multi-rank step needs
+        step_local_apr_embed + the all-reduce of the apr buffer first."""
+        return self.cfg.amf_mode == N.CF_AMF_APR and getattr(self, "_phase", 0) == 1
 
     # ---- multi-rank split step -------------------------------------------------
     def bind_item_grad(self, device_ptr, n_elems):
@@ -308,6 +314,22 @@ class Engine(object):
         B, pairs, negs, gp, _keep = self._batch(pairs, negs, groups)
         N.check(self._L.cf_step_local_grad(self._h, B, _arg(pairs, ctypes.c_int32),
                                            _arg(negs, ctypes.c_int32), gp), "cf_step_local_grad")
+
+    def bind_apr_item_grad(self, device_ptr, n_elems):
+        """The n_items * d buffer an apr step's item sums are all-reduced in
+        (include/cf_engine.h cf_bind_apr_item_grad)."""
+        N.check(self._L.cf_bind_apr_item_grad(self._h, ctypes.c_void_p(device_ptr), int(n_elems)),
+                "cf_bind_apr_item_grad")
+
+    def step_local_apr_embed(self, batch_size=None, pairs=None, negs=None):
+        if pairs is None:
+            N.check(self._L.cf_step_local_apr_embed(self._h, int(batch_size), None, None),
+                    "cf_step_local_apr_embed")
+            return int(batch_size)
+        B, pairs, negs, _gp, _keep = self._batch(pairs, negs, None)
+        N.check(self._L.cf_step_local_apr_embed(self._h, B, _arg(pairs, ctypes.c_int32),
+                                                _arg(negs, ctypes.c_int32)), "cf_step_local_apr_embed")
+        return B
 
     def step_local_apply(self, next_batch_size=0):
         N.check(self._L.cf_step_local_apply(self._h, int(next_batch_size)), "cf_step_local_apply")

@@ -147,8 +147,9 @@ typedef struct cf_config {
                                  Δ_X = epsilon * l2_normalize(dL_embed/dX, axis 1)
                                  from the step's pre-update rows (stop-gradient),
                                  perturbing U_u, V_i, V_j in ui and V_j in uj
-                                 (amf.py:96-116).  Single-rank, not deterministic,
-                                 slot rows (item_slots 0); see DESIGN 3.13      */
+                                 (amf.py:96-116).  Not deterministic, slot rows
+                                 (item_slots 0); across ranks see
+                                 cf_step_local_apr_embed; DESIGN 3.13           */
 } cf_config;
 
 enum cf_amf_mode { CF_AMF_REFERENCE = 0, CF_AMF_APR = 1 };
@@ -300,6 +301,21 @@ int cf_step_local_apply(cf_engine* eng, int32_t next_B);
  * bprmf.py:83-88). */
 int cf_step_item_reduce(cf_engine* eng, int32_t piece);
 int cf_item_piece_rows(cf_engine* eng, int32_t piece, int32_t n_pieces, int64_t* row0, int64_t* row1);
+/* AMF apr across ranks (amf_mode CF_AMF_APR with dense_item_apply=1; DESIGN
+ * 3.13): an item row's Δ = epsilon * l2_normalize of its embedding-loss
+ * gradient over the GLOBAL batch (amf.py:130-137 on the concatenated batch),
+ * so its sum crosses ranks before the gradient launch -- SURVEY 8(e)'s second
+ * all-reduce.  Bind an n_items*d fp32 device buffer once; in the adversarial
+ * phase each step is
+ *   cf_step_local_apr_embed(eng, B, pairs|NULL, negs|NULL)  this rank's sums
+ *   (all-reduce the bound buffer)
+ *   cf_step_local_grad(eng, B, NULL, NULL, NULL)  the step on the summed Δ;
+ *                                 it clears the buffer after reading it
+ * and then the usual item exchange.  cf_step_local_grad without the embed
+ * fails with CF_ESTATE in that phase; cf_step_local (one call, no caller
+ * collective) runs both halves, exact at world size 1. */
+int cf_bind_apr_item_grad(cf_engine* eng, void* device_ptr, int64_t n_elems);
+int cf_step_local_apr_embed(cf_engine* eng, int32_t B, const int32_t* host_pairs, const int32_t* host_negs);
 /* Phase 2, after the buffer holds the cross-rank sum: dense item Adagrad
  * (and CML clip of updated rows); zeroes the buffer. */
 int cf_step_items(cf_engine* eng);

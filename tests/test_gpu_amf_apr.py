@@ -130,8 +130,19 @@ def test_apr_rejects_what_it_does_not_cover(fold1):
     nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
     with pytest.raises(NativeError, match="AMF mode"):
         Engine("bpr", nu, ni, 16, amf_mode="apr")
-    with pytest.raises(NativeError, match="single-rank"):
-        Engine("amf", nu, ni, 16, n_neg=5, amf_mode="apr", dense_item_apply=True)
+    # multi-rank: the item sums cross ranks through a bound buffer, and the
+    # gradient launch comes after the embed pass + the caller's all-reduce
+    d = Engine("amf", nu, ni, 16, n_neg=5, amf_mode="apr", dense_item_apply=True)
+    d.set_interactions(fold1["train_indptr"], fold1["train_indices"])
+    d.begin_phase(1)
+    with pytest.raises(NativeError, match="bind the apr item buffer"):
+        d.step_local_apr_embed(100)
+    import torch
+    buf = torch.zeros(ni * 16, dtype=torch.float32, device="cuda:0")
+    d.bind_apr_item_grad(buf.data_ptr(), buf.numel())
+    with pytest.raises(NativeError, match="cf_step_local_apr_embed and the all-reduce"):
+        d.step_local_grad(100)
+    d.close()
     e = _engine(fold1, 128, 5)
     with pytest.raises(NativeError, match="deterministic"):
         e.set_option("deterministic", 1)

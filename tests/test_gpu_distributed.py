@@ -330,3 +330,109 @@ def test_one_rank_rccl_item_reduce_in_pieces(fold1, one_call):
         # P = 1: one whole reduce per step; P > 1: deferred, P piece launches
         assert n_red == 6 * P, (P, n_red)
         assert worst <= 1.0, (P, worst)
+
+
+def _apr_worker(rank, world, port, fold, batches, U0, V0, q, backend, exchange="allreduce", opts=None):
+    """AMF apr across ranks: each rank's users, the item rows' Δ from the
+    global batch (cf_step_local_apr_embed + the all-reduce of the bound
+    buffer inside ShardedStep)."""
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from collaborativefilteringusingtensorflow_amd.distributed import (make_gpu_sharded,
+                                                                       shard_users, local_csr)
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                                world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank,
+                                world_size=world)
+    ip, ix = fold["train_indptr"], fold["train_indices"]
+    u0, u1 = shard_users(ip, world, rank)
+    lip, lix = local_csr(ip, ix, u0, u1)
+    W = batches[0][1].shape[1]
+    e = Engine("amf", u1 - u0, 1682, U0.shape[1], n_neg=W, dense_item_apply=True, seed=10 + rank,
+               reg=0.05, reg_adv=1.0, epsilon=0.5, amf_mode="apr")
+    for k, v in (opts or {}).items():
+        e.set_option(k, v)
+    e.set_interactions(lip, lix)
+    e.begin_phase(1)
+    e.set_table("user", U0[u0:u1])
+    e.set_table("item", V0)
+    step, items = make_gpu_sharded(e, 1682, U0.shape[1], False, torch.device("cuda", 0), exchange=exchange)
+    for pairs, negs in batches:
+        mine = (pairs[:, 0] >= u0) & (pairs[:, 0] < u1)
+        lp = pairs[mine].copy()
+        lp[:, 0] -= u0
+        step(pairs=lp, negs=negs[mine])
+    step.sync_state()
+    torch.cuda.synchronize()
+    q.put((rank, u0, u1, e.get_table("user"), e.get_table("item"), e.get_table("acc_item")))
+    e.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _apr_oracle(batches, U0, V0):
+    from oracle import cf_oracle as O
+    U, V = U0.astype(np.float64), V0.astype(np.float64)
+    AU, AV = np.full_like(U, 0.1), np.full_like(V, 0.1)
+    for pairs, negs in batches:
+        O.amf_apr_step(U, V, AU, AV, pairs, negs, 0.05, 0.5, reg_adv=1.0)
+    return U, V, AU, AV
+
+
+def _apr_tables(seed, d=24):
+    from oracle import cf_oracle as O
+    rng = np.random.RandomState(seed)
+    return O.init_table(rng, (943, d)), O.init_table(rng, (1682, d))
+
+
+@pytest.mark.parametrize("item_reduce", [1, 0], ids=["reduce", "atomic"])
+def test_one_rank_rccl_apr(fold1, streams, item_reduce):
+    """AMF apr on the multi-rank code path over RCCL (world 1): the embed
+    pass, the all-reduce of the bound buffer, the gradient launch reading
+    every item row's Δ from it, the buffer cleared for the next step."""
+    U0, V0 = _apr_tables(21)
+    batches = [(streams["rank_b100_w5/pairs"][s], streams["rank_b100_w5/negs"][s]) for s in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_apr_worker, args=(0, 1, _free_port(), fold1, batches, U0, V0, q, "nccl",
+                                              "allreduce", {"item_reduce": item_reduce}))
+    p.start()
+    rank, u0, u1, Ul, Vr, AVr = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    U, V, AU, AV = _apr_oracle(batches, U0, V0)
+    _check_elementwise(Ul, U)
+    _check_elementwise(Vr, V)
+    _check_elementwise(AVr, AV)
+
+
+@pytest.mark.parametrize("exchange", ["allreduce", "rs_ag"])
+def test_two_rank_apr_equals_global_step(fold1, streams, exchange):
+    """Two ranks (gloo, one device): a row seen once on each rank is a
+    duplicate of the global batch, so its Δ must come from the summed
+    buffer -- every rank's tables equal the oracle's apr steps on the
+    concatenated batches."""
+    U0, V0 = _apr_tables(22)
+    batches = [(streams["rank_b100_w5/pairs"][s], streams["rank_b100_w5/negs"][s]) for s in range(8)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_apr_worker, args=(r, 2, port, fold1, batches, U0, V0, q, "gloo", exchange))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    U, V, AU, AV = _apr_oracle(batches, U0, V0)
+    for rank, u0, u1, Ul, Vr, AVr in res:
+        _check_elementwise(Ul, U[u0:u1])
+        _check_elementwise(Vr, V)
+        _check_elementwise(AVr, AV)
+    assert np.array_equal(res[0][4], res[1][4])
