@@ -272,7 +272,47 @@ __global__ void epoch_keys_kernel(PermKey p, PermInv v, int64_t nnz, int64_t n_u
     }
 }
 
+// sorted_batches 3: the same keys, with each pair's 16-B record as the
+// value (read in pair order: coalesced), so the sort leaves the records
+// themselves in batch-then-CSR order and the draw reads them sequentially
+__global__ void epoch_rec_keys_kernel(PermKey p, PermInv v, int64_t nnz, int64_t n_used, int B, int32_t nb,
+                                      const int4* __restrict__ pairs, int32_t* __restrict__ keys,
+                                      int4* __restrict__ recs) {
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = t0; q < nnz; q += nt) {
+        const uint64_t slot = perm_inverse((uint64_t)q, p, v);
+        keys[q] = slot < (uint64_t)n_used ? (int32_t)(slot / (uint64_t)B) : nb;
+        recs[q] = pairs[q];
+    }
+}
+
 }  // namespace
+
+size_t epoch_records_scratch(int64_t nnz, int32_t n_batches) {
+    size_t bytes = 0;
+    hipcub::DoubleBuffer<int32_t> k(nullptr, nullptr);
+    hipcub::DoubleBuffer<int4> v(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, k, v, (int)nnz, 0, key_bits((int64_t)n_batches + 1));
+    return bytes;
+}
+
+hipError_t launch_epoch_records(const PermKey& p, int64_t nnz, int B, const int4* pairs, int32_t* keys, int4* recs,
+                                void* tmp, size_t tmp_bytes, const int4** recs_out, hipStream_t s) {
+    if (nnz <= 0 || nnz > INT32_MAX || B <= 0) return hipErrorInvalidValue;
+    const int32_t nb = (int32_t)(nnz / B);
+    PermInv v{};
+    for (int r = 0; r < 3; ++r) v.mi[r] = perm_mul_inverse(p.m[r]);
+    hipLaunchKernelGGL(epoch_rec_keys_kernel, dim3(grid_of(nnz)), dim3(256), 0, s, p, v, nnz, (int64_t)nb * B, B,
+                       nb, pairs, keys, recs);
+    hipcub::DoubleBuffer<int32_t> dk(keys, keys + nnz);
+    hipcub::DoubleBuffer<int4> dv(recs, recs + nnz);
+    size_t bytes = tmp_bytes;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, bytes, dk, dv, (int)nnz, 0, key_bits((int64_t)nb + 1), s);
+    if (e != hipSuccess) return e;
+    *recs_out = dv.Current();
+    return hipGetLastError();
+}
 
 size_t epoch_order_scratch(int64_t nnz, int32_t n_batches) {
     size_t bytes = 0;

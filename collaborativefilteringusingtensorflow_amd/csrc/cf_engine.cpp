@@ -104,7 +104,10 @@ struct cf_engine {
     // atomics share lines) and its row scans stay local.  The batch SET is
     // the epoch bijection's, unchanged.  Two slots: the current epoch's order
     // and the next one's, computed ahead on eo_stream (StepArgs::order)
-    int sorted_batches = 2;   // 0 off, 1 on, 2 auto (kSortedAutoBatches batches per epoch and up)
+    // 0 off, 1 on, 2 auto (kSortedAutoBatches batches per epoch and up): the
+    // pair records sorted into batch-then-CSR order; 3 on, in the index form
+    // (order[] into pairs[]: a quarter of the memory, one more dependent load)
+    int sorted_batches = 2;
     struct EpochOrder {
         int32_t* keys = nullptr;     // [2 nnz]
         int32_t* vals = nullptr;     // [2 nnz]
@@ -114,6 +117,10 @@ struct cf_engine {
         int64_t epoch = -1;
         int B = 0;
         const int32_t* order = nullptr;
+        int4* recs = nullptr;        // sorted_batches 3: [2 nnz] records, sorted as the values
+        int64_t recs_cap = 0;
+        const int4* recs_sorted = nullptr;
+        bool with_recs = false;
         hipEvent_t ready = nullptr;
         bool async = false;          // computed on eo_stream: the engine stream waits on `ready`
     } eo[2];
@@ -745,26 +752,29 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
 constexpr int64_t kSortedAutoBatches = 16;
 bool sorted_batches_on(const cf_engine* e, int B) {
     if (e->sorted_batches == 0 || e->nnz > INT32_MAX || B < 1) return false;
-    return e->sorted_batches == 1 || e->nnz / B >= kSortedAutoBatches;
+    return e->sorted_batches == 1 || e->sorted_batches == 3 || e->nnz / B >= kSortedAutoBatches;
 }
 
 // the order of (epoch, B) in slot k, enqueued on stream st
 int compute_epoch_order(cf_engine* e, int k, int64_t epoch, int B, hipStream_t st) {
     cf_engine::EpochOrder& o = e->eo[k];
     const int64_t nnz = e->nnz;
+    const bool wr = e->sorted_batches != 3;   // the records form
     if (o.cap < nnz) {
         CF_HIP(hipDeviceSynchronize());
         dfree(o.keys);
         dfree(o.vals);
+        dfree(o.recs);
         if (o.tmp) (void)hipFree(o.tmp);
         o.tmp = nullptr;
         o.cap = 0;
+        o.recs_cap = 0;
         CF_TRY(dalloc(&o.keys, (size_t)(2 * nnz)));
-        CF_TRY(dalloc(&o.vals, (size_t)(2 * nnz)));
         o.cap = nnz;
         o.tmp_bytes = 0;
     }
-    const size_t need = epoch_order_scratch(nnz, (int32_t)(nnz / B));
+    if (!wr && !o.vals) CF_TRY(dalloc(&o.vals, (size_t)(2 * o.cap)));
+    const size_t need = wr ? epoch_records_scratch(nnz, (int32_t)(nnz / B)) : epoch_order_scratch(nnz, (int32_t)(nnz / B));
     if (need > o.tmp_bytes) {
         CF_HIP(hipDeviceSynchronize());
         if (o.tmp) (void)hipFree(o.tmp);
@@ -773,10 +783,24 @@ int compute_epoch_order(cf_engine* e, int k, int64_t epoch, int B, hipStream_t s
         if (he != hipSuccess) return fail(CF_ENOMEM, std::string("hipMalloc (epoch order scratch): ") + hipGetErrorString(he));
         o.tmp_bytes = need;
     }
+    if (wr && o.recs_cap < nnz) {
+        CF_HIP(hipDeviceSynchronize());
+        dfree(o.recs);
+        o.recs_cap = 0;
+        CF_TRY(dalloc(&o.recs, (size_t)(2 * nnz)));
+        o.recs_cap = nnz;
+    }
     const PermKey pk = make_perm_key((uint64_t)nnz, e->cfg.seed, (uint64_t)epoch);
     {
         ProfScope ps(e, CF_K_EPOCH_ORDER, st);
-        CF_HIP(launch_epoch_order(pk, nnz, B, o.keys, o.vals, o.tmp, o.tmp_bytes, &o.order, st));
+        if (wr) {
+            CF_HIP(launch_epoch_records(pk, nnz, B, e->pairs, o.keys, o.recs, o.tmp, o.tmp_bytes, &o.recs_sorted, st));
+            o.order = nullptr;
+        } else {
+            CF_HIP(launch_epoch_order(pk, nnz, B, o.keys, o.vals, o.tmp, o.tmp_bytes, &o.order, st));
+            o.recs_sorted = nullptr;
+        }
+        o.with_recs = wr;
     }
     o.epoch = epoch;
     o.B = B;
@@ -787,7 +811,7 @@ int compute_epoch_order(cf_engine* e, int k, int64_t epoch, int B, hipStream_t s
 
 // the order of the sampler's epoch at batch size B, ready on the engine
 // stream; the next epoch's is started on eo_stream
-int epoch_order(cf_engine* e, int B, const int32_t** out) {
+int epoch_order(cf_engine* e, int B, const int32_t** out, const int4** recs_out) {
     if (!e->eo_stream) {
         int lo = 0, hi = 0;
         CF_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -796,10 +820,12 @@ int epoch_order(cf_engine* e, int B, const int32_t** out) {
         for (auto& o : e->eo) CF_HIP(hipEventCreateWithFlags(&o.ready, hipEventDisableTiming));
     }
     const int64_t ep = e->epoch;
-    int k = (e->eo[0].epoch == ep && e->eo[0].B == B) ? 0 : (e->eo[1].epoch == ep && e->eo[1].B == B) ? 1 : -1;
+    const bool wr = e->sorted_batches != 3;
+    auto have = [&](const cf_engine::EpochOrder& o, int64_t epc) { return o.epoch == epc && o.B == B && o.with_recs == wr; };
+    int k = have(e->eo[0], ep) ? 0 : have(e->eo[1], ep) ? 1 : -1;
     if (k < 0) {
         // not computed ahead (first epoch, a jump, another B): in order on the engine stream
-        k = (e->eo[0].epoch == ep + 1 && e->eo[0].B == B) ? 1 : 0;
+        k = have(e->eo[0], ep + 1) ? 1 : 0;
         if (e->eo[k].async) CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
         // a draw on the side stream (prep_stream 1) may still read the slot
         CF_HIP(hipEventRecord(e->eo_mark, e->side));
@@ -810,8 +836,9 @@ int epoch_order(cf_engine* e, int B, const int32_t** out) {
         e->eo[k].async = false;
     }
     *out = e->eo[k].order;
+    *recs_out = e->eo[k].with_recs ? e->eo[k].recs_sorted : nullptr;
     cf_engine::EpochOrder& nx = e->eo[k ^ 1];
-    if (!(nx.epoch == ep + 1 && nx.B == B) && e->nnz / B >= 2) {
+    if (!have(nx, ep + 1) && e->nnz / B >= 2) {
         // the next epoch's order, behind everything the engine stream holds
         // so far (the kernels that still read this slot's previous epoch)
         // (and the side stream's draws, prep_stream 1: a wait takes the
@@ -851,8 +878,10 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
                                                      0x2545F4914F6CDD1Dull));
     if (sorted_batches_on(e, B)) {
         const int32_t* ord = nullptr;
-        CF_TRY(epoch_order(e, B, &ord));
+        const int4* recs = nullptr;
+        CF_TRY(epoch_order(e, B, &ord, &recs));
         a->order = ord;   // batch b's pairs at [bB, bB + B), CSR order
+        a->order_recs = recs;
     }
     e->batch += 1;
     return CF_OK;
@@ -1230,7 +1259,8 @@ int run_steps_device(cf_engine* e, int B, int n, double* loss_acc) {
     // records (StepArgs::pf_out); the draw of s+1 then reads them coalesced
     // (sorted batches read their records coalesced already: no prefetch)
     const bool pf = e->pair_prefetch && a.srec != nullptr && e->pipeline == 1 && !e->prep_side &&
-                    a.pos_set == nullptr && a.order == nullptr;
+                    a.pos_set == nullptr && a.order == nullptr &&
+                    a.order_recs == nullptr;
     if (pf && e->pf_cap < B) {
         CF_HIP(hipStreamSynchronize(e->stream));
         for (int q = 0; q < 2; ++q) {
@@ -1606,6 +1636,7 @@ int cf_destroy(cf_engine* e) {
     for (auto& o : e->eo) {
         dfree(o.keys);
         dfree(o.vals);
+        dfree(o.recs);
         if (o.tmp) (void)hipFree(o.tmp);
         if (o.ready) (void)hipEventDestroy(o.ready);
     }
@@ -1697,6 +1728,10 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
             if (k > rb && indices[k - 1] >= it) return fail(CF_EINVAL, "CSR rows must be sorted, unique");
         }
     }
+    // the sorted batches' cached epoch orders index the old pairs (and may
+    // exceed the new nnz): let an order in flight finish, then drop them
+    if (e->eo_stream) CF_HIP(hipStreamSynchronize(e->eo_stream));
+    for (auto& o : e->eo) o.epoch = -1;
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pos_set);
     CF_TRY(dalloc(&e->indptr, (size_t)c.n_users + 1));
@@ -2777,7 +2812,7 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         return CF_OK;
     }
     if (n == "sorted_batches") {   // each batch's pairs in CSR order (StepArgs::order)
-        if (value < 0 || value > 2) return fail(CF_EINVAL, "sorted_batches must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(CF_EINVAL, "sorted_batches must be 0, 1, 2 or 3");
         CF_TRY(discard_pending(e));
         e->sorted_batches = (int)value;
         return CF_OK;

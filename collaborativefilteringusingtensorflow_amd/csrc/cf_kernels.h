@@ -94,6 +94,9 @@ struct StepArgs {
     // batch set, its records read in ascending order, its users nearly
     // consecutive; null = off
     const int32_t* __restrict__ order;
+    // sorted_batches 3: the records themselves in that order (sorted with the
+    // keys as 16-B values), read sequentially by the draw; null = off
+    const int4* __restrict__ order_recs;
     // deterministic mode on the positive-sorted path (round 3):
     // every sum of gradient rows is taken in 64-bit fixed point (kFxOne
     // units), which is associative, so the result does not depend on the
@@ -396,8 +399,6 @@ hipError_t launch_prep(const StepArgs& a, hipStream_t s);   // sample/load + cou
 hipError_t launch_grad(const StepArgs& a, hipStream_t s, const StepArgs* next = nullptr);
 // AMF apr: the embedding-loss pass alone (cf_step_local_apr_embed)
 hipError_t launch_apr_embed(const StepArgs& a, hipStream_t s);
-// AMF apr: the embedding-loss pass alone (cf_step_local_apr_embed)
-hipError_t launch_apr_embed(const StepArgs& a, hipStream_t s);
 // the phased gradient kernel's compile-time W (1 or 5) a step takes, 0 = generic
 int grad_fast_w(const StepArgs& a);
 // the step takes grad_lds_kernel (LDS-staged negatives)
@@ -476,6 +477,11 @@ hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStre
 size_t epoch_order_scratch(int64_t nnz, int32_t n_batches);
 hipError_t launch_epoch_order(const PermKey& p, int64_t nnz, int B, int32_t* keys, int32_t* vals, void* tmp,
                               size_t tmp_bytes, const int32_t** order_out, hipStream_t s);
+// sorted_batches 3: the records instead (recs: 2 * nnz int4), *recs_out = the
+// epoch's pair records in that order
+size_t epoch_records_scratch(int64_t nnz, int32_t n_batches);
+hipError_t launch_epoch_records(const PermKey& p, int64_t nnz, int B, const int4* pairs, int32_t* keys, int4* recs,
+                                void* tmp, size_t tmp_bytes, const int4** recs_out, hipStream_t s);
 // a discarded draw's phantoms (StepArgs::spec_ph): uncount them, re-zero spec_n
 hipError_t launch_uncount_spec(const int2* ph, int* n, int32_t* cnt, hipStream_t s);
 // grad_sort_kernel carries the pair-record prefetch (StepArgs::pf_out)

@@ -584,6 +584,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         const int4 pr = make_int4((int)(slot % 1000000), (int)(slot % 100000), (int)((slot * 50) % 40000000), 50);
 #else
         const int4 pr = a.pre_pairs != nullptr ? a.pre_pairs[p]
+                      : a.order_recs != nullptr ? a.order_recs[slot]
                       : a.order != nullptr   ? a.pairs[a.order[slot]]
                                              : a.pairs[permute(slot, a.perm)];
 #endif
@@ -753,7 +754,8 @@ __device__ __forceinline__ void prep_lane_body(const StepArgs& a, int block) {
     uint64_t key = 0;
     if (a.sample) {
         const uint64_t slot = a.slot_base + (uint64_t)p;
-        const int4 pr = a.order != nullptr ? a.pairs[a.order[slot]]
+        const int4 pr = a.order_recs != nullptr ? a.order_recs[slot]
+                      : a.order != nullptr ? a.pairs[a.order[slot]]
                                            : a.pairs[permute(slot, a.perm)];   // sampler_ranking.py:24
         u = pr.x;
         i = pr.y;
@@ -885,7 +887,8 @@ __device__ __forceinline__ void prep_body_np(const StepArgs& a, int block) {
     for (int k = 0; k < NP; ++k) {
         const uint64_t slot = a.slot_base + (uint64_t)p[k];
         key[k] = mix64(a.rng_key ^ (slot * 0xD1B54A32D192ED03ull));
-        if (ok[k]) pr[k] = a.order != nullptr ? a.pairs[a.order[slot]]
+        if (ok[k]) pr[k] = a.order_recs != nullptr ? a.order_recs[slot]
+                         : a.order != nullptr ? a.pairs[a.order[slot]]
                                               : a.pairs[permute(slot, a.perm)];   // sampler_ranking.py:24
     }
     int maxchunk = 0;

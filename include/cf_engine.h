@@ -512,10 +512,13 @@ int cf_score_topk_ex(cf_engine* eng, const int32_t* host_users, int32_t n,
  *   "sorted_batches" the device sampler's batches read in pair (CSR) order:
  *                the same batch sets as the epoch bijection, each batch's
  *                pairs ascending, so the draw's records, user count atomics
- *                and row scans stay local.  The order of each epoch (inverse
- *                bijection keys + a radix sort by batch) is computed ahead
- *                on a low-priority stream.  0 off, 1 on, 2 auto (default:
- *                on when an epoch has >= 16 batches)
+ *                and row scans stay local.  Each epoch's pair records are
+ *                radix-sorted by batch (keys from the inverse bijection, the
+ *                16-B records as values) ahead, on a low-priority stream, and
+ *                the draw reads them sequentially.  0 off, 1 on, 2 auto
+ *                (default: on when an epoch has >= 16 batches), 3 on in the
+ *                index form (sorted pair indices into the records: a quarter
+ *                of the memory, one more dependent load in the draw)
  *   "neg_check"  how the device draw rejects a negative candidate in Pos(u):
  *                1 = probe an open-addressed set of the (u, i) pairs (16 B
  *                per interaction, built when selected; ~1 sector per
