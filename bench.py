@@ -123,6 +123,16 @@ def pmc_key(config, B, world, path_flags, exchange=None):
     return k + ("_" + exchange if exchange else "")
 
 
+def missing_orders(order_ms, n_in_region, steps, batches_per_epoch):
+    """Sorted batches: a timed region of `steps` steps owes
+    steps / batches_per_epoch epoch orders; the n_in_region computed inside
+    it are on its clock, the rest are charged at order_ms each.  No order
+    (sorted batches off at this batch size: order_ms 0) -> nothing owed."""
+    if order_ms <= 0 or batches_per_epoch <= 0:
+        return 0.0
+    return max(0.0, steps / float(batches_per_epoch) - n_in_region)
+
+
 def load_pmc(key):
     """HBM bytes per launch of the dominant kernel from the committed
     rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_summary.py) for
@@ -645,7 +655,7 @@ def main():
 
     def order_charge(ms_, n_in, steps, per_ep):
         """Orders (of the region's steps / per_ep share) not on the clock."""
-        miss = max(0.0, steps / per_ep - n_in) if ms_ > 0 else 0.0
+        miss = missing_orders(ms_, n_in, steps, per_ep)
         if world > 1:
             t = torch.tensor([miss], dtype=torch.float64, device="cuda:%d" % local_rank)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -60,3 +60,18 @@ def test_rank_count_mismatch_fails():
     r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, timeout=240,
                        universal_newlines=True)
     assert r.returncode != 0
+
+
+def test_epoch_order_charge():
+    """bench.py charges only the epoch orders a timed region owes but did not
+    compute on its clock (sorted batches)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.missing_orders(1.0, 2, 200, 95) == pytest.approx(200 / 95 - 2)   # 0.105 owed
+    assert b.missing_orders(1.0, 0, 100, 762) == pytest.approx(100 / 762)     # region inside one epoch
+    assert b.missing_orders(1.0, 3, 200, 95) == 0.0                           # an extra order: nothing owed
+    assert b.missing_orders(0.0, 0, 200, 95) == 0.0                           # sorted batches off
