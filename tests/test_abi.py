@@ -42,6 +42,19 @@ def test_defaults_follow_reference_constructors():
     assert abs(cfg.rho - 0.5) < 1e-6                                   # gbprmf.py:14
     assert abs(cfg.margin - 1.5) < 1e-6 and cfg.use_rank_weight == 1   # cml.py:16
     assert abs(cfg.reg_adv - 1.0) < 1e-6 and abs(cfg.epsilon - 0.5) < 1e-6  # amf.py:15
+    assert cfg.amf_mode == N.CF_AMF_REFERENCE   # what amf.py computes (Δ = 0)
+
+
+def test_amf_mode_names_and_rejections():
+    """amf_mode: the header's enum values, the drop-in's names, and the
+    class's ValueError before any device work (CPU)."""
+    with open(N.HEADER_PATH) as f:
+        text = f.read()
+    assert re.search(r"CF_AMF_REFERENCE\s*=\s*0", text) and re.search(r"CF_AMF_APR\s*=\s*1", text)
+    assert N.AMF_MODES == {"reference": 0, "apr": 1}
+    from collaborativefilteringusingtensorflow_amd.amf import AMF
+    with pytest.raises(ValueError):
+        AMF(10, 10, amf_mode="rand")
 
 
 def test_kernel_ids_match_header():
