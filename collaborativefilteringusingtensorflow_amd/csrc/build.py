@@ -22,7 +22,7 @@ LIB = os.path.join(OUT, "libcf_engine.so")
 # split lets the pool below compile the heavy instantiations in parallel
 SOURCES = ["cf_grad_bpr.hip", "cf_grad_amf.hip", "cf_grad_cml.hip", "cf_grad_gbpr.hip", "cf_grad_plr.hip",
            "cf_kernels.hip", "cf_eval.hip", "cf_engine.cpp", "cf_synth.cpp", "cf_ingest.cpp",
-           "cf_mt_sampler.cpp", "cf_ensemble.hip", "cf_det.hip"]
+           "cf_mt_sampler.cpp", "cf_ensemble.hip", "cf_det.hip", "cf_epoch.hip"]
 HEADERS = ["cf_kernels.h", "cf_device.h", "cf_kernels_impl.h", os.path.join(ROOT, "include", "cf_engine.h")]
 ARCH = os.environ.get("CF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -272,7 +272,7 @@ __global__ void epoch_keys_kernel(PermKey p, PermInv v, int64_t nnz, int64_t n_u
     }
 }
 
-// sorted_batches 3: the same keys, with each pair's 16-B record as the
+// the records form (sorted_batches 1 / 2): the same keys, with each pair's 16-B record as the
 // value (read in pair order: coalesced), so the sort leaves the records
 // themselves in batch-then-CSR order and the draw reads them sequentially
 __global__ void epoch_rec_keys_kernel(PermKey p, PermInv v, int64_t nnz, int64_t n_used, int B, int32_t nb,

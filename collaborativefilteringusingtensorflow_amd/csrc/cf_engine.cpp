@@ -108,17 +108,25 @@ struct cf_engine {
     // pair records sorted into batch-then-CSR order; 3 on, in the index form
     // (order[] into pairs[]: a quarter of the memory, one more dependent load)
     int sorted_batches = 2;
+    bool sorted_auto_off = false;   // auto, and the orders did not fit in HBM (sorted_auto_fits)
+    int64_t sorted_reserve_mb = 1024;
+    // cf_set_option("epoch_sort"): 0 the counting scatter (cf_epoch.hip) where
+    // it applies (<= kEpochMaxBins batches per epoch), 1 the hipCUB radix sort
+    int epoch_sort = 0;
+    // cf_set_option("user_runs"): sorted batches take user ranks / counts from
+    // the batch's user runs (StepArgs::user_runs), 0 = one count atomic per pair
+    int user_runs = 1;
     struct EpochOrder {
-        int32_t* keys = nullptr;     // [2 nnz]
-        int32_t* vals = nullptr;     // [2 nnz]
+        int32_t* keys = nullptr;     // radix-sort path: [2 nnz]
+        int32_t* vals = nullptr;     // index form: [nnz] (counting) or [2 nnz] (radix sort)
         void* tmp = nullptr;
         size_t tmp_bytes = 0;
-        int64_t cap = 0;
+        int64_t keys_cap = 0, vals_cap = 0;
         int64_t epoch = -1;
         int B = 0;
         const int32_t* order = nullptr;
-        int4* recs = nullptr;        // sorted_batches 3: [2 nnz] records, sorted as the values
-        int64_t recs_cap = 0;
+        int4* recs = nullptr;        // records form (sorted_batches 1 / 2): the sorted pair records
+        int64_t recs_cap = 0;        // elements, like keys_cap / vals_cap
         const int4* recs_sorted = nullptr;
         bool with_recs = false;
         hipEvent_t ready = nullptr;
@@ -752,7 +760,91 @@ StepArgs base_step_args(cf_engine* e, int B, int k) {
 constexpr int64_t kSortedAutoBatches = 16;
 bool sorted_batches_on(const cf_engine* e, int B) {
     if (e->sorted_batches == 0 || e->nnz > INT32_MAX || B < 1) return false;
+    if (e->sorted_batches == 2 && e->sorted_auto_off) return false;
     return e->sorted_batches == 1 || e->sorted_batches == 3 || e->nnz / B >= kSortedAutoBatches;
+}
+
+// the epoch order's buffers for (nnz, B) and the option values: the counting
+// scatter (cf_epoch.hip) writes the result once (records: int4[nnz], index
+// form: int32[nnz]) and takes a small histogram scratch; the radix sort
+// (more than kEpochMaxBins bins, or cf_set_option("epoch_sort", 1)) needs
+// keys int32[2 nnz] and double-buffered values
+struct EpochNeed {
+    bool counting;
+    int64_t keys, vals, recs;   // elements
+    size_t tmp;                 // bytes
+    double bytes() const { return 4.0 * (double)(keys + vals) + 16.0 * (double)recs + (double)tmp; }
+};
+EpochNeed epoch_need(const cf_engine* e, int B) {
+    const int64_t nnz = e->nnz;
+    const bool wr = e->sorted_batches != 3;   // the records form
+    EpochNeed n{};
+    n.counting = e->epoch_sort == 0 && epoch_count_ok(nnz, B);
+    if (n.counting) {
+        n.recs = wr ? nnz : 0;
+        n.vals = wr ? 0 : nnz;
+        n.tmp = epoch_count_scratch(nnz, B);
+    } else {
+        n.keys = 2 * nnz;
+        n.recs = wr ? 2 * nnz : 0;
+        n.vals = wr ? 0 : 2 * nnz;
+        n.tmp = wr ? epoch_records_scratch(nnz, (int32_t)(nnz / B)) : epoch_order_scratch(nnz, (int32_t)(nnz / B));
+    }
+    return n;
+}
+
+// auto mode only: the two order slots take 2 x epoch_need (32 B per
+// interaction in the default records form, 80 B on the radix-sort path).  An
+// engine whose tables leave less than that (and a 1 GiB reserve) free keeps
+// the unsorted batches -- the same batch sets, in permutation order --
+// instead of failing its first step with CF_ENOMEM (the reserve:
+// cf_set_option "sorted_auto_reserve_mb")
+void free_epoch_orders(cf_engine* e) {
+    (void)hipDeviceSynchronize();
+    for (auto& o : e->eo) {
+        dfree(o.keys);
+        dfree(o.vals);
+        dfree(o.recs);
+        if (o.tmp) (void)hipFree(o.tmp);
+        o.tmp = nullptr;
+        o.tmp_bytes = 0;
+        o.keys_cap = o.vals_cap = o.recs_cap = 0;
+        o.epoch = -1;
+        o.async = false;
+        o.order = nullptr;
+        o.recs_sorted = nullptr;
+    }
+}
+
+bool sorted_auto_fits(cf_engine* e, int B) {
+    const EpochNeed n = epoch_need(e, B);
+    double more = 0.0;   // what the two slots still have to allocate
+    for (const auto& o : e->eo) {
+        if (o.keys_cap < n.keys) more += 4.0 * (double)n.keys;
+        if (o.vals_cap < n.vals) more += 4.0 * (double)n.vals;
+        if (o.recs_cap < n.recs) more += 16.0 * (double)n.recs;
+        if (o.tmp_bytes < n.tmp) more += (double)n.tmp;
+    }
+    if (more == 0.0) return true;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;                            // unknown: the allocation decides
+    }
+    return (double)free_b >= more + (double)e->sorted_reserve_mb * (double)(1 << 20);
+}
+
+// grow one buffer of an order slot (the device is synchronised first: the
+// old buffer may still be read by a draw or written by the other stream)
+template <typename T>
+int grow(T** p, int64_t* cap, int64_t need) {
+    if (*cap >= need) return CF_OK;
+    CF_HIP(hipDeviceSynchronize());
+    dfree(*p);
+    *cap = 0;
+    CF_TRY(dalloc(p, (size_t)need));
+    *cap = need;
+    return CF_OK;
 }
 
 // the order of (epoch, B) in slot k, enqueued on stream st
@@ -760,40 +852,28 @@ int compute_epoch_order(cf_engine* e, int k, int64_t epoch, int B, hipStream_t s
     cf_engine::EpochOrder& o = e->eo[k];
     const int64_t nnz = e->nnz;
     const bool wr = e->sorted_batches != 3;   // the records form
-    if (o.cap < nnz) {
+    const EpochNeed n = epoch_need(e, B);
+    CF_TRY(grow(&o.keys, &o.keys_cap, n.keys));
+    CF_TRY(grow(&o.vals, &o.vals_cap, n.vals));
+    CF_TRY(grow(&o.recs, &o.recs_cap, n.recs));
+    if (n.tmp > o.tmp_bytes) {
         CF_HIP(hipDeviceSynchronize());
-        dfree(o.keys);
-        dfree(o.vals);
-        dfree(o.recs);
         if (o.tmp) (void)hipFree(o.tmp);
         o.tmp = nullptr;
-        o.cap = 0;
-        o.recs_cap = 0;
-        CF_TRY(dalloc(&o.keys, (size_t)(2 * nnz)));
-        o.cap = nnz;
         o.tmp_bytes = 0;
-    }
-    if (!wr && !o.vals) CF_TRY(dalloc(&o.vals, (size_t)(2 * o.cap)));
-    const size_t need = wr ? epoch_records_scratch(nnz, (int32_t)(nnz / B)) : epoch_order_scratch(nnz, (int32_t)(nnz / B));
-    if (need > o.tmp_bytes) {
-        CF_HIP(hipDeviceSynchronize());
-        if (o.tmp) (void)hipFree(o.tmp);
-        o.tmp = nullptr;
-        hipError_t he = hipMalloc(&o.tmp, need);
+        hipError_t he = hipMalloc(&o.tmp, n.tmp);
         if (he != hipSuccess) return fail(CF_ENOMEM, std::string("hipMalloc (epoch order scratch): ") + hipGetErrorString(he));
-        o.tmp_bytes = need;
-    }
-    if (wr && o.recs_cap < nnz) {
-        CF_HIP(hipDeviceSynchronize());
-        dfree(o.recs);
-        o.recs_cap = 0;
-        CF_TRY(dalloc(&o.recs, (size_t)(2 * nnz)));
-        o.recs_cap = nnz;
+        o.tmp_bytes = n.tmp;
     }
     const PermKey pk = make_perm_key((uint64_t)nnz, e->cfg.seed, (uint64_t)epoch);
     {
         ProfScope ps(e, CF_K_EPOCH_ORDER, st);
-        if (wr) {
+        if (n.counting) {
+            CF_HIP(launch_epoch_count(pk, nnz, B, wr ? e->pairs : nullptr, wr ? o.recs : nullptr,
+                                      wr ? nullptr : o.vals, o.tmp, o.tmp_bytes, st));
+            o.recs_sorted = wr ? o.recs : nullptr;
+            o.order = wr ? nullptr : o.vals;
+        } else if (wr) {
             CF_HIP(launch_epoch_records(pk, nnz, B, e->pairs, o.keys, o.recs, o.tmp, o.tmp_bytes, &o.recs_sorted, st));
             o.order = nullptr;
         } else {
@@ -831,8 +911,13 @@ int epoch_order(cf_engine* e, int B, const int32_t** out, const int4** recs_out)
         CF_HIP(hipEventRecord(e->eo_mark, e->side));
         CF_HIP(hipStreamWaitEvent(e->stream, e->eo_mark, 0));
         CF_TRY(compute_epoch_order(e, k, ep, B, e->stream));
+        // the draw that reads it may be launched on the side stream
+        // (prep_stream 1, cf_sample): that stream waits for the order too
+        CF_HIP(hipEventRecord(e->eo_mark, e->stream));
+        CF_HIP(hipStreamWaitEvent(e->side, e->eo_mark, 0));
     } else if (e->eo[k].async) {
         CF_HIP(hipStreamWaitEvent(e->stream, e->eo[k].ready, 0));
+        CF_HIP(hipStreamWaitEvent(e->side, e->eo[k].ready, 0));
         e->eo[k].async = false;
     }
     *out = e->eo[k].order;
@@ -876,12 +961,21 @@ int sampler_args(cf_engine* e, int B, StepArgs* a) {
     a->perm = make_perm_key((uint64_t)e->nnz, e->cfg.seed, (uint64_t)e->epoch);
     a->rng_key = mix64_host(e->cfg.seed ^ mix64_host((uint64_t)e->epoch * 0x9E3779B97F4A7C15ull +
                                                      0x2545F4914F6CDD1Dull));
+    if (sorted_batches_on(e, B) && e->sorted_batches == 2 && !sorted_auto_fits(e, B)) e->sorted_auto_off = true;
     if (sorted_batches_on(e, B)) {
         const int32_t* ord = nullptr;
         const int4* recs = nullptr;
-        CF_TRY(epoch_order(e, B, &ord, &recs));
-        a->order = ord;   // batch b's pairs at [bB, bB + B), CSR order
-        a->order_recs = recs;
+        const int rc = epoch_order(e, B, &ord, &recs);
+        if (rc == CF_ENOMEM && e->sorted_batches == 2) {
+            free_epoch_orders(e);   // auto: unsorted batches from here on
+            e->sorted_auto_off = true;
+        } else if (rc != CF_OK) {
+            return rc;
+        } else {
+            a->order = ord;   // batch b's pairs at [bB, bB + B), CSR order
+            a->order_recs = recs;
+            a->user_runs = e->user_runs && group_count(e->cfg) == 0 ? 1 : 0;
+        }
     }
     e->batch += 1;
     return CF_OK;
@@ -1324,13 +1418,16 @@ int check_fx(cf_engine* e) {
     const int n = std::min(e->fx_step, kFxSlots);
     e->fx_step = 0;
     if (n == 0) return CF_OK;
-    CF_HIP(hipMemcpyAsync(e->h_fx_bad, e->fx_bad, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, e->stream));
+    // every word: a step drawn ahead (or a split step) took its word when
+    // its arguments were built and may write one at or above n
+    CF_HIP(hipMemcpyAsync(e->h_fx_bad, e->fx_bad, (size_t)kFxSlots * sizeof(int), hipMemcpyDeviceToHost,
+                          e->stream));
     CF_HIP(hipStreamSynchronize(e->stream));
     int first = -1;
-    for (int q = 0; q < n && first < 0; ++q)
+    for (int q = 0; q < kFxSlots && first < 0; ++q)
         if (e->h_fx_bad[q] != 0) first = q;
     if (first < 0) return CF_OK;
-    CF_HIP(hipMemsetAsync(e->fx_bad, 0, (size_t)n * sizeof(int), e->stream));
+    CF_HIP(hipMemsetAsync(e->fx_bad, 0, (size_t)kFxSlots * sizeof(int), e->stream));
     const std::string at = first == kFxSlots - 1 ? "at or after step " + std::to_string(first)
                                                   : "at step " + std::to_string(first);
     return fail(CF_ENUMERIC, "deterministic mode: a gradient term was not finite or outside the "
@@ -1732,6 +1829,7 @@ int cf_set_interactions(cf_engine* e, const int64_t* indptr, const int32_t* indi
     // exceed the new nnz): let an order in flight finish, then drop them
     if (e->eo_stream) CF_HIP(hipStreamSynchronize(e->eo_stream));
     for (auto& o : e->eo) o.epoch = -1;
+    e->sorted_auto_off = false;   // sorted_auto_fits decides again for the new nnz
     dfree(e->indptr); dfree(e->indices); dfree(e->pairs); dfree(e->indptr_t); dfree(e->indices_t);
     dfree(e->pos_set);
     CF_TRY(dalloc(&e->indptr, (size_t)c.n_users + 1));
@@ -1937,7 +2035,10 @@ int cf_train_epoch(cf_engine* e, int32_t B, double* mean_loss_out) {
     CF_TRY(discard_pending(e));   // the sampler position a caller sees
     const int64_t per_epoch = e->nnz / B;
     int64_t left = per_epoch;
-    if (e->sampler_B == B && e->batch > 0 && e->batch < per_epoch) left = per_epoch - e->batch;
+    // sampler_args keeps the position when the batch size is this one, or
+    // not yet set (cf_set_sampler_state on a fresh engine)
+    if ((e->sampler_B == B || e->sampler_B == 0) && e->batch > 0 && e->batch < per_epoch)
+        left = per_epoch - e->batch;
     if (left > INT32_MAX) return fail(CF_EINVAL, "epoch too long for one call");
     double sum = 0.0;
     CF_TRY(cf_train_steps(e, B, (int32_t)left, mean_loss_out ? &sum : nullptr));
@@ -2815,6 +2916,28 @@ int cf_set_option(cf_engine* e, const char* name, int64_t value) {
         if (value < 0 || value > 3) return fail(CF_EINVAL, "sorted_batches must be 0, 1, 2 or 3");
         CF_TRY(discard_pending(e));
         e->sorted_batches = (int)value;
+        e->sorted_auto_off = false;
+        return CF_OK;
+    }
+    if (n == "user_runs") {   // StepArgs::user_runs
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "user_runs must be 0 or 1");
+        CF_TRY(discard_pending(e));
+        e->user_runs = (int)value;
+        return CF_OK;
+    }
+    if (n == "epoch_sort") {   // how the sorted batches' epoch order is formed (epoch_need)
+        if (value < 0 || value > 1) return fail(CF_EINVAL, "epoch_sort must be 0 or 1");
+        CF_TRY(discard_pending(e));
+        if (e->eo_stream) CF_HIP(hipStreamSynchronize(e->eo_stream));
+        e->epoch_sort = (int)value;
+        for (auto& o : e->eo) o.epoch = -1;   // recomputed in the new form
+        return CF_OK;
+    }
+    if (n == "sorted_auto_reserve_mb") {   // HBM auto mode leaves free beside the orders (sorted_auto_fits)
+        if (value < 0) return fail(CF_EINVAL, "sorted_auto_reserve_mb must be >= 0");
+        CF_TRY(discard_pending(e));
+        e->sorted_reserve_mb = value;
+        e->sorted_auto_off = false;
         return CF_OK;
     }
     if (n == "spec_neg") {   // speculative negative counts in the pos_sort draw (StepArgs::spec_ph)
@@ -2975,6 +3098,7 @@ int cf_step_path(cf_engine* e, int32_t B, int32_t* flags_out) {
     if (e->item_recs && (!c.dense_item_apply || e->item_reduce)) f |= CF_PATH_ITEM_RECORDS;
     if (e->det) f |= CF_PATH_DETERMINISTIC;
     if (c.dense_item_apply) f |= CF_PATH_DENSE_ITEMS;
+    if (e->pairs && sorted_batches_on(e, B)) f |= CF_PATH_SORTED_BATCHES;
     f |= (e->pipeline & 3) << 8;
     *flags_out = f;
     return CF_OK;

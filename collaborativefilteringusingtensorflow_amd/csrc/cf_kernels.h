@@ -94,9 +94,15 @@ struct StepArgs {
     // batch set, its records read in ascending order, its users nearly
     // consecutive; null = off
     const int32_t* __restrict__ order;
-    // sorted_batches 3: the records themselves in that order (sorted with the
-    // keys as 16-B values), read sequentially by the draw; null = off
+    // the records form (sorted_batches 1 / 2): the records themselves in
+    // that order, read sequentially by the draw; null = off (the index form,
+    // sorted_batches 3, sets only `order`)
     const int4* __restrict__ order_recs;
+    // sorted batches of a model without group users (cf_set_option
+    // "user_runs"): a user's occurrences are one run of consecutive pairs, so
+    // the draw takes user ranks and counts from the runs (prep_body) instead
+    // of one returning count atomic per pair
+    int user_runs;
     // deterministic mode on the positive-sorted path (round 3):
     // every sum of gradient rows is taken in 64-bit fixed point (kFxOne
     // units), which is associative, so the result does not depend on the
@@ -477,11 +483,22 @@ hipError_t launch_psort(const PsortArgs& a, void* tmp, size_t tmp_bytes, hipStre
 size_t epoch_order_scratch(int64_t nnz, int32_t n_batches);
 hipError_t launch_epoch_order(const PermKey& p, int64_t nnz, int B, int32_t* keys, int32_t* vals, void* tmp,
                               size_t tmp_bytes, const int32_t** order_out, hipStream_t s);
-// sorted_batches 3: the records instead (recs: 2 * nnz int4), *recs_out = the
-// epoch's pair records in that order
+// the records form (sorted_batches 1 / 2): the records instead (recs: 2 * nnz
+// int4), *recs_out = the epoch's pair records in that order
+// (both hipCUB radix sorts: the fallback above kEpochMaxBins bins and
+// cf_set_option("epoch_sort", 1); the default is launch_epoch_count)
 size_t epoch_records_scratch(int64_t nnz, int32_t n_batches);
 hipError_t launch_epoch_records(const PermKey& p, int64_t nnz, int B, const int4* pairs, int32_t* keys, int4* recs,
                                 void* tmp, size_t tmp_bytes, const int4** recs_out, hipStream_t s);
+// the same orders as one hand-written counting sort by batch id
+// (cf_epoch.hip), for nnz <= 2^31 and at most kEpochMaxBins = nnz / B + 1
+// bins: out_recs[nnz] (records form, pairs != null) or out_idx[nnz] (index
+// form), bitwise the stable radix sort's result
+constexpr int kEpochMaxBins = 1024;
+bool epoch_count_ok(int64_t nnz, int B);
+size_t epoch_count_scratch(int64_t nnz, int B);
+hipError_t launch_epoch_count(const PermKey& p, int64_t nnz, int B, const int4* pairs, int4* out_recs,
+                              int32_t* out_idx, void* tmp, size_t tmp_bytes, hipStream_t s);
 // a discarded draw's phantoms (StepArgs::spec_ph): uncount them, re-zero spec_n
 hipError_t launch_uncount_spec(const int2* ph, int* n, int32_t* cnt, hipStream_t s);
 // grad_sort_kernel carries the pair-record prefetch (StepArgs::pf_out)

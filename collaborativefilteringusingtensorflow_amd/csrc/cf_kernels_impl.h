@@ -597,6 +597,35 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         u = a.occU[p];
         i = a.occV[p];
     }
+    // sorted batches without group users (StepArgs::user_runs): the batch is
+    // in CSR order, so each user's occurrences are one run of consecutive
+    // pairs.  rank = the pair's place in its run, count = the run's length,
+    // stored plainly by the run's first pair -- no returning atomic.  The
+    // wave's first and last runs may continue in the neighbouring waves: they
+    // add their in-wave length with one atomic, whose return is the base of
+    // their ranks (two atomics per wave instead of one per pair; the
+    // neighbours' users come from the adjacent groups by shuffle, so nothing
+    // waits on another load -- a variant that loaded the wave's edge records
+    // to settle those two runs too measured 23 us slower per apply + draw
+    // launch at cfg2, profiles/r06/r06b)
+    const bool runs = a.user_runs != 0 && a.sample && a.count_users;   // wave-uniform
+    int run_rank = 0, run_len = 0, run_lead = 0, run_base = 0;
+    bool run_atomic = false;
+    if (runs) {
+        constexpr int GPW = kWave / PGL;
+        const int lane = threadIdx.x & 63, lead = lane & ~(PGL - 1), g = lane / PGL;
+        const int uprev = __shfl_up(u, PGL, kWave), unext = __shfl_down(u, PGL, kWave);
+        const bool head = g == 0 || uprev != u;
+        const bool tail = g == GPW - 1 || p + 1 >= B || unext != u;
+        const uint64_t H = __ballot(gl == 0 && head), T = __ballot(gl == 0 && tail);
+        const uint64_t hm = H & ((2ull << lead) - 1ull);    // heads at or before this pair (group 0's at least)
+        const uint64_t tm = T & ~((1ull << lead) - 1ull);   // tails at or after it (the last active group's at least)
+        run_lead = 63 - __clzll((long long)hm);
+        const int last = __ffsll((unsigned long long)tm) - 1;
+        run_rank = (lead - run_lead) / PGL;
+        run_len = (last - run_lead) / PGL + 1;
+        run_atomic = run_lead == 0 || last == (GPW - 1) * PGL;
+    }
     // the user's and the positive's returning count atomics need only the
     // record: issued first, they are in flight during the row scan (their
     // ranks are stored at the end).  pos_sort: the positive's rank among the
@@ -607,7 +636,14 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
 #else
     if (gl == 0) {
 #endif
-        if (a.count_users) rk_u = atomicAdd(&a.cntU[u], 1);
+        if (runs) {
+            if (run_rank == 0) {   // the run's first pair in this wave
+                if (run_atomic) run_base = atomicAdd(&a.cntU[u], run_len);
+                else a.cntU[u] = run_len;
+            }
+        } else if (a.count_users) {
+            rk_u = atomicAdd(&a.cntU[u], 1);
+        }
         if (a.count_items) rk_i = atomicAdd(a.cntP != nullptr ? &a.cntP[i] : &a.cntV[i], 1);
     }
     const bool spec = a.sample && a.spec_n != nullptr && a.count_items && a.pos_set == nullptr;
@@ -711,6 +747,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             if (a.count_users && g >= 0) a.rankU[B + p * G + k] = atomicAdd(&a.cntU[g], 1);
         }
     }
+    if (runs) rk_u = __shfl(run_base, run_lead, kWave) + run_rank;   // every lane: the run's base
     if (gl == 0) {
         if (a.sample) {
             a.occU[p] = u;

@@ -502,7 +502,7 @@ class Engine(object):
         return idx
 
     PATH_FLAGS = {"phased": 1, "pos_sort": 2, "item_records": 4, "deterministic": 8, "dense_items": 16,
-                  "lds": 32}
+                  "lds": 32, "sorted_batches": 64}
 
     def step_path(self, batch_size):
         """The kernel path a step of ``batch_size`` pairs takes now

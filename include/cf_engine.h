@@ -424,7 +424,9 @@ enum cf_path_flag {
     CF_PATH_ITEM_RECORDS = 4,   /* item records + user-row stash instead of slot rows      */
     CF_PATH_DETERMINISTIC = 8,  /* sort-based ranks, compact slots, no float atomics       */
     CF_PATH_DENSE_ITEMS = 16,   /* multi-rank item path (dense item gradient)              */
-    CF_PATH_LDS = 32            /* gradient kernel with LDS-staged negatives (grad_lds_kernel) */
+    CF_PATH_LDS = 32,           /* gradient kernel with LDS-staged negatives (grad_lds_kernel) */
+    CF_PATH_SORTED_BATCHES = 64 /* device-sampled batches in CSR order (option "sorted_batches";
+                                   auto turns off for good once the orders did not fit in HBM) */
 };
 int cf_step_path(cf_engine* eng, int32_t B, int32_t* flags_out);
 

@@ -131,11 +131,29 @@ def _dedup_adagrad_bounded(X, A, EX, EA, rows, grads, egrads, lr):
     return uniq
 
 
+def _no_nan(E):
+    """A bound carried over many steps can reach inf (see
+    _dedup_adagrad_bounded); a later product of it with an exact 0 (an
+    untouched row's E = 0) is NaN in IEEE arithmetic.  NaN compares false with
+    everything, so it would read as 'no bound' silently: make it inf, which is
+    sound (an upper bound) and which the tests count and limit
+    (tests/conftest.py assert_close(max_excluded=...), LocalStepCheck)."""
+    for t in E:
+        np.copyto(E[t], np.inf, where=np.isnan(E[t]))
+
+
 def bpr_step_bounded(U, V, AU, AV, E, pairs, negs, reg, lr=0.1, adversarial=None, reg_adv=1.0):
     """One BPRMF step (bprmf.py:52-88; = cf_oracle.bpr_step) or, with
     ``adversarial`` not None, one AMF step (amf.py:139-162; = amf_step), on the
     float64 tables in place, and E (dict over TABLES) advanced to bound the
     float32 result.  Returns the pre-update loss."""
+    with np.errstate(invalid="ignore", over="ignore"):
+        loss = _bpr_step_bounded(U, V, AU, AV, E, pairs, negs, reg, lr, adversarial, reg_adv)
+    _no_nan(E)
+    return loss
+
+
+def _bpr_step_bounded(U, V, AU, AV, E, pairs, negs, reg, lr, adversarial, reg_adv):
     pairs = np.asarray(pairs)
     Bn = pairs.shape[0]
     negs = np.asarray(negs).reshape(Bn, -1)
@@ -218,6 +236,16 @@ def _clip_bounded(X, EX, clip_norm):
 
 def cml_step_bounded(U, V, AU, AV, E, pairs, negs, margin, reg_cov, clip_norm,
                      use_rank_weight=True, lr=0.1, n_items=None):
+    """cml_step_bounded_ (below) with inf for NaN in E (_no_nan)."""
+    with np.errstate(invalid="ignore", over="ignore"):
+        loss = cml_step_bounded_(U, V, AU, AV, E, pairs, negs, margin, reg_cov, clip_norm,
+                                 use_rank_weight, lr, n_items)
+    _no_nan(E)
+    return loss
+
+
+def cml_step_bounded_(U, V, AU, AV, E, pairs, negs, margin, reg_cov, clip_norm,
+                      use_rank_weight=True, lr=0.1, n_items=None):
     """One CML step (cml.py:55-129; = cf_oracle.cml_step) on the float64 tables
     in place, and E advanced to bound the float32 result.
 

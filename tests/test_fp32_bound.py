@@ -243,3 +243,60 @@ def test_cml_bound_catches_one_occurrence_on_a_hot_row():
     # large summed G, then the clip), its accumulator G^2 does
     ratio = np.abs(T2[3][7].astype(np.float64) - L[3][7]) / E["acc_item"][7]
     assert ratio.max() > 3.0, ratio.max()
+
+
+def _fold_batches(fold1, rng, B, W, n):
+    """Uniform pairs of ml-100k fold 1 with W negatives outside Pos(u)."""
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    users = np.repeat(np.arange(len(ip) - 1), np.diff(ip))
+    out = []
+    for _ in range(n):
+        q = rng.choice(len(ix), B, replace=False)
+        negs = rng.randint(0, 1682, (B, W))
+        for r in range(B):
+            row = ix[ip[users[q[r]]]:ip[users[q[r]] + 1]]
+            while np.isin(negs[r], row).any():
+                negs[r] = rng.randint(0, 1682, W)
+        out.append((np.stack([users[q], ix[q]], 1).astype(np.int32), negs.astype(np.int32)))
+    return out
+
+
+def test_carried_bound_goes_inf_never_nan(fold1):
+    """The shape of round 5's cf_train_epoch trajectory check (d = 32,
+    B = 2048, W = 5, 21 steps): the bound carried over the epoch outgrows the
+    Zipf head's accumulators and reads inf on most elements.  It must never
+    read NaN (which compares false with everything, and raised a
+    RuntimeWarning), and conftest.assert_close must refuse to pass the
+    unbounded elements silently -- it fails unless the caller allows and
+    counts them (max_excluded)."""
+    import warnings
+    from conftest import assert_close
+    rng = np.random.RandomState(9)
+    T = [t.astype(np.float64) for t in tabs(rng, 943, 1682, 32)]
+    E = FB.zero_bounds(T[0], T[1], acc_exact=True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")   # a RuntimeWarning from the bound fails the test
+        for pairs, negs in _fold_batches(fold1, rng, 2048, 5, 21):
+            FB.bpr_step_bounded(*T, E, pairs, negs, 0.05)
+    assert not any(np.isnan(E[k]).any() for k in FB.TABLES)
+    frac = (~np.isfinite(E["item"])).mean()
+    assert frac > 0.5, frac               # the carried bound checks (almost) nothing here
+    with pytest.raises(AssertionError, match="non-finite a-priori bound"):
+        assert_close(T[1], T[1], "item", bound=E["item"])
+    with pytest.raises(AssertionError, match="non-finite a-priori bound"):
+        assert_close(T[1], T[1], "item", bound=E["item"], max_excluded=0.01)
+    assert_close(T[1], T[1], "item", bound=E["item"], max_excluded=1.0)   # allowed and counted
+
+
+def test_one_step_bound_is_finite_everywhere(fold1):
+    """The per-step check (conftest.LocalStepCheck) needs a finite E on every
+    element: one step from any tables, at that same shape, gives one."""
+    rng = np.random.RandomState(10)
+    T = [t.astype(np.float64) for t in tabs(rng, 943, 1682, 32)]
+    batches = _fold_batches(fold1, rng, 2048, 5, 6)
+    for pairs, negs in batches:
+        O.bpr_step(*T, pairs, negs, 0.05)          # move the tables off their init
+    for pairs, negs in batches[:2]:
+        E = FB.zero_bounds(T[0], T[1], acc_exact=True)
+        FB.bpr_step_bounded(*[t.copy() for t in T], E, pairs, negs, 0.05)
+        assert all(np.isfinite(E[k]).all() for k in FB.TABLES)

@@ -1,12 +1,11 @@
 """GPU checks of the SURVEY 8(b) entry points added in round 5: cf_train_epoch
-(one iteration of the reference's train loop, bprmf.py:138-150) against the
-float64 oracle's epoch mean loss on the identical batch stream, and
+(one iteration of the reference's train loop, bprmf.py:138-150), bitwise
+against single steps each checked against the float64 oracle, and
 cf_set_params / cf_get_params (every table in one call, NULL = keep)."""
 import numpy as np
 import pytest
 
-from conftest import assert_close
-from oracle import cf_oracle as O
+from conftest import LocalStepCheck
 
 pytestmark = pytest.mark.gpu
 
@@ -19,41 +18,75 @@ def _engine(fold1, seed=17, d=32, W=1, **kw):
     return e
 
 
+TABLES = ("user", "item", "acc_user", "acc_item")
+
+
 @pytest.mark.parametrize("B,W", [(4096, 1), (2048, 5)])
 def test_train_epoch_matches_oracle_mean_loss(fold1, B, W):
     """cf_train_epoch = n_batches = int(nnz / B) device-sampled steps and the
-    mean of their pre-update losses (the reference's TraLoss).  A second
-    engine with the same seed draws the same stream with cf_sample; the
-    float64 oracle steps those batches from the same initial tables.  The
-    tables after the epoch are checked in the strict band plus the a-priori
-    fp32 bound carried over the epoch (oracle/fp32_bound.py: ml-100k's head
-    items sum hundreds of occurrences per step)."""
-    from oracle import fp32_bound as FB
+    mean of their pre-update losses (the reference's TraLoss,
+    bprmf.py:138-150).  In deterministic mode (order-free fixed-point sums)
+    the epoch call is BITWISE the same model as n_batches single steps
+    cf_train_steps(B, 1) of a second engine from the same state and sampler
+    seed; each of those steps is checked against the float64 oracle from that
+    engine's own pre-step tables, every element of every table within the
+    a-priori fp32 bound (conftest.LocalStepCheck: a one-step bound is finite
+    everywhere, so nothing goes unchecked), and the epoch's mean loss against
+    the mean of the checked step losses."""
     nnz = int(fold1["train_indices"].shape[0])
     n_batches = nnz // B
     e = _engine(fold1, W=W)
-    T0 = {t: e.get_table(t).astype(np.float64) for t in ("user", "item", "acc_user", "acc_item")}
+    f = _engine(fold1, W=W)
+    for x in (e, f):
+        x.set_option("deterministic", 1)
+    assert all(np.array_equal(e.get_table(t), f.get_table(t)) for t in TABLES)
     mean = e.train_epoch(B)
     assert e.sampler_state() in ((0, n_batches), (1, 0))   # ends at the epoch boundary
-    f = _engine(fold1, W=W)
-    batches = [f.sample(B)[:2] for _ in range(n_batches)]
+    chk = LocalStepCheck(0.05)
+    losses = []
+    for s in range(n_batches):
+        st = f.sampler_state()
+        pairs, negs, _ = f.sample(B)         # the batch the next step draws
+        f.set_sampler_state(*st)
+        chk.before(f)
+        loss = f.train_steps(B, 1)
+        chk.after(f, pairs, negs, loss, "step %d" % s)
+        losses.append(loss)
+    assert chk.excluded == 0
+    for t in TABLES:
+        assert np.array_equal(e.get_table(t), f.get_table(t)), t
+    assert abs(mean - np.mean(losses)) <= 1e-12 * abs(np.mean(losses)), (mean, np.mean(losses))
     f.close()
-    U, V, AU, AV = T0["user"], T0["item"], T0["acc_user"], T0["acc_item"]
-    E = FB.zero_bounds(U, V, acc_exact=True)
-    losses = [FB.bpr_step_bounded(U, V, AU, AV, E, p, n, 0.05) for p, n in batches]
-    assert abs(mean - np.mean(losses)) <= 1e-5 * abs(np.mean(losses)), (mean, np.mean(losses))
-    for t, o in (("user", U), ("item", V), ("acc_user", AU), ("acc_item", AV)):
-        assert_close(e.get_table(t), o, t, bound=E[t])
-    # the next call is a whole epoch again; from inside an epoch, its rest
+    e.close()
+    # (fast path) the next call is a whole epoch again; from inside an epoch, its rest
+    e = _engine(fold1, W=W)
+    e.train_epoch(B)
     e.train_epoch(B)
     e.train_steps(B, 3)
-    ep, bt = e.sampler_state()
     e.profile_reset()
     e.profile(True)
     e.train_epoch(B)
     e.profile(False)
     steps = e.profile_read("apply_prep")[1] + e.profile_read("apply")[1]
     assert steps == n_batches - 3, (steps, n_batches)
+    e.close()
+
+
+def test_train_epoch_after_state_jump_on_fresh_engine(fold1):
+    """cf_set_sampler_state(epoch, b > 0) on an engine that has not drawn yet:
+    cf_train_epoch runs the epoch's remaining batches and stops at its end
+    (the position is kept, as sampler_args keeps it)."""
+    B = 4096
+    n_batches = int(fold1["train_indices"].shape[0]) // B
+    e = _engine(fold1)
+    e.set_sampler_state(2, 4)
+    e.profile_reset()
+    e.profile(True)
+    e.train_epoch(B)
+    e.profile(False)
+    steps = e.profile_read("apply_prep")[1] + e.profile_read("apply")[1]
+    assert steps == n_batches - 4, (steps, n_batches)
+    assert e.sampler_state() in ((2, n_batches), (3, 0))
     e.close()
 
 

@@ -28,16 +28,19 @@ TABLES = ("user", "item", "acc_user", "acc_item")
 HP = {"bpr": dict(reg=0.02), "amf": dict(reg=0.05, reg_adv=1.0)}
 
 
-def assert_close(got, ref, name, rtol=1e-5, atol=1e-6, bound=None):
+def assert_close(got, ref, name, rtol=1e-5, atol=1e-6, bound=None, max_excluded=0.0):
     """Elementwise |got - ref| <= atol + rtol |ref| (+ the carried a-priori
-    fp32 bound where given)."""
-    return _assert_close(got, ref, name, rtol=rtol, atol=atol, bound=bound)
+    fp32 bound where given; non-finite bounds only up to ``max_excluded``)."""
+    return _assert_close(got, ref, name, rtol=rtol, atol=atol, bound=bound, max_excluded=max_excluded)
 
 
 def _host_fed(e, B, n, ni, reg=0.02):
     """n host-fed steps on device-drawn batches: each step checked locally
-    (conftest.LocalStepCheck), the trajectory against the float64 oracle
-    within the strict band plus the carried a-priori bound."""
+    (conftest.LocalStepCheck, every element), the trajectory against the
+    float64 oracle within the strict band plus the carried a-priori bound --
+    finite on all but a few Zipf-head item elements after 3-4 steps (a CPU
+    replay of these shapes: 0 of 128,000 at B = 8192 x 4, 4 of 256,000 at
+    B = 32768 x 3), so at most 1 % may go unchecked (asserted)."""
     from oracle import fp32_bound as FB
     T = {t: e.get_table(t).astype(np.float64) for t in TABLES}
     E = FB.zero_bounds(T["user"], T["item"], acc_exact=True)
@@ -53,7 +56,7 @@ def _host_fed(e, B, n, ni, reg=0.02):
         lo = FB.bpr_step_bounded(T["user"], T["item"], T["acc_user"], T["acc_item"], E, pairs, negs, reg)
         assert abs(lg - lo) <= 1e-5 * abs(lo), (lg, lo)
     for t in TABLES:
-        assert_close(e.get_table(t), T[t], t, bound=E[t])
+        assert_close(e.get_table(t), T[t], t, bound=E[t], max_excluded=0.01)
     return hot, hot_user
 
 
@@ -168,3 +171,34 @@ def test_det_fixed_point_range_guard(skewed_graph, how):
     assert not np.isfinite(f.get_table("item")[:200]).all() or how == "huge"
     e.close()
     f.close()
+
+
+@pytest.mark.parametrize("B,W", [(1 << 17, 1), (16384, 5)])
+def test_user_runs_equal_atomic_ranks(skewed_graph, B, W):
+    """Sorted batches take each user's rank and count from the batch's runs
+    of consecutive pairs (StepArgs::user_runs) -- a plain store per run, one
+    atomic per wave only for a run crossing into another wave -- instead of
+    one returning count atomic per pair.  The ranks are a different
+    permutation, so in deterministic mode (order-free fixed-point sums) the
+    training must be BITWISE the same with user_runs on and off; at
+    B = 2^17 on 40K users a batch has ~3.3 pairs per user, so many runs cross
+    the 16-pair wave boundaries.  The fast path trains the same model up to
+    fp32 summation order."""
+    out = {}
+    for det in (1, 0):
+        for ur in (0, 1):
+            e = _engine("bpr", skewed_graph, 32, W, det=bool(det), seed=43)
+            e.set_option("user_runs", ur)
+            e.set_option("sorted_batches", 1)
+            assert e.step_path(B)[1]["sorted_batches"]
+            loss = e.train_steps(B, 5)
+            out[det, ur] = (loss, {t: e.get_table(t) for t in TABLES})
+            e.close()
+    (l0, T0), (l1, T1) = out[1, 0], out[1, 1]
+    assert l0 == l1
+    for t in TABLES:
+        assert np.array_equal(T0[t], T1[t]), t
+    (l0, T0), (l1, T1) = out[0, 0], out[0, 1]
+    assert abs(l1 - l0) <= 1e-5 * abs(l0)
+    for t in TABLES:
+        assert_close(T1[t], T0[t].astype(np.float64), t, rtol=1e-4, atol=1e-6)

@@ -236,8 +236,18 @@ def test_pos_sort_auto_by_batch_size():
     on a 60K x 8K Zipf(0.8) graph the auto path (psort + partial rows, hot
     items past capP on float atomics) is checked against the float64 oracle
     replaying the engine's own draws -- the test through which the round-2
-    owner race (a duplicated item applied twice) surfaced."""
+    owner race (a duplicated item applied twice) surfaced:
+
+    * K single device-drawn steps, each from the engine's own pre-step tables
+      within the one-step a-priori fp32 bound (conftest.LocalStepCheck: every
+      element of every table, none excluded);
+    * one two-step cf_train_steps call (the apply launch of step 1 draws and
+      counts step 2) within the bound carried over its two steps, which stays
+      finite on all but a handful of elements (asserted: <= 1 %; over three
+      or more steps the carried accumulator bound outgrows the accumulators of
+      the Zipf head and reads inf)."""
     from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+    from oracle import fp32_bound as FB
     nu, ni, d, reg = 60_000, 8_000, 64, 0.02
     ip, ix = synth_graph(nu, ni, 30.0, 0.8, 7, n_threads=8)
     e = Engine("bpr", nu, ni, d, n_neg=1, reg=reg, seed=3)
@@ -252,32 +262,36 @@ def test_pos_sort_auto_by_batch_size():
     # size changes, and (epoch, batch) alone does not restore that
     e.train_steps(B, 1)
     n_small += 1
+    chk = LocalStepCheck(reg)
+    for s in range(K):
+        st = e.sampler_state()
+        pairs, negs, _ = e.sample(B)     # the batch the next step draws
+        e.set_sampler_state(*st)
+        chk.before(e)
+        loss = e.train_steps(B, 1)
+        chk.after(e, pairs, negs, loss, "step %d" % s)
+        if s == 0:   # the batches really overflow capP (8 partials) on their hottest positives
+            cnt = np.bincount(pairs[:, 1], minlength=ni)
+            off = np.cumsum(cnt) - cnt
+            nparts = np.where(cnt > 0, (off + cnt - 1) // 16 - off // 16 + 1, 0)
+            assert nparts.max() > 8, nparts.max()
+    assert chk.excluded == 0
+    # two pipelined steps in one call
     T = {t: e.get_table(t).astype(np.float64) for t in ("user", "item", "acc_user", "acc_item")}
     st = e.sampler_state()
-    batches = [e.sample(B)[:2] for _ in range(K)]
+    batches = [e.sample(B)[:2] for _ in range(2)]
     e.set_sampler_state(*st)
-    loss = e.train_steps(B, K)
+    loss = e.train_steps(B, 2)
     e.profile(False)
     n_big = psort_launches(e) - n_small
-    assert n_small == 1 and n_big == K
-    # the strict band plus the a-priori fp32 bound carried over the K steps
-    # (oracle/fp32_bound.py): 8K Zipf items at 2^18 pairs put
-    # thousands of occurrences on the head rows, whose fp32 sums leave the
-    # strict band in some summation orders (round 4: acc_item at 1.011x of it,
-    # profiles/r04/red_runs/)
-    from oracle import fp32_bound as FB
+    assert n_small == 1 and n_big == K + 2
     E = FB.zero_bounds(T["user"], T["item"], acc_exact=True)
     lo = 0.0
     for pairs, negs in batches:
         lo += FB.bpr_step_bounded(T["user"], T["item"], T["acc_user"], T["acc_item"], E, pairs, negs, reg)
     assert abs(loss - lo) <= RTOL * abs(lo), (loss, lo)
-    # the batches really overflow capP (8 partials) on their hottest positives
-    cnt = np.bincount(batches[0][0][:, 1], minlength=ni)
-    off = np.cumsum(cnt) - cnt
-    nparts = np.where(cnt > 0, (off + cnt - 1) // 16 - off // 16 + 1, 0)
-    assert nparts.max() > 8, nparts.max()
     for t in T:
-        assert_close(e.get_table(t), T[t], t, bound=E[t])
+        assert_close(e.get_table(t), T[t], t, bound=E[t], max_excluded=0.01)
     e.close()
 
 

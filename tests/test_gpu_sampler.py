@@ -116,6 +116,114 @@ def test_sorted_batches_with_records_equal_order_only(fold1, B):
         assert np.array_equal(p1, p3) and np.array_equal(n1, n3), b
 
 
+@pytest.mark.parametrize("sb", [1, 3], ids=["records", "index"])
+@pytest.mark.parametrize("B", [20, 100, 997, 4096])
+def test_epoch_counting_scatter_equals_radix_sort(fold1, sb, B):
+    """The hand-written counting scatter that forms each epoch's order
+    (cf_epoch.hip, cf_set_option("epoch_sort", 0), the default) gives the same
+    batches as the stable radix sort it replaced (epoch_sort 1): bitwise the
+    same pairs and negatives over two epochs, in both the records and the
+    index form.  B = 20 has 2,213 batches per epoch, past kEpochMaxBins
+    (1,024): both settings take the radix sort there."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    per_epoch = len(ix) // B
+    n = 2 * per_epoch + 3 if B >= 100 else 40
+    out = []
+    for es in (0, 1):
+        e = Engine("bpr", nu, ni, 8, n_neg=2, seed=36)
+        e.set_option("sorted_batches", sb)
+        e.set_option("epoch_sort", es)
+        e.set_interactions(ip, ix)
+        got = [e.sample(B)[:2] for _ in range(n)]
+        if B < 100:   # the end of the epoch and the next one's start
+            e.set_sampler_state(0, per_epoch - 3)
+            got += [e.sample(B)[:2] for _ in range(6)]
+        out.append(got)
+        e.close()
+    for b, ((p0, n0), (p1, n1)) in enumerate(zip(*out)):
+        assert np.array_equal(p0, p1) and np.array_equal(n0, n1), b
+
+
+@pytest.mark.parametrize("B", [1 << 16, 1 << 19, 3000])
+def test_epoch_counting_scatter_large(B):
+    """The same equality on a 2M-pair Zipf graph (the bijection's domain not a
+    power of two, cycle walking on; 30 / 3 / 666 batches per epoch): the first
+    batches, the last whole batch of the epoch and the first of the next."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+    nu, ni = 70_000, 9_000
+    ip, ix = synth_graph(nu, ni, 30.0, 0.8, 11, n_threads=8)
+    per_epoch = len(ix) // B
+    out = []
+    for es in (0, 1):
+        e = Engine("bpr", nu, ni, 8, n_neg=1, seed=37)
+        e.set_option("sorted_batches", 1)
+        e.set_option("epoch_sort", es)
+        e.set_interactions(ip, ix)
+        got = [e.sample(B)[0] for _ in range(2)]
+        e.set_sampler_state(0, per_epoch - 1)
+        got += [e.sample(B)[0] for _ in range(2)]
+        out.append(got)
+        e.close()
+    for b, (p0, p1) in enumerate(zip(*out)):
+        assert np.array_equal(p0, p1), b
+        k = p0[:, 0].astype(np.int64) * ni + p0[:, 1]
+        assert (np.diff(k) > 0).all(), b                     # CSR order inside the batch
+
+
+@pytest.mark.parametrize("jump", [False, True], ids=["fresh", "state-jump"])
+def test_side_stream_draw_waits_for_epoch_order(fold1, jump):
+    """prep_stream 1 draws on the side stream; an epoch order computed in line
+    on the engine stream (the first epoch, a cf_set_sampler_state jump, a new
+    B) must be complete before that draw reads it.  The side-stream engine's
+    batches equal the main-stream engine's, from a fresh engine and after a
+    jump, on a graph big enough that the order takes a while."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine, synth_graph
+    nu, ni = 200_000, 20_000
+    ip, ix = synth_graph(nu, ni, 25.0, 0.8, 13, n_threads=8)
+    B = 1 << 16
+    out = []
+    for side in (0, 1):
+        e = Engine("bpr", nu, ni, 8, n_neg=1, seed=38)
+        e.set_option("prep_stream", side)
+        e.set_option("pipeline", 0)
+        e.set_interactions(ip, ix)
+        if jump:
+            e.train_steps(B, 2)
+            e.set_sampler_state(5, 7)
+        got = [e.sample(B)[:2] for _ in range(3)]
+        out.append(got)
+        e.close()
+    for b, ((p0, n0), (p1, n1)) in enumerate(zip(*out)):
+        assert np.array_equal(p0, p1) and np.array_equal(n0, n1), b
+
+
+def test_sorted_auto_falls_back_when_orders_do_not_fit(fold1):
+    """Auto sorted batches need 2 x 16 B per pair for the two epoch orders;
+    when HBM does not hold them beside the reserve (here: a reserve larger than
+    any GPU), the engine keeps the unsorted batches -- the same batch sets --
+    instead of failing with CF_ENOMEM, and cf_step_path reports it."""
+    from collaborativefilteringusingtensorflow_amd.engine import Engine
+    nu, ni = int(fold1["n_users"]), int(fold1["n_items"])
+    ip, ix = fold1["train_indptr"], fold1["train_indices"]
+    B = 1000
+    out = []
+    for reserve in (1024, 1 << 30):
+        e = Engine("bpr", nu, ni, 8, n_neg=1, seed=39)
+        e.set_option("sorted_auto_reserve_mb", reserve)
+        e.set_interactions(ip, ix)
+        e.train_steps(B, 3)
+        assert e.step_path(B)[1]["sorted_batches"] == (reserve == 1024), reserve
+        out.append([e.sample(B)[0] for _ in range(4)])
+        e.close()
+    for b, (srt, plain) in enumerate(zip(*out)):
+        ks = srt[:, 0].astype(np.int64) * ni + srt[:, 1]
+        kp = plain[:, 0].astype(np.int64) * ni + plain[:, 1]
+        assert (np.diff(ks) > 0).all() and not (np.diff(kp) > 0).all(), b
+        assert np.array_equal(np.sort(kp), ks), b
+
+
 @pytest.mark.parametrize("sb", [1, 3])
 def test_sorted_batches_new_interactions_drop_cached_orders(fold1, sb):
     """A second cf_set_interactions (a smaller graph) must not reuse the
