@@ -36,7 +36,10 @@ namespace cfk {
 
 namespace {
 
-constexpr int kEpochTile = 2048;                  // consecutive pairs per block
+#ifndef CF_EPOCH_TILE
+#define CF_EPOCH_TILE 2048
+#endif
+constexpr int kEpochTile = CF_EPOCH_TILE;         // consecutive pairs per block
 constexpr int kEpochItems = kEpochTile / kBlock;  // 8 per thread
 constexpr int kEpochWaveSpan = kEpochTile / kWavesPerBlock;   // 512 consecutive pairs per wave (scatter)
 constexpr int kEpochChunkTiles = 32;              // tiles per chunk of the column scan

@@ -636,10 +636,17 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
 #else
     if (gl == 0) {
 #endif
-        if (runs) {
+#ifndef CF_RUNS_MODE
+#define CF_RUNS_MODE 0   // experiments: 1 = the interior runs' count as a non-returning atomic, 2 = runs unused
+#endif
+        if (runs && CF_RUNS_MODE != 2) {
             if (run_rank == 0) {   // the run's first pair in this wave
                 if (run_atomic) run_base = atomicAdd(&a.cntU[u], run_len);
+#if CF_RUNS_MODE == 1
+                else (void)atomicAdd(&a.cntU[u], run_len);
+#else
                 else a.cntU[u] = run_len;
+#endif
             }
         } else if (a.count_users) {
             rk_u = atomicAdd(&a.cntU[u], 1);
@@ -747,7 +754,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             if (a.count_users && g >= 0) a.rankU[B + p * G + k] = atomicAdd(&a.cntU[g], 1);
         }
     }
-    if (runs) rk_u = __shfl(run_base, run_lead, kWave) + run_rank;   // every lane: the run's base
+    if (runs && CF_RUNS_MODE != 2) rk_u = __shfl(run_base, run_lead, kWave) + run_rank;   // every lane: the run's base
     if (gl == 0) {
         if (a.sample) {
             a.occU[p] = u;

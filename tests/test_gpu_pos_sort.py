@@ -345,6 +345,38 @@ def test_spec_neg_steps_match_oracle(fold1, model, W):
     e.close()
 
 
+def test_cml_spec_neg_on_and_off_each_match_oracle(fold1):
+    """CML with speculative negative counts on and off (round 5 dropped CML
+    from test_spec_neg_equals_plain_draw after its fast-path case put 6 user
+    elements at 4.4x the CML trajectory band, profiles/r05/r05a/pytest.log;
+    DESIGN 4.1).  Two fp32 runs whose duplicate sums add in different orders
+    drift apart through CML's branch points (hinge, argmin, the rank weight's
+    indicators), so a band between the two runs is not a sound check.  What
+    must hold is that both settings draw the same batches and that every step
+    of each is the float64 oracle's step from that engine's own tables within
+    the a-priori bound (conftest.LocalStepCheck, ambiguous pairs excluded and
+    counted) -- a phantom occurrence that leaked into a count, a slot row or a
+    clip would land outside it."""
+    kw = SPEC_MODELS["cml"]
+    drawn = []
+    for spec in (0, 1):
+        e = _spec_engine(fold1, "cml", 1, spec, 0)
+        chk = LocalStepCheck(model="cml", use_rank_weight=True, **kw)
+        got = []
+        for s in range(12):
+            st = e.sampler_state()
+            pairs, negs, _ = e.sample(2048)
+            e.set_sampler_state(*st)
+            chk.before(e)
+            loss = e.train_steps(2048, 1)
+            chk.after(e, pairs, negs, loss, "spec %d step %d" % (spec, s))
+            got.append((pairs, negs))
+        drawn.append(got)
+        e.close()
+    for s, ((p0, n0), (p1, n1)) in enumerate(zip(*drawn)):
+        assert np.array_equal(p0, p1) and np.array_equal(n0, n1), s
+
+
 @pytest.mark.parametrize("det", [0, 1], ids=["fast", "det"])
 @pytest.mark.parametrize("model,W", [("bpr", 1), ("bpr", 5), ("amf", 1), ("amf", 5)])
 def test_spec_neg_equals_plain_draw(fold1, model, W, det):
