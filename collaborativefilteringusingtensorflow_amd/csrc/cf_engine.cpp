@@ -114,8 +114,9 @@ struct cf_engine {
     // it applies (<= kEpochMaxBins batches per epoch), 1 the hipCUB radix sort
     int epoch_sort = 0;
     // cf_set_option("user_runs"): sorted batches take user ranks / counts from
-    // the batch's user runs (StepArgs::user_runs), 0 = one count atomic per pair
-    int user_runs = 1;
+    // the batch's user runs (StepArgs::user_runs); 0 (default) = one returning
+    // count atomic per pair -- the runs measured even at cfg2 (prep_body)
+    int user_runs = 0;
     struct EpochOrder {
         int32_t* keys = nullptr;     // radix-sort path: [2 nnz]
         int32_t* vals = nullptr;     // index form: [nnz] (counting) or [2 nnz] (radix sort)

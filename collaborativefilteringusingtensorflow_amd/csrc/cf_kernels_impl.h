@@ -597,17 +597,20 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
         u = a.occU[p];
         i = a.occV[p];
     }
-    // sorted batches without group users (StepArgs::user_runs): the batch is
-    // in CSR order, so each user's occurrences are one run of consecutive
-    // pairs.  rank = the pair's place in its run, count = the run's length,
-    // stored plainly by the run's first pair -- no returning atomic.  The
-    // wave's first and last runs may continue in the neighbouring waves: they
-    // add their in-wave length with one atomic, whose return is the base of
-    // their ranks (two atomics per wave instead of one per pair; the
-    // neighbours' users come from the adjacent groups by shuffle, so nothing
-    // waits on another load -- a variant that loaded the wave's edge records
-    // to settle those two runs too measured 23 us slower per apply + draw
-    // launch at cfg2, profiles/r06/r06b)
+    // sorted batches without group users (StepArgs::user_runs, cf_set_option
+    // "user_runs", default 0): the batch is in CSR order, so each user's
+    // occurrences are one run of consecutive pairs.  rank = the pair's place
+    // in its run, count = the run's length, added by the run's first pair with
+    // a non-returning atomic; the wave's first and last runs may continue in
+    // the neighbouring waves and add their in-wave length with one returning
+    // atomic, the base of their ranks -- two returning atomics per wave
+    // instead of one per pair (the neighbours' users come from the adjacent
+    // groups by shuffle).  Measured EVEN at cfg2 (apply + draw 139.3 vs 140.2
+    // us same box, profiles/r06/r06e): the returning user atomics are not what
+    // bounds the draw.  Storing the interior runs' counts with plain stores
+    // instead made the fused apply + draw launch 58 us SLOWER (198 vs 140 us;
+    // the draw alone only +3 us, pipeline 0), and loading the wave's edge
+    // records to settle those runs too +23 us.  Kept as an option for that record.
     const bool runs = a.user_runs != 0 && a.sample && a.count_users;   // wave-uniform
     int run_rank = 0, run_len = 0, run_lead = 0, run_base = 0;
     bool run_atomic = false;
@@ -636,17 +639,10 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
 #else
     if (gl == 0) {
 #endif
-#ifndef CF_RUNS_MODE
-#define CF_RUNS_MODE 0   // experiments: 1 = the interior runs' count as a non-returning atomic, 2 = runs unused
-#endif
-        if (runs && CF_RUNS_MODE != 2) {
+        if (runs) {
             if (run_rank == 0) {   // the run's first pair in this wave
                 if (run_atomic) run_base = atomicAdd(&a.cntU[u], run_len);
-#if CF_RUNS_MODE == 1
-                else (void)atomicAdd(&a.cntU[u], run_len);
-#else
-                else a.cntU[u] = run_len;
-#endif
+                else (void)atomicAdd(&a.cntU[u], run_len);   // (a plain store: 58 us slower, above)
             }
         } else if (a.count_users) {
             rk_u = atomicAdd(&a.cntU[u], 1);
@@ -754,7 +750,7 @@ __device__ __forceinline__ void prep_body(const StepArgs& a, int block) {
             if (a.count_users && g >= 0) a.rankU[B + p * G + k] = atomicAdd(&a.cntU[g], 1);
         }
     }
-    if (runs && CF_RUNS_MODE != 2) rk_u = __shfl(run_base, run_lead, kWave) + run_rank;   // every lane: the run's base
+    if (runs) rk_u = __shfl(run_base, run_lead, kWave) + run_rank;   // every lane: the run's base
     if (gl == 0) {
         if (a.sample) {
             a.occU[p] = u;
