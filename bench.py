@@ -620,8 +620,8 @@ def main():
     loss = eng.take_loss()
     log("rank %d: loss accumulated %.4e" % (rank, loss))
 
-    # sorted batches: each epoch's pair order -- inverse
-    # bijection keys + a radix sort by batch -- is computed once per epoch,
+    # sorted batches: each epoch's pair order -- a
+    # counting sort of the pairs by batch (cf_epoch.hip, round 6) -- is computed once per epoch,
     # ahead, on a low-priority stream.  The orders computed inside the timed
     # region (eo_in) are already on its clock; a region shorter than an epoch
     # may meet fewer than its share (steps / batches per epoch).  The missing
@@ -776,8 +776,8 @@ def main():
         "epoch_order": {"ms_per_epoch": eo_ms, "batches_per_epoch": per_epoch,
                         "in_timed_region": eo_in, "charged": eo_missing,
                         "charged_ms_per_step": eo_ms * eo_missing / args.steps,
-                        "def": "sorted batches: one epoch's pair order (inverse-bijection keys + radix sort "
-                               "by batch) is computed per epoch; those inside the timed region are on its "
+                        "def": "sorted batches: one epoch's pair order (a counting sort of the pairs by batch, "
+                               "cf_epoch.hip) is computed per epoch; those inside the timed region are on its "
                                "clock, the rest of the region's share (steps / batches_per_epoch) is charged "
                                "at the standalone time (DESIGN 3.1)"},
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

@@ -266,10 +266,33 @@ __global__ void __launch_bounds__(kBlock) epoch_scatter_kernel(EpochCtx c, const
         }
     }
     __syncthreads();
-    // each bin's run with consecutive lanes
-    for (int L = tid; L < tile_len; L += kBlock) {
-        if (RECS) out_recs[gstage[L]] = pairs[stage[L]];
-        else out_idx[gstage[L]] = stage[L];
+    // each bin's run with consecutive lanes; the records form issues all of a
+    // thread's gathers before its first store (one memory round trip, not
+    // kEpochItems)
+    if (RECS) {
+        int4 r[kEpochItems];
+        int32_t g[kEpochItems];
+#pragma unroll
+        for (int i = 0; i < kEpochItems; ++i) {
+            // past the tile's end (its last, partial tile only): entry 0 again,
+            // an identical second store of the same record -- every load and
+            // store stays unconditional, so the compiler cannot sink each load
+            // into its store's branch and wait for it there (kEpochItems round
+            // trips instead of one, seen in the ISA)
+            const int L = tid + i * kBlock;
+            const int Lc = L < tile_len ? L : 0;
+            g[i] = gstage[Lc];
+            r[i] = pairs[stage[Lc]];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < kEpochItems; ++i) out_recs[g[i]] = r[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < kEpochItems; ++i) {
+            const int L = tid + i * kBlock;
+            if (L < tile_len) out_idx[gstage[L]] = stage[L];
+        }
     }
 }
 
@@ -337,8 +360,10 @@ hipError_t launch_epoch_count(const PermKey& p, int64_t nnz, int B, const int4* 
                        dim3(kBlock), 0, s, c, csum, n_chunks);
     hipLaunchKernelGGL(epoch_tile_offsets_kernel, dim3((unsigned)n_chunks), dim3(kBlock), 0, s, c, cnt, csum);
     // <= 36 KB at kEpochMaxBins bins; 19.5 KB (8 blocks per CU) at cfg2's 96
-    const size_t lds3 = (size_t)(kWavesPerBlock + 1) * c.n_bins * sizeof(int32_t) +
-                        (size_t)(2 * kEpochTile + kWavesPerBlock) * sizeof(int32_t);
+    size_t lds3 = (size_t)(kWavesPerBlock + 1) * c.n_bins * sizeof(int32_t) +
+                  (size_t)(2 * kEpochTile + kWavesPerBlock) * sizeof(int32_t);
+    // (fewer blocks per CU -- LDS padded to 40 / 54 / 80 KB -- measured
+    // slower: records 0.72 / 0.75 / 0.75 vs 0.70 ms, profiles/r06/r06g)
     if (out_recs)
         hipLaunchKernelGGL(epoch_scatter_kernel<true>, grid, dim3(kBlock), lds3, s, c, bins, cnt, pairs, out_recs,
                            nullptr);
