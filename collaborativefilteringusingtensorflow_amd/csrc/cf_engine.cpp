@@ -1556,11 +1556,34 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
     f.variant = e->fused_variant;
     f.item_mask = item_mask;
     hipError_t he = hipMemcpyAsync(d_users, users, (size_t)n * 4, hipMemcpyHostToDevice, e->stream);
+#ifdef CF_FUSED_STAMPS
+    // diagnostic builds: per-wave cycles of each phase of the sweep, summed
+    // over the waves and printed (tools/score_ab.py)
+    const size_t n_st = (size_t)((n + 63) / 64) * 8 * 16;
+    std::vector<unsigned long long> h_st(n_st, 0ull);
+    if (he == hipSuccess) he = hipMalloc(&f.stamps, n_st * sizeof(unsigned long long));
+    if (he == hipSuccess) he = hipMemsetAsync(f.stamps, 0, n_st * sizeof(unsigned long long), e->stream);
+#endif
     if (he == hipSuccess) {
         ProfScope ps(e, CF_K_TOPK);
         he = launch_fused_topk(f, e->stream);
     }
     if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+#ifdef CF_FUSED_STAMPS
+    if (he == hipSuccess) he = hipMemcpy(h_st.data(), f.stamps, n_st * sizeof(unsigned long long), hipMemcpyDefault);
+    if (f.stamps) (void)hipFree(f.stamps);
+    if (he == hipSuccess) {
+        static const char* names[9] = {"stage", "bar1", "mfma", "cand", "bar2", "tile_wait", "store",
+                                       "compact", "bar3"};
+        double tot[16] = {0};
+        for (size_t q = 0; q < n_st; ++q) tot[q & 15] += (double)h_st[q];
+        double all = 0.0;
+        for (int q = 0; q < 9; ++q) all += tot[q];
+        std::fprintf(stderr, "fused stamps: total %.4e wave-cycles; exact-path wave-steps %.0f, compaction wave-steps %.0f\n",
+                     all, tot[9], tot[10]);
+        for (int q = 0; q < 9; ++q) std::fprintf(stderr, "fused stamps: %-14s %.4e  %.3f\n", names[q], tot[q], tot[q] / all);
+    }
+#endif
     if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDefault);
     if (he == hipSuccess && val_out)
         he = hipMemcpy(val_out, d_val, (size_t)n * k * 4, hipMemcpyDefault);

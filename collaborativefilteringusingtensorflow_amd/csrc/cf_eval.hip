@@ -250,6 +250,50 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
     return ((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+#ifndef CF_FUSED_DPP_SORT
+// 1 (round 6): the compaction's bitonic exchanges read lane ^ s through DPP
+// (s <= 8, inside a 16-lane row) and gfx950's permlane16 / permlane32 swaps
+// (s = 16, 32) instead of ds_bpermute round trips through the LDS crossbar,
+// and a list of <= 64 entries is sorted in one register per lane.  Phase
+// stamps of the cfg5 pass (CF_FUSED_STAMPS, profiles/r06/r06s) put the
+// compactions and the waits they cause the block's other waves at ~18 % of
+// the wave cycles; 0: the shuffle form
+#define CF_FUSED_DPP_SORT 0
+#endif
+
+// the value lane ^ s holds (s < 64, a constant after unrolling), all lanes
+// active: DPP quad_perm for s = 1, 2; row_shr / row_shl with bank masks for
+// s = 4, 8 (the partner is in the same 16-lane row); permlane16_swap /
+// permlane32_swap for s = 16, 32 (rows 2r, 2r+1 and the wave's halves swap
+// in one instruction: one result holds the even rows' / lower half's values,
+// the other the odd rows' / upper half's)
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int s) {
+    switch (s) {
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+        case 4: {
+            const int t = __builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xA, false);   // banks 1,3 <- lane-4
+            return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x104, 0xF, 0x5, false);     // banks 0,2 <- lane+4
+        }
+        case 8: {
+            const int t = __builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xC, false);   // banks 2,3 <- lane-8
+            return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x108, 0xF, 0x3, false);     // banks 0,1 <- lane+8
+        }
+        case 16: {
+            const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return (lane_id() & 16) ? r[0] : r[1];
+        }
+        default: {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return (lane_id() & 32) ? r[0] : r[1];
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned long long xor_lane_u64(unsigned long long v, int s) {
+    return ((unsigned long long)xor_lane((uint32_t)(v >> 32), s) << 32) | xor_lane((uint32_t)v, s);
+}
+
 // one wave sorts a user's <= 64 R candidates descending (R registers per
 // lane: entry e = lane + 64 r), keeps the best `keep` (<= 64 R - 64) in place
 // and returns how many it kept; the k-th best becomes the row's threshold
@@ -258,6 +302,65 @@ __device__ int wave_compact(unsigned long long* __restrict__ buf, int* cnt,
                             unsigned long long* thr, int keep, int k) {
     const int lane = lane_id();
     const int n = *cnt;
+#if CF_FUSED_DPP_SORT
+    if (R >= 2 && n <= 64 && keep <= 64) {   // wave-uniform: one register per lane
+        unsigned long long x = lane < n ? buf[lane] : 0ull;
+#pragma unroll
+        for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const unsigned long long y = xor_lane_u64(x, stride);
+                const bool lower = (lane & stride) == 0;
+                const bool desc = (lane & size) == 0;
+                const unsigned long long mx = x > y ? x : y, mn = x > y ? y : x;
+                x = (desc == lower) ? mx : mn;
+            }
+        }
+        const int m = n < keep ? n : keep;
+        if (lane < m) buf[lane] = x;
+        const unsigned long long kth = shfl_u64(x, k - 1);
+        if (lane == 0) {
+            *cnt = m;
+            if (m >= k) *thr = kth;
+        }
+        return m;
+    }
+    if constexpr (R == 2) {
+        unsigned long long x0 = lane < n ? buf[lane] : 0ull;
+        unsigned long long x1 = lane + 64 < n ? buf[lane + 64] : 0ull;
+#pragma unroll
+        for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                if (stride == 64) {  // partner is the lane's other register; size == 128
+                    if (x0 < x1) { const unsigned long long t = x0; x0 = x1; x1 = t; }
+                    continue;
+                }
+                const bool lower = (lane & stride) == 0;
+                {
+                    const unsigned long long y = xor_lane_u64(x0, stride);
+                    const bool desc = (lane & size) == 0;
+                    const unsigned long long mx = x0 > y ? x0 : y, mn = x0 > y ? y : x0;
+                    x0 = (desc == lower) ? mx : mn;
+                }
+                {
+                    const unsigned long long y = xor_lane_u64(x1, stride);
+                    const bool desc = ((lane + 64) & size) == 0;
+                    const unsigned long long mx = x1 > y ? x1 : y, mn = x1 > y ? y : x1;
+                    x1 = (desc == lower) ? mx : mn;
+                }
+            }
+        }
+        const int m = n < keep ? n : keep;
+        if (lane < m) buf[lane] = x0;            // keep <= 64
+        const unsigned long long kth = shfl_u64(x0, k - 1);
+        if (lane == 0) {
+            *cnt = m;
+            if (m >= k) *thr = kth;
+        }
+        return m;
+    }
+#endif
     if constexpr (R == 2) {   // the two-block-per-CU kernel's form (its register budget is tight)
         unsigned long long x0 = lane < n ? buf[lane] : 0ull;
         unsigned long long x1 = lane + 64 < n ? buf[lane + 64] : 0ull;
@@ -368,6 +471,27 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 #ifndef CF_FUSED_BPREFETCH
 #define CF_FUSED_BPREFETCH 0   // 1: read each MFMA group's B operand one group ahead (measured slower: 74 vs 84.5 TF)
 #endif
+#ifndef CF_FUSED_STRICT
+// 1 (round 6): the exact candidate test reads thr[R] only for a score equal
+// to its row's threshold float; 0: every prefilter pass reads it.  (Slots
+// from one LDS atomic per row and half-wave, ballot ranks and readlanes,
+// measured slower: cfg5 86.8 vs 89.5 TFLOP/s, profiles/r06/r06s/r06s7)
+#define CF_FUSED_STRICT 0
+#endif
+#ifndef CF_FUSED_MASK_AHEAD
+// 1 (round 6): the users' threads build the next tile's train masks during
+// this tile's candidate phase (two mask buffers, +512 B of LDS), so the
+// cursor walk no longer holds the other waves at the staging barrier; 0: the
+// masks are built in the staging phase of their own tile
+#define CF_FUSED_MASK_AHEAD 0
+#endif
+#ifndef CF_FUSED_CURSOR2
+// 1 (round 6): the train-row cursor keeps the next TWO items in registers, so
+// consuming one issues the load of the one after without waiting for it;
+// 0: each consumption waits for its dependent load (wave 0 of the block, at
+// nearly every step of a 64-user block), and the block with it at barrier 1
+#define CF_FUSED_CURSOR2 0
+#endif
 #ifndef CF_FUSED_SETPRIO
 // 1 (round 5 experiment): a wave raises its issue priority for its MFMA
 // stream (s_setprio 3) and drops it for the candidate phase, so the SIMD's
@@ -390,7 +514,12 @@ void fused_topk_kernel(FusedTopkArgs a) {
     __shared__ __attribute__((aligned(16))) float Vs[kFusedItems * kFusedMaxD];
     __shared__ unsigned long long buf[NU * CAP];
     __shared__ unsigned long long thr[NU];
-    __shared__ unsigned long long mask[NU];
+    // the train masks: AHEAD keeps two tiles' (the next one is built by the
+    // users' threads during this tile's candidate phase).  BPR only: GBPR's
+    // bias tile and CML's norms leave no room for the second buffer beside
+    // two blocks per CU (81,928 B > 80 KiB)
+    constexpr bool AHEAD = CF_FUSED_MASK_AHEAD && MODEL == BPR;
+    __shared__ unsigned long long mask_buf[AHEAD ? 2 : 1][NU];
     __shared__ int cnt[NU];
     __shared__ float unorm[NU];
     __shared__ float bt[kFusedItems];
@@ -440,6 +569,9 @@ void fused_topk_kernel(FusedTopkArgs a) {
     }
     int64_t cur = 0, end = 0;                // train-row cursor of user `tid` (tid < 64)
     int64_t nxt = INT64_MAX;                 // the train item at the cursor, kept in a register
+#if CF_FUSED_CURSOR2
+    int nxt2 = INT_MAX;                      // the one after it, loaded a consumption ahead
+#endif
     if (tid < NU) {
         thr[tid] = 0ull;
         cnt[tid] = 0;
@@ -448,6 +580,9 @@ void fused_topk_kernel(FusedTopkArgs a) {
             cur = a.indptr[u];
             end = a.indptr[u + 1];
             if (cur < end) nxt = a.indices[cur];
+#if CF_FUSED_CURSOR2
+            if (cur + 1 < end) nxt2 = a.indices[cur + 1];
+#endif
         }
     }
     // the next item tile is loaded into registers during this tile's MFMA and
@@ -479,6 +614,39 @@ void fused_topk_kernel(FusedTopkArgs a) {
         load_tile(0);
         store_tile();
     }
+    // tile jt's train mask of user tid (tid < NU): the caller's item
+    // exclusions (one word per 64-item tile), then the user's train items
+    auto build_mask = [&](int64_t jt, int slot) {
+        unsigned long long m = (MASK && a.item_mask != nullptr) ? a.item_mask[jt >> 6] : 0ull;
+        while (nxt < jt + kFusedItems) {   // sorted row: no load unless an item is consumed
+            m |= 1ull << (int)(nxt - jt);
+            ++cur;
+#if CF_FUSED_CURSOR2
+            // the next item is already in a register; the load issued
+            // here is waited on only at a later consumption
+            nxt = nxt2 == INT_MAX ? INT64_MAX : (int64_t)nxt2;
+            nxt2 = cur + 1 < end ? a.indices[cur + 1] : INT_MAX;
+#else
+            nxt = cur < end ? (int64_t)a.indices[cur] : INT64_MAX;
+#endif
+        }
+        mask_buf[slot][tid] = m;
+    };
+    if (AHEAD && tid < NU) build_mask(0, 0);   // seen after the first barrier
+    int mslot = 0;                                            // mask_buf slot of the current tile
+#ifdef CF_FUSED_STAMPS
+    // diagnostic builds (cf_engine.cpp score_topk_fused): cycles per phase of
+    // the sweep, per wave ([0..8], in the order of the CF_STAMP sites); [9]
+    // steps that took the exact candidate path, [10] steps with a compaction
+    unsigned long long st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_last = __builtin_amdgcn_s_memtime();
+#define CF_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                         st_acc[i] += t_ - st_last; st_last = t_; } while (0)
+#define CF_STAMP_COUNT(i) (st_acc[i] += 1)
+#else
+#define CF_STAMP(i) do {} while (0)
+#define CF_STAMP_COUNT(i) do {} while (0)
+#endif
 
     for (int64_t j0 = 0; j0 < a.n_items; j0 += kFusedItems) {
         // ---- stage the item tile (unless prefetched), its bias, the train mask --
@@ -491,18 +659,10 @@ void fused_topk_kernel(FusedTopkArgs a) {
         }
         if (MODEL == GBPR && tid < kFusedItems)
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
-        if (tid < NU) {
-            // the caller's item exclusions (one word per 64-item tile), then
-            // the user's train items
-            unsigned long long m = (MASK && a.item_mask != nullptr) ? a.item_mask[j0 >> 6] : 0ull;
-            while (nxt < j0 + kFusedItems) {   // sorted row: no load unless an item is consumed
-                m |= 1ull << (int)(nxt - j0);
-                ++cur;
-                nxt = cur < end ? (int64_t)a.indices[cur] : INT64_MAX;
-            }
-            mask[tid] = m;
-        }
+        if (!AHEAD && tid < NU) build_mask(j0, 0);
+        CF_STAMP(0);
         __syncthreads();
+        CF_STAMP(1);
 #ifdef CF_FUSED_EXP_NOLOAD   // attribution: no tile streaming (stale tile)
         const bool more = false;
 #else
@@ -566,11 +726,13 @@ void fused_topk_kernel(FusedTopkArgs a) {
         }
 #endif
         if (CF_FUSED_SETPRIO) __builtin_amdgcn_s_setprio(0);
+        CF_STAMP(2);
         float vnorm = 0.f;
         if (MODEL == CML) vnorm = vsq + __shfl_xor(vsq, 32, 64);   // |v_col|^2
         // ---- candidates above each user's threshold -------------------------------
         const int jl = wc * 32 + c;
         const int64_t J = j0 + jl;
+        const unsigned long long* __restrict__ mask = mask_buf[mslot];
 #ifndef CF_FUSED_EXP_NOCAND
 #if CF_FUSED_FCMP
         if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
@@ -597,6 +759,29 @@ void fused_topk_kernel(FusedTopkArgs a) {
             anyp |= !(s < thf[q]);
         }
         if (__ballot(anyp) != 0ull) {   // wave-uniform
+            CF_STAMP_COUNT(9);
+#if CF_FUSED_STRICT
+            // a score strictly above its row's threshold float has a key above
+            // the threshold key (float_key is order-preserving; thf is the
+            // float of thr[R]'s high word, refreshed with it): only an equal
+            // score (or +-0, NaN) needs thr[R] itself -- one LDS round trip
+            // per active q fewer (mask read, then the slot atomic)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+                float s = acc[q];
+                if (MODEL == GBPR) s += bj_;
+                if (MODEL == CML) s = 2.f * s - vnorm - unorm[R];
+                if (!(s < thf[q]) && R < nu && J < a.n_items && !((mask[R] >> jl) & 1ull)) {
+                    const unsigned long long key = ((unsigned long long)float_key(s) << 32) |
+                                                   (0xFFFFFFFFull - (unsigned long long)J);
+                    if (s > thf[q] || key > thr[R]) {
+                        const int pos = atomicAdd(&cnt[R], 1);
+                        buf[R * CAP + pos] = key;
+                    }
+                }
+            }
+#else
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int R = wr * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -612,6 +797,7 @@ void fused_topk_kernel(FusedTopkArgs a) {
                     }
                 }
             }
+#endif
         }
 #else
         if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
@@ -684,8 +870,21 @@ void fused_topk_kernel(FusedTopkArgs a) {
 #else
         if (acc[0] == 12345.f && J == 7) cnt[0] = 1;   // keep the MFMA result live
 #endif
+        if (AHEAD && tid < NU && j0 + kFusedItems < a.n_items)
+            build_mask(j0 + kFusedItems, mslot ^ 1);   // read after this tile's barriers
+        if (AHEAD) mslot ^= 1;
+        CF_STAMP(3);
         __syncthreads();
+        CF_STAMP(4);
+#ifdef CF_FUSED_STAMPS
+        if (more) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the tile's loads
+        CF_STAMP(5);
+#endif
         if (more) store_tile();   // every wave is past its MFMA reads of this tile
+#ifdef CF_FUSED_STAMPS
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the tile's LDS stores
+        CF_STAMP(6);
+#endif
         // ---- shrink lists that could overflow at the next step ---------------------
         // the wave's 16 rows (wv, wv + 4, ..) are checked with one LDS read and
         // a ballot, not 16 dependent reads
@@ -695,6 +894,7 @@ void fused_topk_kernel(FusedTopkArgs a) {
             unsigned long long need = __ballot(lane < kRowsPerWave && Rl < nu &&
                                                cnt[lane < kRowsPerWave ? Rl : 0] > CAP - kFusedItems);
             if (need != 0ull) {
+                CF_STAMP_COUNT(10);
                 if (lane == 0) atomicAdd(&thr_ver, 1);
                 while (need != 0ull) {
                     const int l = __ffsll((long long)need) - 1;
@@ -704,8 +904,16 @@ void fused_topk_kernel(FusedTopkArgs a) {
                 }
             }
         }
+        CF_STAMP(7);
         __syncthreads();
+        CF_STAMP(8);
     }
+#ifdef CF_FUSED_STAMPS
+    if (a.stamps != nullptr && lane == 0 && NW <= 8) {
+#pragma unroll
+        for (int q = 0; q < 11; ++q) a.stamps[((size_t)blockIdx.x * 8 + wv) * 16 + q] = st_acc[q];
+    }
+#endif
     // ---- final sort and output -------------------------------------------------------
     for (int R = wv; R < nu; R += NW) {
         const int n = wave_compact<SR>(buf + R * CAP, &cnt[R], &thr[R], a.k, a.k);

@@ -388,6 +388,7 @@ struct FusedTopkArgs {
     float* __restrict__ val_out;         // [n_users, k] (nullable)
     int variant;                         // 0: the sequential kernel, 1: software-pipelined (A/B)
     const uint64_t* __restrict__ item_mask;   // as ScoreArgs::item_mask, nullable
+    unsigned long long* stamps;          // -DCF_FUSED_STAMPS diagnostic builds only: [blocks][waves][8]
 };
 
 struct TopkArgs {
