@@ -1573,15 +1573,18 @@ int score_topk_fused(cf_engine* e, const int32_t* users, int n, int k, int exclu
     if (he == hipSuccess) he = hipMemcpy(h_st.data(), f.stamps, n_st * sizeof(unsigned long long), hipMemcpyDefault);
     if (f.stamps) (void)hipFree(f.stamps);
     if (he == hipSuccess) {
-        static const char* names[9] = {"stage", "bar1", "mfma", "cand", "bar2", "tile_wait", "store",
-                                       "compact", "bar3"};
+        static const char* names[14] = {"stage", "bar1", "mfma", "cand_rest", "bar2", "tile_wait", "store",
+                                        "compact", "bar3", "", "", "prefilter", "exact", ""};
         double tot[16] = {0};
         for (size_t q = 0; q < n_st; ++q) tot[q & 15] += (double)h_st[q];
         double all = 0.0;
-        for (int q = 0; q < 9; ++q) all += tot[q];
+        for (int q = 0; q < 14; ++q)
+            if (q != 9 && q != 10) all += tot[q];
         std::fprintf(stderr, "fused stamps: total %.4e wave-cycles; exact-path wave-steps %.0f, compaction wave-steps %.0f\n",
                      all, tot[9], tot[10]);
-        for (int q = 0; q < 9; ++q) std::fprintf(stderr, "fused stamps: %-14s %.4e  %.3f\n", names[q], tot[q], tot[q] / all);
+        for (int q = 0; q < 14; ++q)
+            if (q != 9 && q != 10 && q != 13)
+                std::fprintf(stderr, "fused stamps: %-14s %.4e  %.3f\n", names[q], tot[q], tot[q] / all);
     }
 #endif
     if (he == hipSuccess) he = hipMemcpy(idx_out, d_idx, (size_t)n * k * 4, hipMemcpyDefault);

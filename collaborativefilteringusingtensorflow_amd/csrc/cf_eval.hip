@@ -257,8 +257,9 @@ __device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int
 // and a list of <= 64 entries is sorted in one register per lane.  Phase
 // stamps of the cfg5 pass (CF_FUSED_STAMPS, profiles/r06/r06s) put the
 // compactions and the waits they cause the block's other waves at ~18 % of
-// the wave cycles; 0: the shuffle form
-#define CF_FUSED_DPP_SORT 0
+// the wave cycles; measured cfg5 86.0 -> 89.8 TFLOP/s (same box,
+// tools/score_ab.py); 0: the shuffle form
+#define CF_FUSED_DPP_SORT 1
 #endif
 
 // the value lane ^ s holds (s < 64, a constant after unrolling), all lanes
@@ -473,23 +474,27 @@ __device__ __forceinline__ int vs_off(int r, int kk) {
 #endif
 #ifndef CF_FUSED_STRICT
 // 1 (round 6): the exact candidate test reads thr[R] only for a score equal
-// to its row's threshold float; 0: every prefilter pass reads it.  (Slots
+// to its row's threshold float; 0: every prefilter pass reads it.  Measured
+// even (89.7 vs 89.8 TFLOP/s): the exact path's cost is not that read.  (Slots
 // from one LDS atomic per row and half-wave, ballot ranks and readlanes,
 // measured slower: cfg5 86.8 vs 89.5 TFLOP/s, profiles/r06/r06s/r06s7)
-#define CF_FUSED_STRICT 0
+#define CF_FUSED_STRICT 1
 #endif
 #ifndef CF_FUSED_MASK_AHEAD
 // 1 (round 6): the users' threads build the next tile's train masks during
 // this tile's candidate phase (two mask buffers, +512 B of LDS), so the
-// cursor walk no longer holds the other waves at the staging barrier; 0: the
-// masks are built in the staging phase of their own tile
-#define CF_FUSED_MASK_AHEAD 0
+// cursor walk no longer holds the other waves at the staging barrier, and
+// with the prefetched tile that barrier goes (two per step instead of
+// three): cfg5 89.7 -> 91.2 TFLOP/s; 0: the masks are built in the staging
+// phase of their own tile
+#define CF_FUSED_MASK_AHEAD 1
 #endif
 #ifndef CF_FUSED_CURSOR2
 // 1 (round 6): the train-row cursor keeps the next TWO items in registers, so
 // consuming one issues the load of the one after without waiting for it;
 // 0: each consumption waits for its dependent load (wave 0 of the block, at
-// nearly every step of a 64-user block), and the block with it at barrier 1
+// nearly every step of a 64-user block).  Measured even (86.1 vs 85.9,
+// 90.7 vs 91.2 TFLOP/s with the masks built ahead), so 0
 #define CF_FUSED_CURSOR2 0
 #endif
 #ifndef CF_FUSED_SETPRIO
@@ -632,13 +637,15 @@ void fused_topk_kernel(FusedTopkArgs a) {
         }
         mask_buf[slot][tid] = m;
     };
-    if (AHEAD && tid < NU) build_mask(0, 0);   // seen after the first barrier
+    if (AHEAD && tid < NU) build_mask(0, 0);
+    if (AHEAD && vec) __syncthreads();         // tile 0 and its masks, before the first MFMA
     int mslot = 0;                                            // mask_buf slot of the current tile
 #ifdef CF_FUSED_STAMPS
     // diagnostic builds (cf_engine.cpp score_topk_fused): cycles per phase of
-    // the sweep, per wave ([0..8], in the order of the CF_STAMP sites); [9]
+    // the sweep, per wave ([0..8], in the order of the CF_STAMP sites; the
+    // candidate phase split as [11] prefilter, [12] exact path, [3] the rest); [9]
     // steps that took the exact candidate path, [10] steps with a compaction
-    unsigned long long st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long st_last = __builtin_amdgcn_s_memtime();
 #define CF_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
                          st_acc[i] += t_ - st_last; st_last = t_; } while (0)
@@ -661,7 +668,10 @@ void fused_topk_kernel(FusedTopkArgs a) {
             bt[tid] = (j0 + tid < a.n_items) ? a.b[j0 + tid] : 0.f;
         if (!AHEAD && tid < NU) build_mask(j0, 0);
         CF_STAMP(0);
-        __syncthreads();
+        // AHEAD with the prefetched tile: nothing is staged here (the masks
+        // and the tile were written before the previous step's last barrier),
+        // so that barrier is this step's
+        if (!AHEAD || !vec) __syncthreads();
         CF_STAMP(1);
 #ifdef CF_FUSED_EXP_NOLOAD   // attribution: no tile streaming (stale tile)
         const bool more = false;
@@ -758,6 +768,7 @@ void fused_topk_kernel(FusedTopkArgs a) {
             }
             anyp |= !(s < thf[q]);
         }
+        CF_STAMP(11);
         if (__ballot(anyp) != 0ull) {   // wave-uniform
             CF_STAMP_COUNT(9);
 #if CF_FUSED_STRICT
@@ -799,6 +810,7 @@ void fused_topk_kernel(FusedTopkArgs a) {
             }
 #endif
         }
+        CF_STAMP(12);
 #else
         if (thi_ver != thr_ver) {   // block-uniform (thr_ver changes only between barriers)
             thi_ver = thr_ver;
@@ -911,7 +923,7 @@ void fused_topk_kernel(FusedTopkArgs a) {
 #ifdef CF_FUSED_STAMPS
     if (a.stamps != nullptr && lane == 0 && NW <= 8) {
 #pragma unroll
-        for (int q = 0; q < 11; ++q) a.stamps[((size_t)blockIdx.x * 8 + wv) * 16 + q] = st_acc[q];
+        for (int q = 0; q < 14; ++q) a.stamps[((size_t)blockIdx.x * 8 + wv) * 16 + q] = st_acc[q];
     }
 #endif
     // ---- final sort and output -------------------------------------------------------
