@@ -1545,6 +1545,25 @@ __device__ __forceinline__ bool minor_block(int b, int nmajor, int nminor, int& 
     return hi > lo;
 }
 
+// The same with the minor blocks front-loaded (experiment, CF_APPLY_DRAW_SKEW):
+// the number of minor blocks before block b is F(b) = nminor - floor(nminor
+// (tot - b)^2 / tot^2), whose slope falls from 2 nminor / tot to 0, so the
+// latency-bound draw starts first and the bandwidth-bound apply blocks form
+// the tail.  Needs nminor <= nmajor (slope <= 1: at most one minor block per
+// block id); otherwise the even spread.
+__device__ __forceinline__ bool minor_block_front(int b, int nmajor, int nminor, int& idx) {
+    if (nminor > nmajor) return minor_block(b, nmajor, nminor, idx);
+    const int64_t tot = (int64_t)nmajor + nminor;
+    auto F = [&](int64_t x) {
+        const int64_t r = tot - x;
+        // r^2 nminor <= tot^3 < 2^63 for tot < 2^21
+        return (int64_t)nminor - (r * r * (int64_t)nminor) / (tot * tot);
+    };
+    const int64_t lo = F(b), hi = F((int64_t)b + 1);
+    idx = (int)((hi > lo) ? lo : (int64_t)b - lo);
+    return hi > lo;
+}
+
 // DRAW: the launch also carries the draw blocks of the next step (pipeline
 // 2); without it the draw's registers do not count against the gradient
 template <int MODEL, int EPL, int WT, bool DRAW>
@@ -3098,6 +3117,9 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 #ifndef CF_APPLY_DRAW_TAIL
 #define CF_APPLY_DRAW_TAIL 0
 #endif
+#ifndef CF_APPLY_DRAW_SKEW
+#define CF_APPLY_DRAW_SKEW 0   // 1: the draw blocks front-loaded (minor_block_front; experiment)
+#endif
 // minimum waves per SIMD the pos_sort apply is built for: 7 (72 VGPRs, 12-B
 // spill) measured even-to-slower at cfg2 (round 4, profiles/r04/ab/ab_r04w_occupancy.txt)
 #ifndef CF_APPLY_MIN_WAVES
@@ -3113,7 +3135,8 @@ __global__ __launch_bounds__(kBlock, CF_APPLY_MIN_WAVES) void apply_ps_kernel(Ap
     if (FX && blockIdx.x == 0 && threadIdx.x == 0 && p.hot_n != nullptr) *p.hot_n = 0;
     if constexpr (DRAW && !CF_APPLY_DRAW_TAIL) {
         int idx;
-        if (minor_block(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)) {
+        if (CF_APPLY_DRAW_SKEW ? minor_block_front(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)
+                               : minor_block(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)) {
             prep_any<BPR>(nx, idx);
             return;
         }
