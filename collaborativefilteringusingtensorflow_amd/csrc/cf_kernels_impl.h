@@ -1551,12 +1551,16 @@ __device__ __forceinline__ bool minor_block(int b, int nmajor, int nminor, int& 
 // latency-bound draw starts first and the bandwidth-bound apply blocks form
 // the tail.  Needs nminor <= nmajor (slope <= 1: at most one minor block per
 // block id); otherwise the even spread.
+// BACK: the mirror image, F(b) = floor(nminor b^2 / tot^2): the draw blocks
+// thin at the start and dense at the end (the apply's bandwidth first).
+template <bool BACK = false>
 __device__ __forceinline__ bool minor_block_front(int b, int nmajor, int nminor, int& idx) {
     if (nminor > nmajor) return minor_block(b, nmajor, nminor, idx);
     const int64_t tot = (int64_t)nmajor + nminor;
     auto F = [&](int64_t x) {
+        // x^2 nminor <= tot^3 < 2^63 for tot < 2^21
+        if (BACK) return (x * x * (int64_t)nminor) / (tot * tot);
         const int64_t r = tot - x;
-        // r^2 nminor <= tot^3 < 2^63 for tot < 2^21
         return (int64_t)nminor - (r * r * (int64_t)nminor) / (tot * tot);
     };
     const int64_t lo = F(b), hi = F((int64_t)b + 1);
@@ -3118,7 +3122,10 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 #define CF_APPLY_DRAW_TAIL 0
 #endif
 #ifndef CF_APPLY_DRAW_SKEW
-#define CF_APPLY_DRAW_SKEW 0   // 1: the draw blocks front-loaded (minor_block_front; experiment)
+// 1: the draw blocks front-loaded (minor_block_front): cfg2 apply + draw 141
+// -> 163 us, B = 65,536 0.0699 -> 0.0783 ms/step (same box, r06k), slower;
+// 2: back-loaded; 0: evenly interleaved
+#define CF_APPLY_DRAW_SKEW 0
 #endif
 // minimum waves per SIMD the pos_sort apply is built for: 7 (72 VGPRs, 12-B
 // spill) measured even-to-slower at cfg2 (round 4, profiles/r04/ab/ab_r04w_occupancy.txt)
@@ -3135,8 +3142,10 @@ __global__ __launch_bounds__(kBlock, CF_APPLY_MIN_WAVES) void apply_ps_kernel(Ap
     if (FX && blockIdx.x == 0 && threadIdx.x == 0 && p.hot_n != nullptr) *p.hot_n = 0;
     if constexpr (DRAW && !CF_APPLY_DRAW_TAIL) {
         int idx;
-        if (CF_APPLY_DRAW_SKEW ? minor_block_front(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)
-                               : minor_block(blockIdx.x, nbI + nbW, (int)gridDim.x - nbI - nbW, idx)) {
+        const int nmin = (int)gridDim.x - nbI - nbW;
+        if (CF_APPLY_DRAW_SKEW == 1   ? minor_block_front<false>(blockIdx.x, nbI + nbW, nmin, idx)
+            : CF_APPLY_DRAW_SKEW == 2 ? minor_block_front<true>(blockIdx.x, nbI + nbW, nmin, idx)
+                                      : minor_block(blockIdx.x, nbI + nbW, nmin, idx)) {
             prep_any<BPR>(nx, idx);
             return;
         }
