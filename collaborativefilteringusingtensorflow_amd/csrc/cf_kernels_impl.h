@@ -3124,7 +3124,7 @@ __device__ __forceinline__ void apply_rows_item_block(const ApplyArgs& a, int bl
 #ifndef CF_APPLY_DRAW_SKEW
 // 1: the draw blocks front-loaded (minor_block_front): cfg2 apply + draw 141
 // -> 163 us, B = 65,536 0.0699 -> 0.0783 ms/step (same box, r06k), slower;
-// 2: back-loaded; 0: evenly interleaved
+// 2: back-loaded, 155 vs 140 us (r06k2), slower too; 0: evenly interleaved
 #define CF_APPLY_DRAW_SKEW 0
 #endif
 // minimum waves per SIMD the pos_sort apply is built for: 7 (72 VGPRs, 12-B
